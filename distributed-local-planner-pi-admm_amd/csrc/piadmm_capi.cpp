@@ -1,0 +1,320 @@
+// piadmm_capi.cpp -- C-ABI of libpiadmm (include/piadmm.h): handle, device
+// buffers, scenario upload, step launches and state download.
+//
+// Replaces the reference's per-call CasADi/OSQP instantiation
+// (casadi/main.py:96,146) and its Python loop state (casadi/main.py:52-72).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "piadmm_internal.h"
+
+struct piadmm_ctx {
+  piadmm_config_t cfg{};
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool have_scn = false;
+  int N = 0, E = 0, C = 0, T = 0;
+  std::vector<int> comp_ptr, comp_edge;
+  std::vector<void*> allocs;
+  pd::DevArgs a{};
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(piadmm_ctx* h, int code, const std::string& msg) {
+  if (h) h->err = msg;
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(h, expr)                                                              \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess)                                                            \
+      return fail((h), PIADMM_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename T>
+int dalloc(piadmm_ctx* h, T** p, size_t n) {
+  void* q = nullptr;
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc(&q, n * sizeof(T));
+  if (e != hipSuccess) return fail(h, PIADMM_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+  e = hipMemsetAsync(q, 0, n * sizeof(T), h->stream);
+  if (e != hipSuccess) return fail(h, PIADMM_E_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  h->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return 0;
+}
+
+void free_all(piadmm_ctx* h) {
+  for (void* p : h->allocs) (void)hipFree(p);
+  h->allocs.clear();
+  h->have_scn = false;
+}
+
+int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
+  if (c.n_agents <= 0) return fail(h, PIADMM_E_ARG, "n_agents must be > 0");
+  if (c.H < 3 || c.H > pd::HMAX) return fail(h, PIADMM_E_ARG, "H must be in [3, 32] in this version");
+  if (c.max_outer <= 0) return fail(h, PIADMM_E_ARG, "max_outer must be > 0");
+  if (c.dual_mode != PIADMM_DUAL_PLAIN && c.dual_mode != PIADMM_DUAL_PI)
+    return fail(h, PIADMM_E_ARG, "dual_mode must be 0 (plain) or 1 (PI)");
+  if (!(c.dt > 0) || !(c.L > 0) || !(c.rho > 0) || !(c.Pcost > 0) || c.Pnorm < 0 || c.beta < 0)
+    return fail(h, PIADMM_E_ARG, "dt, L, rho, Pcost must be > 0; Pnorm, beta >= 0");
+  if (c.max_inner <= 0 || c.polish_every <= 0) return fail(h, PIADMM_E_ARG, "max_inner, polish_every must be > 0");
+  if (c.round_decimals > 12) return fail(h, PIADMM_E_ARG, "round_decimals must be <= 12");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t piadmm_abi_version(void) { return PIADMM_ABI_VERSION; }
+
+const char* piadmm_build_info(void) {
+  static char buf[160];
+  std::snprintf(buf, sizeof(buf), "libpiadmm abi=%d arch=gfx950 hip=%d.%d waves/wg=%d hmax=%d", PIADMM_ABI_VERSION,
+                HIP_VERSION_MAJOR, HIP_VERSION_MINOR, pd::NW, pd::HMAX);
+  return buf;
+}
+
+int32_t piadmm_config_size(void) { return (int32_t)sizeof(piadmm_config_t); }
+
+int32_t piadmm_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* piadmm_last_error(piadmm_handle_t h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int32_t piadmm_create(const piadmm_config_t* cfg, piadmm_handle_t* out) {
+  if (!cfg || !out) return fail(nullptr, PIADMM_E_ARG, "null argument");
+  *out = nullptr;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return fail(nullptr, PIADMM_E_NODEV, "no HIP device");
+  if (cfg->device < 0 || cfg->device >= nd) return fail(nullptr, PIADMM_E_ARG, "device ordinal out of range");
+  piadmm_ctx* h = new piadmm_ctx();
+  h->cfg = *cfg;
+  if (h->cfg.admm_rho <= 0) h->cfg.admm_rho = 0.05;
+  if (h->cfg.admm_sigma <= 0) h->cfg.admm_sigma = 1e-6;
+  if (h->cfg.admm_alpha <= 0 || h->cfg.admm_alpha >= 2) h->cfg.admm_alpha = 1.6;
+  if (h->cfg.qp_tol <= 0) h->cfg.qp_tol = 1e-9;
+  if (int rc = check_cfg(h, h->cfg)) {
+    g_err = h->err;
+    delete h;
+    return rc;
+  }
+  hipError_t e = hipSetDevice(cfg->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&h->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&h->ev1);
+  if (e != hipSuccess) {
+    g_err = std::string("HIP init: ") + hipGetErrorString(e);
+    delete h;
+    return PIADMM_E_HIP;
+  }
+  *out = h;
+  return PIADMM_OK;
+}
+
+int32_t piadmm_destroy(piadmm_handle_t h) {
+  if (!h) return PIADMM_OK;
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  free_all(h);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return PIADMM_OK;
+}
+
+int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* xt0, const double* ref,
+                            int32_t T, const int32_t* edges, int32_t n_edges) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!spd || !xt0 || !ref || (n_edges > 0 && !edges)) return fail(h, PIADMM_E_ARG, "null array");
+  const int N = h->cfg.n_agents, H = h->cfg.H;
+  if (T < H + 1) return fail(h, PIADMM_E_ARG, "reference too short: T < H+1");
+  if (n_edges < 0) return fail(h, PIADMM_E_ARG, "n_edges < 0");
+  // components: consecutive pairs (v, v+1) joined by an edge, or single agents
+  std::vector<int> pair_of(N, -1);
+  for (int e = 0; e < n_edges; ++e) {
+    const int v1 = edges[2 * e], v2 = edges[2 * e + 1];
+    if (v1 < 0 || v2 >= N || v1 >= v2) return fail(h, PIADMM_E_ARG, "edge must satisfy 0 <= v1 < v2 < N");
+    if (v2 != v1 + 1)
+      return fail(h, PIADMM_E_ARG, "this version needs every candidate pair to be (v, v+1) (components of <= 2 agents)");
+    if (pair_of[v1] >= 0 || pair_of[v2] >= 0)
+      return fail(h, PIADMM_E_ARG, "an agent belongs to two pairs: components of <= 2 agents only in this version");
+    pair_of[v1] = e;
+    pair_of[v2] = e;
+  }
+  for (int i = 0; i < N; ++i)
+    if (!std::isfinite(spd[i]) || !std::isfinite(xt0[3 * i]) || !std::isfinite(xt0[3 * i + 1]) ||
+        !std::isfinite(xt0[3 * i + 2]))
+      return fail(h, PIADMM_E_ARG, "non-finite speed or state");
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  free_all(h);
+  h->comp_ptr.assign(1, 0);
+  h->comp_edge.clear();
+  std::vector<int> nbr(N, 0);
+  for (int a = 0; a < N;) {
+    const int e = pair_of[a];
+    if (e >= 0) {
+      h->comp_edge.push_back(e);
+      nbr[a] = nbr[a + 1] = 1;
+      a += 2;
+    } else {
+      h->comp_edge.push_back(-1);
+      a += 1;
+    }
+    h->comp_ptr.push_back(a);
+  }
+  h->N = N;
+  h->E = n_edges;
+  h->C = (int)h->comp_edge.size();
+  h->T = T;
+  pd::DevArgs& A = h->a;
+  A = pd::DevArgs{};
+  A.cfg = h->cfg;
+  A.N = N;
+  A.E = n_edges;
+  A.C = h->C;
+  A.T = T;
+  const size_t H1 = H + 1, E = n_edges, C = h->C;
+  double *d_spd, *d_ref;
+  int *d_cp, *d_ce, *d_ed, *d_nb;
+  int rc = 0;
+  rc |= dalloc(h, &d_spd, N);
+  rc |= dalloc(h, &d_ref, (size_t)N * 2 * T);
+  rc |= dalloc(h, &d_cp, C + 1);
+  rc |= dalloc(h, &d_ce, C);
+  rc |= dalloc(h, &d_ed, 2 * E);
+  rc |= dalloc(h, &d_nb, N);
+  rc |= dalloc(h, &A.xt, (size_t)N * 3);
+  rc |= dalloc(h, &A.u, (size_t)N * H);
+  rc |= dalloc(h, &A.pos_old, (size_t)N * 2 * H1);
+  rc |= dalloc(h, &A.hat, E * 4 * H1);
+  rc |= dalloc(h, &A.lam, E * 4 * H1);
+  rc |= dalloc(h, &A.edge_active, E);
+  rc |= dalloc(h, &A.iters, C);
+  rc |= dalloc(h, &A.resid, C * h->cfg.max_outer * 2);
+  rc |= dalloc(h, &A.status, (size_t)N + E);
+  rc |= dalloc(h, &A.Pinv_x, (size_t)N * H * H);
+  rc |= dalloc(h, &A.sc_x, (size_t)N * 4 * pd::HMAX);
+  rc |= dalloc(h, &A.ws_x, (size_t)N * 5 * pd::HMAX);
+  rc |= dalloc(h, &A.lab_x, (size_t)N * 2 * pd::HMAX);
+  rc |= dalloc(h, &A.Pinv_e, E * 4 * H * H);
+  rc |= dalloc(h, &A.PGt, E * 2 * H * H);
+  rc |= dalloc(h, &A.GPG, E * H * H);
+  rc |= dalloc(h, &A.sc_e, E * 8 * pd::HMAX);
+  rc |= dalloc(h, &A.ws_e, E * 12 * pd::HMAX);
+  rc |= dalloc(h, &A.lab_e, E * 5 * pd::HMAX);
+  rc |= dalloc(h, &A.gcoef_e, E * 4);
+  if (rc) return PIADMM_E_HIP;
+  HIPCHK(h, hipMemcpyAsync(d_spd, spd, N * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(d_ref, ref, (size_t)N * 2 * T * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(d_cp, h->comp_ptr.data(), (C + 1) * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(d_ce, h->comp_edge.data(), C * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  if (E) HIPCHK(h, hipMemcpyAsync(d_ed, edges, 2 * E * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(d_nb, nbr.data(), N * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(A.xt, xt0, (size_t)N * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  A.spd = d_spd;
+  A.ref = d_ref;
+  A.comp_ptr = d_cp;
+  A.comp_edge = d_ce;
+  A.edges = d_ed;
+  A.nbr_cnt = d_nb;
+  h->have_scn = true;
+  return PIADMM_OK;
+}
+
+int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
+  if (!h || !xt) return fail(h, PIADMM_E_ARG, "null argument");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  HIPCHK(h, hipMemcpyAsync(h->a.xt, xt, (size_t)h->N * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PIADMM_OK;
+}
+
+static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  if (n < 0 || t0 < 0 || t0 + (n > 0 ? n - 1 : 0) + h->cfg.H + 1 > h->T)
+    return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  for (int i = 0; i < n; ++i)
+    if (pd::launch_mpc_step(h->a, t0 + i, h->stream) != 0)
+      return fail(h, PIADMM_E_HIP, std::string("kernel launch: ") + hipGetErrorString(hipGetLastError()));
+  return PIADMM_OK;
+}
+
+int32_t piadmm_mpc_steps_async(piadmm_handle_t h, int32_t t0, int32_t n_steps) {
+  return enqueue_steps(h, t0, n_steps);
+}
+
+int32_t piadmm_sync(piadmm_handle_t h) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PIADMM_OK;
+}
+
+int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_old, double* hat, double* lam,
+                         uint8_t* edge_active, int32_t* iters) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  const int N = h->N, E = h->E, C = h->C, H = h->cfg.H, H1 = H + 1;
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  hipStream_t s = h->stream;
+  if (xt) HIPCHK(h, hipMemcpyAsync(xt, h->a.xt, (size_t)N * 3 * 8, hipMemcpyDeviceToHost, s));
+  if (u) HIPCHK(h, hipMemcpyAsync(u, h->a.u, (size_t)N * H * 8, hipMemcpyDeviceToHost, s));
+  if (pos_old) HIPCHK(h, hipMemcpyAsync(pos_old, h->a.pos_old, (size_t)N * 2 * H1 * 8, hipMemcpyDeviceToHost, s));
+  if (hat && E) HIPCHK(h, hipMemcpyAsync(hat, h->a.hat, (size_t)E * 4 * H1 * 8, hipMemcpyDeviceToHost, s));
+  if (lam && E) HIPCHK(h, hipMemcpyAsync(lam, h->a.lam, (size_t)E * 4 * H1 * 8, hipMemcpyDeviceToHost, s));
+  if (edge_active && E) HIPCHK(h, hipMemcpyAsync(edge_active, h->a.edge_active, E, hipMemcpyDeviceToHost, s));
+  if (iters) HIPCHK(h, hipMemcpyAsync(iters, h->a.iters, (size_t)C * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  return PIADMM_OK;
+}
+
+int32_t piadmm_mpc_step(piadmm_handle_t h, int32_t t, double* xt_out, double* u_out, double* resid_out,
+                        int32_t* iters_out, int32_t* status_out) {
+  if (int rc = enqueue_steps(h, t, 1)) return rc;
+  hipStream_t s = h->stream;
+  const int N = h->N, E = h->E, C = h->C, H = h->cfg.H;
+  if (xt_out) HIPCHK(h, hipMemcpyAsync(xt_out, h->a.xt, (size_t)N * 3 * 8, hipMemcpyDeviceToHost, s));
+  if (u_out) HIPCHK(h, hipMemcpyAsync(u_out, h->a.u, (size_t)N * H * 8, hipMemcpyDeviceToHost, s));
+  if (resid_out)
+    HIPCHK(h, hipMemcpyAsync(resid_out, h->a.resid, (size_t)C * h->cfg.max_outer * 2 * 8, hipMemcpyDeviceToHost, s));
+  if (iters_out) HIPCHK(h, hipMemcpyAsync(iters_out, h->a.iters, (size_t)C * 4, hipMemcpyDeviceToHost, s));
+  if (status_out) HIPCHK(h, hipMemcpyAsync(status_out, h->a.status, (size_t)(N + E) * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  return PIADMM_OK;
+}
+
+int32_t piadmm_time_steps(piadmm_handle_t h, int32_t t0, int32_t n_steps, float* ms_out) {
+  if (!h || !ms_out) return fail(h, PIADMM_E_ARG, "null argument");
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  if (int rc = enqueue_steps(h, t0, n_steps)) return rc;
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  HIPCHK(h, hipEventSynchronize(h->ev1));
+  HIPCHK(h, hipEventElapsedTime(ms_out, h->ev0, h->ev1));
+  return PIADMM_OK;
+}
+
+int32_t piadmm_n_components(piadmm_handle_t h) { return h && h->have_scn ? h->C : 0; }
+
+}  // extern "C"

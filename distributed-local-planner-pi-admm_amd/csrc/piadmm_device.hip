@@ -1,0 +1,1280 @@
+// piadmm_device.hip -- MI355X (gfx950) kernels of the batched PI-ADMM consensus solver.
+//
+// One workgroup = one connected component of the candidate-pair graph (two
+// agents and their pair in the tiled scenario); one launch = one whole MPC step
+// of the reference loop (casadi/main.py:43-201): seeds, per-step setup of every
+// QP, the outer ADMM loop with device-side termination, and propagation.  The
+// components are independent, so no inter-workgroup communication exists.
+//
+// Wave layout: wave w solves agent w's x-step; wave 0 also owns the pair.
+// Lane k <-> time/variable index k (H <= 32).  All arithmetic is fp64.
+//
+// Per QP the solver is an OSQP-style ADMM in a Ruiz-scaled space (K^-1 staged
+// in LDS) whose iterates feed a primal-dual active-set (PDAS) polish: the
+// reduced KKT system of a guessed active set is solved exactly through the
+// Schur complement S = A_W P^-1 A_W' (Cholesky in LDS) and accepted only when
+// the KKT conditions hold.  So the answer is the exact QP minimiser, not an
+// eps=1e-3 OSQP iterate.  tools/qp_sim.py is the NumPy prototype of this math.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "piadmm_internal.h"
+
+namespace pd {
+
+// ============================================================ wave primitives
+__device__ __forceinline__ int lid() { return (int)__lane_id(); }
+
+// Intra-wave LDS hand-off: LDS ops of one wave execute in order, so only the
+// compiler must be kept from moving memory operations across this point.
+__device__ __forceinline__ void wsync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Broadcast lane k's value (k wave-uniform) through SGPRs.
+__device__ __forceinline__ double rdl(double v, int k) {
+  unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffull), k);
+  int hi = __builtin_amdgcn_readlane((int)(unsigned)(b >> 32), k);
+  unsigned long long r = ((unsigned long long)(unsigned)hi << 32) | (unsigned long long)(unsigned)lo;
+  return __longlong_as_double((long long)r);
+}
+__device__ __forceinline__ int rdli(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+
+__device__ __forceinline__ double shup(double v, int o) {
+  double t = __shfl_up(v, (unsigned)o);
+  return lid() >= o ? t : 0.0;
+}
+__device__ __forceinline__ double shdn(double v, int o) {
+  double t = __shfl_down(v, (unsigned)o);
+  return lid() + o < WAVE ? t : 0.0;
+}
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ double wmax(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
+__device__ __forceinline__ bool wall(bool p) { return __ballot(!p) == 0ull; }
+
+__device__ __forceinline__ double scan_incl(double v) {
+  const int l = lid();
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    double t = __shfl_up(v, (unsigned)o);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ double scan_incl_rev(double v) {
+  const int l = lid();
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    double t = __shfl_down(v, (unsigned)o);
+    if (l + o < WAVE) v += t;
+  }
+  return v;
+}
+// T(t, j) = (t-1-j)+ is the rollout's double integrator (casadi/PI_ADMM_class.py:59-69:
+// theta accumulates u, x/y accumulate theta).  "hinge lane" k holds time t = k+1.
+// T_apply : var lanes u_j        -> hinge lanes (T u)_{k+1} = sum_{j<=k-1} (k-j) u_j
+// Tt_apply: hinge lanes w_k      -> var lanes   sum_{k>=j+1} (k-j) w_k
+__device__ __forceinline__ double T_apply(double u) { return shup(scan_incl(scan_incl(u)), 1); }
+__device__ __forceinline__ double Tt_apply(double w) { return shdn(scan_incl_rev(scan_incl_rev(w)), 1); }
+
+// ============================================================ reference arithmetic
+__device__ __forceinline__ double pow10i(int d) {
+  double f = 1.0;
+  for (int i = 0; i < d; ++i) f *= 10.0;
+  return f;
+}
+// np.around(x, d) = rint(x * 10^d) / 10^d   (casadi/main.py:48-49,103,153)
+__device__ __forceinline__ double around(double x, int d) {
+  if (d < 0) return x;
+  const double f = pow10i(d);
+  return rint(x * f) / f;
+}
+
+// sum_{k=0}^{H} (k-1-i)+ (k-1-j)+ = (T'T)_{ij}, exact in integers.
+__device__ __forceinline__ double TT(int i, int j, int H) {
+  const int a = max(i, j), b = min(i, j);
+  const long long n = H - 1 - a;
+  if (n < 0) return 0.0;
+  const long long d = a - b;
+  const long long s = n * (n + 1) * (2 * n + 1) / 6 + d * n * (n + 1) / 2;
+  return (double)s;
+}
+// (D2'D2)_{ij}, D2 = second difference (H-2) x H  (cost_smooth, PI_ADMM_class.py:123)
+__device__ __forceinline__ double d2c(int d) { return d == 1 ? -2.0 : ((d == 0 || d == 2) ? 1.0 : 0.0); }
+__device__ __forceinline__ double D2D2(int i, int j, int H) {
+  if (abs(i - j) > 2) return 0.0;
+  double s = 0.0;
+  const int r0 = max(max(i, j) - 2, 0), r1 = min(min(i, j), H - 3);
+  for (int r = r0; r <= r1; ++r) s += d2c(i - r) * d2c(j - r);
+  return s;
+}
+
+struct Geo {
+  double x0, y0, th0, s, sn, cs, ax, ay, mm, xdot0, ydot0;
+};
+// Linearised rollout at theta0 (PI_ADMM_class.py:56-69): p = c + M u with
+// M = [ax T; ay T], c_{t+1} = c_t + xdot0*dt.
+__device__ __forceinline__ Geo make_geo(const double* xt3, double s, const piadmm_config_t& c) {
+#pragma clang fp contract(off)
+  Geo g;
+  g.x0 = xt3[0];
+  g.y0 = xt3[1];
+  g.th0 = xt3[2];
+  g.s = s;
+  g.sn = sin(g.th0);
+  g.cs = cos(g.th0);
+  g.ax = (-s * g.sn * c.dt) * (s / c.L * c.dt);
+  g.ay = (s * g.cs * c.dt) * (s / c.L * c.dt);
+  g.mm = g.ax * g.ax + g.ay * g.ay;
+  g.xdot0 = -s * g.sn * g.th0 + (s * g.cs + s * g.th0 * g.sn);
+  g.ydot0 = s * g.cs * g.th0 + (s * g.sn - s * g.th0 * g.cs);
+  return g;
+}
+// c at time lanes t = 0..H (literal sequential accumulation).
+__device__ __forceinline__ void affine_c(const Geo& g, double dt, int H, double& cx, double& cy) {
+#pragma clang fp contract(off)
+  const int l = lid();
+  double ax = g.x0, ay = g.y0;
+  cx = (l == 0) ? ax : 0.0;
+  cy = (l == 0) ? ay : 0.0;
+  for (int t = 0; t < H; ++t) {
+    ax = ax + g.xdot0 * dt;
+    ay = ay + g.ydot0 * dt;
+    if (l == t + 1) {
+      cx = ax;
+      cy = ay;
+    }
+  }
+}
+
+// Numeric rollouts at time lanes (u at var lanes).  Linear: dynamic_update_local
+// numeric branch (PI_ADMM_class.py:56-70).  Nonlinear: dynamic_update_edge
+// numeric branch (:88-105) = MATLAB numeric dynamic_update_local (:312-330).
+__device__ __forceinline__ void rollout(const double* xt3, double s, double u, const piadmm_config_t& c, int H,
+                        bool nonlinear, double& px, double& py, double& pth) {
+#pragma clang fp contract(off)
+  const int l = lid();
+  const double th0 = xt3[2];
+  const double sn0 = sin(th0), cs0 = cos(th0);
+  // theta sequence (sequential, literal order)
+  double th = th0, my_th = (l == 0) ? th0 : 0.0;
+  for (int k = 0; k < H; ++k) {
+    const double uk = rdl(u, k);
+    const double theta_dot = s / c.L * uk;
+    th = th + theta_dot * c.dt;
+    if (l == k + 1) my_th = th;
+  }
+  // per-lane rates at time k = lane
+  double xd, yd;
+  if (nonlinear) {
+    const double sk = sin(my_th), ck = cos(my_th);
+    xd = -s * sk * my_th + (s * ck + s * my_th * sk);
+    yd = s * ck * my_th + (s * sk - s * my_th * ck);
+  } else {
+    xd = -s * sn0 * my_th + (s * cs0 + s * th0 * sn0);
+    yd = s * cs0 * my_th + (s * sn0 - s * th0 * cs0);
+  }
+  double x = xt3[0], y = xt3[1];
+  px = (l == 0) ? x : 0.0;
+  py = (l == 0) ? y : 0.0;
+  for (int k = 0; k < H; ++k) {
+    x = x + rdl(xd, k) * c.dt;
+    y = y + rdl(yd, k) * c.dt;
+    if (l == k + 1) {
+      px = x;
+      py = y;
+    }
+  }
+  pth = my_th;
+  if (l > H) px = py = pth = 0.0;
+}
+
+// ============================================================ in-wave dense kernels
+// In-place Gauss-Jordan inverse of an SPD matrix held in LDS (stride LD), lane = column.
+__device__ __forceinline__ void gj_invert(double* m, int n) {
+  const int l = lid();
+  for (int p = 0; p < n; ++p) {
+    const double colp = (l < n) ? m[l * LD + p] : 0.0;   // a_lp
+    const double ip = 1.0 / rdl(colp, p);
+    const double rpj = (l < n) ? ((l == p) ? ip : m[p * LD + l] * ip) : 0.0;
+    wsync();
+    for (int i = 0; i < n; ++i) {
+      if (i == p) continue;
+      const double aip = rdl(colp, i);
+      if (l < n) {
+        if (l == p) m[i * LD + p] = -aip * ip;
+        else m[i * LD + l] -= aip * rpj;
+      }
+    }
+    if (l < n) m[p * LD + l] = rpj;
+    wsync();
+  }
+}
+
+__device__ __forceinline__ double clamp_norm(double v) {
+  if (!(v > 1e-6)) return 1.0;
+  return v > 1e6 ? 1e6 : v;
+}
+
+// ============================================================ QP solver
+// Generalised QP  min 1/2 x'Px + q'x + sum_r phi_r(a_r'x)  with box rows
+// (indicator of [lo,hi]) and, for the pair, hinge rows beta*max(0, h - a'x).
+template <int NV>
+struct QP {
+  static constexpr int NR = (NV == 1) ? 2 : 5;
+  int H, n;
+  double q[NV];
+  double D[NV];
+  double E[NR];
+  double lo[NR], hi[NR];
+  bool valid[NR];
+  double g1, g2;          // hinge coefficients (pair only)
+  double beta, rho, sigma, alpha, tol;
+  const double* K;        // LDS  n x n  scaled (P_s + sigma I + rho A_s'A_s)^-1
+  const double* Pinv;     // HBM  n x n  unscaled P^-1
+  const double* PGt;      // HBM  H x n  row k = P^-1 G_k'
+  const double* GPG;      // HBM  H x H
+  double* vb;             // per-wave LDS vectors (512 doubles)
+  double* scr;            // per-wave LDS matrix scratch
+  int* ib;                // per-wave LDS ints (128)
+
+  __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
+};
+
+template <int NV>
+__device__ __forceinline__ void A_mul(const QP<NV>& P, const double* x, double* ax) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double xn = shdn(x[v], 1);
+    ax[2 * v] = P.valid[2 * v] ? x[v] : 0.0;
+    ax[2 * v + 1] = P.valid[2 * v + 1] ? xn - x[v] : 0.0;
+  }
+  if constexpr (NV == 2) {
+    const double th = T_apply(P.g1 * x[0] + P.g2 * x[1]);
+    ax[4] = P.valid[4] ? th : 0.0;
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void At_mul(const QP<NV>& P, const double* w, double* out) {
+  const bool in = lid() < P.H;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double wr = P.valid[2 * v + 1] ? w[2 * v + 1] : 0.0;
+    const double wb = P.valid[2 * v] ? w[2 * v] : 0.0;
+    out[v] = wb - wr + shup(wr, 1);
+  }
+  if constexpr (NV == 2) {
+    const double tt = Tt_apply(P.valid[4] ? w[4] : 0.0);
+    out[0] += P.g1 * tt;
+    out[1] += P.g2 * tt;
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    if (!in) out[v] = 0.0;
+}
+
+// y = M r with M (n x n, symmetric) at row-major base (LDS or HBM), r at var lanes.
+template <int NV, typename Ptr>
+__device__ __forceinline__ void gemv_sym(const QP<NV>& P, Ptr M, const double* r, double* y) {
+  const int l = lid();
+  const int H = P.H, n = P.n;
+  if (l < H) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) P.vb[v * H + l] = r[v];
+  }
+  wsync();
+  double acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+  const int lc = (l < H) ? l : 0;
+  for (int j = 0; j < n; ++j) {
+    const double rj = P.vb[j];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] += M[j * n + v * H + lc] * rj;
+  }
+  wsync();
+#pragma unroll
+  for (int v = 0; v < NV; ++v) y[v] = (l < H) ? acc[v] : 0.0;
+}
+
+// prox of phi/rho at v in scaled units for row slot s
+template <int NV>
+__device__ __forceinline__ double prox_s(const QP<NV>& P, int s, double v) {
+  const double e = P.E[s];
+  if (P.hinge(s)) {
+    const double hs = e * P.lo[s];
+    const double thr = (P.beta / e) / P.rho;
+    return v >= hs ? v : (v <= hs - thr ? v + thr : hs);
+  }
+  return fmin(fmax(v, e * P.lo[s]), e * P.hi[s]);
+}
+
+// label from a prox input in scaled units (ADMM state)
+template <int NV>
+__device__ __forceinline__ signed char label_scaled(const QP<NV>& P, int s, double v) {
+  const double e = P.E[s];
+  if (!P.valid[s]) return 0;
+  if (P.hinge(s)) {
+    const double hs = e * P.lo[s];
+    const double thr = (P.beta / e) / P.rho;
+    return v >= hs ? HZERO : (v <= hs - thr ? HLINEAR : HKINK);
+  }
+  return v <= e * P.lo[s] ? LOWER : (v >= e * P.hi[s] ? UPPER : FREE);
+}
+
+template <int NV>
+__device__ __forceinline__ void admm_iter(const QP<NV>& P, double* xs, double* zs, double* ys) {
+  constexpr int NR = QP<NV>::NR;
+  double w[NR], t[NV], rhs[NV], xt[NV], xu[NV], a[NR];
+#pragma unroll
+  for (int s = 0; s < NR; ++s) w[s] = P.valid[s] ? P.E[s] * (P.rho * zs[s] - ys[s]) : 0.0;
+  At_mul(P, w, t);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) rhs[v] = P.sigma * xs[v] - P.D[v] * P.q[v] + P.D[v] * t[v];
+  gemv_sym(P, P.K, rhs, xt);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xu[v] = P.D[v] * xt[v];
+  A_mul(P, xu, a);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xs[v] = P.alpha * xt[v] + (1.0 - P.alpha) * xs[v];
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (!P.valid[s]) {
+      zs[s] = ys[s] = 0.0;
+      continue;
+    }
+    const double zr = P.alpha * (P.E[s] * a[s]) + (1.0 - P.alpha) * zs[s];
+    const double vin = zr + ys[s] / P.rho;
+    const double zn = prox_s(P, s, vin);
+    ys[s] += P.rho * (zr - zn);
+    zs[s] = zn;
+  }
+}
+
+// ---- Schur-complement entry a' P^-1 b for rows given by ids (slot*H + lane).
+// A box/rate row is c0 e_{i0} + c1 e_{i1} (c1 = 0 for a box row); hinge rows use PGt/GPG.
+struct RowT {
+  int i0, i1, hk;
+  double c0, c1;
+};
+template <int NV>
+__device__ __forceinline__ RowT row_terms(const QP<NV>& P, int id) {
+  const int s = id / P.H, k = id - s * P.H;
+  RowT r;
+  if (NV == 2 && s == 4) {
+    r.hk = k;
+    r.i0 = r.i1 = 0;
+    r.c0 = r.c1 = 0.0;
+    return r;
+  }
+  const int base = (s >> 1) * P.H + k;
+  r.hk = -1;
+  if ((s & 1) == 0) {
+    r.i0 = base; r.c0 = 1.0; r.i1 = base; r.c1 = 0.0;
+  } else {
+    r.i0 = base + 1; r.c0 = 1.0; r.i1 = base; r.c1 = -1.0;
+  }
+  return r;
+}
+
+template <int NV>
+__device__ __forceinline__ double s_entry(const QP<NV>& P, int ia, int ibd) {
+  const RowT a = row_terms(P, ia), b = row_terms(P, ibd);
+  const int n = P.n;
+  if (a.hk < 0 && b.hk < 0) {
+    double s = a.c0 * b.c0 * P.Pinv[a.i0 * n + b.i0];
+    if (b.c1 != 0.0) s += a.c0 * b.c1 * P.Pinv[a.i0 * n + b.i1];
+    if (a.c1 != 0.0) {
+      s += a.c1 * b.c0 * P.Pinv[a.i1 * n + b.i0];
+      if (b.c1 != 0.0) s += a.c1 * b.c1 * P.Pinv[a.i1 * n + b.i1];
+    }
+    return s;
+  }
+  if (a.hk < 0) {
+    double s = a.c0 * P.PGt[b.hk * n + a.i0];
+    if (a.c1 != 0.0) s += a.c1 * P.PGt[b.hk * n + a.i1];
+    return s;
+  }
+  if (b.hk < 0) {
+    double s = b.c0 * P.PGt[a.hk * n + b.i0];
+    if (b.c1 != 0.0) s += b.c1 * P.PGt[a.hk * n + b.i1];
+    return s;
+  }
+  return P.GPG[a.hk * P.H + b.hk];
+}
+// (P^-1 a_id) at variable index i
+template <int NV>
+__device__ __forceinline__ double pcol(const QP<NV>& P, int id, int i) {
+  const RowT a = row_terms(P, id);
+  if (a.hk >= 0) return P.PGt[a.hk * P.n + i];
+  double s = a.c0 * P.Pinv[a.i0 * P.n + i];
+  if (a.c1 != 0.0) s += a.c1 * P.Pinv[a.i1 * P.n + i];
+  return s;
+}
+
+// Solve L L' x = b in place (lane a holds b_a, a < m).  L lower in scr, linv = 1/L_aa.
+__device__ __forceinline__ double chol_solve(const double* L, double linv, double b, int m) {
+  const int l = lid();
+  // forward
+  for (int k = 0; k < m; ++k) {
+    const double zk = rdl(b * linv, k);
+    if (l == k) b = zk;
+    if (l > k && l < m) b -= L[l * LD + k] * zk;
+  }
+  // backward with L'
+  for (int k = m - 1; k >= 0; --k) {
+    const double xk = rdl(b * linv, k);
+    if (l == k) b = xk;
+    if (l < k) b -= L[k * LD + l] * xk;
+  }
+  return (l < m) ? b : 0.0;
+}
+
+// One PDAS reduced solve for labels lab; returns false on numerical failure.
+template <int NV>
+__device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char* lab, double* x, double* y) {
+  constexpr int NR = QP<NV>::NR;
+  const int l = lid();
+  const int H = P.H;
+  double* vb_q = P.vb;             // [0,64)   gemv buffer
+  double* vb_b = P.vb + 64;        // [64,128) rhs b of W rows
+  double* vb_lam = P.vb + 128;     // [128,192)
+  double* vb_ax = P.vb + 192;      // [192,512) A x0 by row id (<= 5*32 = 160)
+  (void)vb_q;
+  // q~ = q - beta G'(1_linear)
+  double qt[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) qt[v] = P.q[v];
+  if constexpr (NV == 2) {
+    const double lin = (P.valid[4] && lab[4] == HLINEAR) ? 1.0 : 0.0;
+    const double tt = Tt_apply(lin);
+    if (l < H) {
+      qt[0] -= P.beta * P.g1 * tt;
+      qt[1] -= P.beta * P.g2 * tt;
+    }
+  }
+  double x0[NV];
+  gemv_sym(P, P.Pinv, qt, x0);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) x0[v] = -x0[v];
+  // working set, compacted in slot-major order
+  bool inW[NR];
+  int pos[NR];
+  int m = 0;
+  const unsigned long long ltmask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    inW[s] = P.valid[s] && (P.hinge(s) ? (lab[s] == HKINK) : (lab[s] != FREE));
+    const unsigned long long bm = __ballot(inW[s]);
+    pos[s] = m + __popcll(bm & ltmask);
+    m += __popcll(bm);
+  }
+  double ax0[NR];
+  A_mul(P, x0, ax0);
+  if (m > WAVE) return false;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (l < H) vb_ax[s * H + l] = ax0[s];
+    if (inW[s]) {
+      P.ib[pos[s]] = s * H + l;
+      vb_b[pos[s]] = P.hinge(s) ? P.lo[s] : (lab[s] == LOWER ? P.lo[s] : P.hi[s]);
+    }
+  }
+  wsync();
+  if (m == 0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = x0[v];
+#pragma unroll
+    for (int s = 0; s < NR; ++s) y[s] = (P.hinge(s) && P.valid[s] && lab[s] == HLINEAR) ? -P.beta : 0.0;
+    return true;
+  }
+  const int myid = (l < m) ? P.ib[l] : 0;
+  const double rhs = (l < m) ? (vb_ax[myid] - vb_b[l]) : 0.0;
+  // S (full, symmetric) into scr: lane a = row a
+  double sdiag = 0.0;
+  for (int b = 0; b < m; ++b) {
+    const int idb = P.ib[b];
+    if (l < m) {
+      const double sv = s_entry(P, myid, idb);
+      P.scr[l * LD + b] = sv;
+      if (b == l) sdiag = sv;
+    }
+  }
+  const double dmax = wmax(l < m ? sdiag : 0.0);
+  const double delta = 1e-14 * dmax;
+  wsync();
+  // Cholesky of S + delta I into the lower triangle (upper triangle keeps S)
+  double linv = 0.0;
+  if (l < m) P.scr[l * LD + l] = sdiag + delta;
+  wsync();
+  for (int k = 0; k < m; ++k) {
+    const double v = (l < m) ? P.scr[l * LD + k] : 0.0;
+    const double piv = rdl(v, k);
+    if (!(piv > 0.0) || !isfinite(piv)) return false;
+    const double inv = 1.0 / sqrt(piv);
+    const double lk = v * inv;
+    if (l == k) {
+      P.scr[k * LD + k] = piv * inv;   // sqrt(piv)
+      linv = inv;
+    }
+    if (l > k && l < m) P.scr[l * LD + k] = lk;
+    wsync();
+    for (int j = k + 1; j < m; ++j) {
+      const double ljk = rdl(lk, j);
+      if (l >= j && l < m) P.scr[l * LD + j] -= lk * ljk;
+    }
+    wsync();
+  }
+  double lamv = chol_solve(P.scr, linv, rhs, m);
+  // one step of iterative refinement against the unregularised S
+  {
+    double sl = 0.0;
+    for (int b = 0; b < m; ++b) {
+      const double lb = rdl(lamv, b);
+      if (l < m) {
+        const double sab = (b == l) ? sdiag : (b > l ? P.scr[l * LD + b] : P.scr[b * LD + l]);
+        sl += sab * lb;
+      }
+    }
+    const double r = (l < m) ? rhs - sl : 0.0;
+    lamv += chol_solve(P.scr, linv, r, m);
+  }
+  if (!isfinite(lamv)) return false;
+  // x = x0 - sum_a (P^-1 a_a) lam_a
+  double xv[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xv[v] = x0[v];
+  for (int a = 0; a < m; ++a) {
+    const int ida = P.ib[a];
+    const double la = rdl(lamv, a);
+    if (l < H) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) xv[v] -= pcol(P, ida, v * H + l) * la;
+    }
+  }
+  if (l < m) vb_lam[l] = lamv;
+  wsync();
+#pragma unroll
+  for (int v = 0; v < NV; ++v) x[v] = (l < H) ? xv[v] : 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (inW[s]) y[s] = vb_lam[pos[s]];
+    else if (P.hinge(s) && P.valid[s] && lab[s] == HLINEAR) y[s] = -P.beta;
+    else y[s] = 0.0;
+  }
+  wsync();
+  return true;
+}
+
+// KKT test of (x, y) for labels lab; on failure fills new labels (PDAS update).
+template <int NV>
+__device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* lab, const double* x, const double* y,
+                          signed char* nlab) {
+  constexpr int NR = QP<NV>::NR;
+  double ax[NR];
+  A_mul(P, x, ax);
+  double ym = 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) ym = fmax(ym, fabs(y[s]));
+  ym = wmax(ym);
+  const double ty = P.tol * (1.0 + ym);
+  bool ok = true;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (!P.valid[s]) {
+      nlab[s] = 0;
+      continue;
+    }
+    const double tp = P.tol * (1.0 + fabs(P.lo[s]));
+    const double c = P.rho * P.E[s] * P.E[s];
+    const double wv = ax[s] + y[s] / c;
+    if (P.hinge(s)) {
+      const double h = P.lo[s];
+      if (lab[s] == HZERO) ok &= ax[s] >= h - tp;
+      else if (lab[s] == HLINEAR) ok &= ax[s] <= h + tp;
+      else ok &= (y[s] <= ty) && (y[s] >= -P.beta - ty);
+      nlab[s] = wv >= h ? HZERO : (wv <= h - P.beta / c ? HLINEAR : HKINK);
+    } else {
+      if (lab[s] == FREE) ok &= (ax[s] >= P.lo[s] - tp) && (ax[s] <= P.hi[s] + tp);
+      else if (lab[s] == LOWER) ok &= y[s] <= ty;
+      else ok &= y[s] >= -ty;
+      nlab[s] = wv <= P.lo[s] ? LOWER : (wv >= P.hi[s] ? UPPER : FREE);
+    }
+    ok &= isfinite(x[0]) && isfinite(y[s]);
+  }
+  return wall(ok);
+}
+
+template <int NV>
+__device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y) {
+  constexpr int NR = QP<NV>::NR;
+  signed char nl[NR];
+  for (int it = 0; it < PDAS_STEPS; ++it) {
+    if (!reduced_solve(P, lab, x, y)) return false;
+    if (kkt_check(P, lab, x, y, nl)) return true;
+    bool same = true;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) same &= (nl[s] == lab[s]);
+    if (wall(same)) return false;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) lab[s] = nl[s];
+  }
+  return false;
+}
+
+// Solve one QP.  (xs, zs, ys) is the warm ADMM state (scaled), lab the warm labels.
+// Returns PIADMM_QP_* flags; x_out = unscaled minimiser.
+template <int NV>
+__device__ __forceinline__ int qp_solve(const QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
+                        bool warm_lab, int max_inner, int polish_every, double* x_out) {
+  constexpr int NR = QP<NV>::NR;
+  double x[NV], y[NR];
+  bool ok = false;
+  if (warm_lab) ok = pdas(P, lab, x, y);
+  for (int it = 1; !ok && it <= max_inner; ++it) {
+    admm_iter(P, xs, zs, ys);
+    const bool try_polish = (it % polish_every == 0) && (it <= 20 * polish_every || it % (10 * polish_every) == 0);
+    if (try_polish) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) lab[s] = label_scaled(P, s, zs[s] + ys[s] / P.rho);
+      ok = pdas(P, lab, x, y);
+    }
+  }
+  int st = PIADMM_QP_OK;
+  if (ok) {
+    // warm ADMM state at the exact optimum
+    double ax[NR];
+    A_mul(P, x, ax);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xs[v] = (P.D[v] != 0.0) ? x[v] / P.D[v] : 0.0;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      zs[s] = P.valid[s] ? P.E[s] * ax[s] : 0.0;
+      ys[s] = P.valid[s] ? y[s] / P.E[s] : 0.0;
+    }
+  } else {
+    st |= PIADMM_QP_INEXACT;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = P.D[v] * xs[v];
+#pragma unroll
+    for (int s = 0; s < NR; ++s) lab[s] = label_scaled(P, s, zs[s] + ys[s] / P.rho);
+  }
+  bool fin = true;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    x_out[v] = (lid() < P.H) ? x[v] : 0.0;
+    fin &= isfinite(x_out[v]);
+  }
+  if (!wall(fin)) st |= PIADMM_QP_NAN;
+  return st;
+}
+
+// ============================================================ per-step setup
+struct WaveMem {
+  double* scr;
+  double* vb;
+  int* ib;
+};
+
+// x-step QP of agent a (cost_function_primal, PI_ADMM_class.py:114-135):
+// P = (2 Pnorm + rho |N|) M'M + 2 D2'D2 + 2 Pcost I;  A = [I; D1].
+__device__ __forceinline__ double xP(const Geo& g, double coefAL, double Pcost, int i, int j, int H) {
+  return coefAL * g.mm * TT(i, j, H) + 2.0 * D2D2(i, j, H) + (i == j ? 2.0 * Pcost : 0.0);
+}
+
+__device__ __forceinline__ void setup_agent(const DevArgs& A, int a, int ai, double* Kx_lds, const WaveMem& wm) {
+  const piadmm_config_t& c = A.cfg;
+  const int H = c.H, l = lid();
+  const Geo g = make_geo(A.xt + 3 * a, A.spd[a], c);
+  const double coefAL = 2.0 * c.Pnorm + c.rho * (double)A.nbr_cnt[a];
+  const bool in = l < H;
+  // Ruiz equilibration of [P A'; A 0] (OSQP-style)
+  double D = in ? 1.0 : 0.0, Eb = in ? 1.0 : 0.0, Er = (l < H - 1) ? 1.0 : 0.0;
+  for (int it = 0; it < RUIZ_ITERS; ++it) {
+    double cn = 0.0;
+    for (int i = 0; i < H; ++i) {
+      const double Di = rdl(D, i);
+      if (in) cn = fmax(cn, fabs(Di * xP(g, coefAL, c.Pcost, i, l, H) * D));
+    }
+    const double Erm = shup(Er, 1);
+    cn = fmax(cn, fmax(Eb * D, fmax(Er * D, Erm * D)));
+    const double rb = Eb * D;
+    const double rr = Er * fmax(D, shdn(D, 1));
+    if (in) {
+      D *= 1.0 / sqrt(clamp_norm(cn));
+      Eb *= 1.0 / sqrt(clamp_norm(rb));
+    }
+    if (l < H - 1) Er *= 1.0 / sqrt(clamp_norm(rr));
+  }
+  // K_s = D P D + sigma I + rho A_s'A_s  (lane = column j)
+  const double rho = c.admm_rho, sig = c.admm_sigma;
+  for (int i = 0; i < H; ++i) {
+    const double Di = rdl(D, i), Ebi = rdl(Eb, i), Eri = rdl(Er, i);
+    const double Erim = (i >= 1) ? rdl(Er, i - 1) : 0.0;
+    if (in) {
+      double v = Di * xP(g, coefAL, c.Pcost, i, l, H) * D;
+      double ata = 0.0;
+      if (i == l) ata = Ebi * Ebi + Eri * Eri + Erim * Erim;
+      else if (l == i + 1) ata = -Eri * Eri;
+      else if (l == i - 1) ata = -Erim * Erim;
+      v += rho * Di * D * ata + (i == l ? sig : 0.0);
+      wm.scr[i * LD + l] = v;
+    }
+  }
+  wsync();
+  gj_invert(wm.scr, H);
+  for (int i = 0; i < H; ++i)
+    if (in) Kx_lds[i * H + l] = wm.scr[i * LD + l];
+  wsync();
+  // P^-1 (unscaled) for the polish
+  for (int i = 0; i < H; ++i)
+    if (in) wm.scr[i * LD + l] = xP(g, coefAL, c.Pcost, i, l, H);
+  wsync();
+  gj_invert(wm.scr, H);
+  double* Pi = A.Pinv_x + (size_t)a * H * H;
+  for (int i = 0; i < H; ++i)
+    if (in) Pi[i * H + l] = wm.scr[i * LD + l];
+  double* sc = A.sc_x + (size_t)a * 4 * HMAX;
+  if (l < HMAX) {
+    sc[0 * HMAX + l] = D;
+    sc[1 * HMAX + l] = Eb;
+    sc[2 * HMAX + l] = Er;
+  }
+  wsync();
+}
+
+// Pair (z-step) QP of cost_function_edge (PI_ADMM_class.py:145-169), heading frozen
+// at xt (MATLAB symbolic dynamic_update_edge, ADMM_CVX_..._PI_antiwindup.m:378-397).
+// Variables [uh_1; uh_2]; P = blockdiag(rho M_v'M_v + 2 Pcost I); hinge rows
+// G_k = [g1 T(k+1,.), g2 T(k+1,.)],  h_k = D^2 + |dbar|^2 - 2 dbar'(c2 - c1)_{k+1}.
+__device__ __forceinline__ double eP(double mmv, double rho, double Pcost, int i, int j, int H) {
+  return rho * mmv * TT(i, j, H) + (i == j ? 2.0 * Pcost : 0.0);
+}
+
+__device__ __forceinline__ void setup_pair(const DevArgs& A, int e, int a1, const double* seeds, double* Ke_lds,
+                           const WaveMem& wm) {
+  const piadmm_config_t& c = A.cfg;
+  const int H = c.H, n = 2 * H, l = lid();
+  const bool in = l < H;
+  const int a2 = a1 + 1;
+  const Geo g1 = make_geo(A.xt + 3 * a1, A.spd[a1], c);
+  const Geo g2 = make_geo(A.xt + 3 * a2, A.spd[a2], c);
+  double c1x, c1y, c2x, c2y;
+  affine_c(g1, c.dt, H, c1x, c1y);
+  affine_c(g2, c.dt, H, c2x, c2y);
+  const double dbx = seeds[2] - seeds[0], dby = seeds[3] - seeds[1];
+  const double dd = dbx * dbx + dby * dby;
+  const double gg1 = -2.0 * (dbx * g1.ax + dby * g1.ay);
+  const double gg2 = 2.0 * (dbx * g2.ax + dby * g2.ay);
+  const double Dsq = c.dis_thres * c.dis_thres;
+  const double h_time = Dsq + dd - 2.0 * (dbx * (c2x - c1x) + dby * (c2y - c1y));
+  const double h0 = shdn(h_time, 1);                 // hinge lane k <-> time k+1
+  const bool hv = (l >= 1) && in && (gg1 != 0.0 || gg2 != 0.0);
+
+  // ---- P_v^-1 blocks, PGt = P^-1 G', GPG = G P^-1 G'  (PGt staged in Ke region)
+  double* PGt_l = Ke_lds;          // H x n (temporarily)
+  double* Pi = A.Pinv_e + (size_t)e * n * n;
+  for (int v = 0; v < 2; ++v) {
+    const double mmv = v == 0 ? g1.mm : g2.mm;
+    const double gv = v == 0 ? gg1 : gg2;
+    for (int i = 0; i < H; ++i)
+      if (in) wm.scr[i * LD + l] = eP(mmv, c.rho, c.Pcost, i, l, H);
+    wsync();
+    gj_invert(wm.scr, H);
+    for (int i = 0; i < H; ++i) {
+      if (in) {
+        Pi[(v * H + i) * n + v * H + l] = wm.scr[i * LD + l];
+        Pi[(v * H + i) * n + (1 - v) * H + l] = 0.0;
+      }
+    }
+    // lane i: Y_k = sum_{j<=k-1} (k-j) Pinv_v[i][j]
+    double acc1 = 0.0, Y = 0.0;
+    for (int k = 0; k < H; ++k) {
+      if (in) PGt_l[k * n + v * H + l] = gv * Y;
+      if (in) acc1 += wm.scr[l * LD + k];
+      Y += acc1;
+    }
+    wsync();
+  }
+  // GPG[a][b] = sum_i G_a[i] PGt[b][i]; lane b
+  {
+    double* Gg = A.GPG + (size_t)e * H * H;
+    double* Pg = A.PGt + (size_t)e * H * n;
+    const int b = in ? l : 0;
+    double B = 0.0, Z = 0.0;
+    for (int a = 0; a < H; ++a) {
+      if (in) Gg[a * H + l] = Z;
+      const double wa = gg1 * PGt_l[b * n + a] + gg2 * PGt_l[b * n + H + a];
+      B += wa;
+      Z += B;
+    }
+    for (int k = 0; k < H; ++k) {
+      Pg[k * n + l] = PGt_l[k * n + l];
+      if (l + 64 < n) Pg[k * n + l + 64] = PGt_l[k * n + l + 64];
+    }
+    wsync();
+  }
+  // ---- Ruiz equilibration
+  double D1 = in ? 1.0 : 0.0, D2 = D1;
+  double Eb1 = D1, Eb2 = D1, Er1 = (l < H - 1) ? 1.0 : 0.0, Er2 = Er1, Eh = hv ? 1.0 : 0.0;
+  const double ag1 = fabs(gg1), ag2 = fabs(gg2);
+  for (int it = 0; it < RUIZ_ITERS; ++it) {
+    double cn1 = 0.0, cn2 = 0.0, rh = 0.0;
+    for (int i = 0; i < H; ++i) {
+      const double D1i = rdl(D1, i), D2i = rdl(D2, i), Ehi = rdl(Eh, i);
+      if (in) {
+        cn1 = fmax(cn1, fabs(D1i * eP(g1.mm, c.rho, c.Pcost, i, l, H) * D1));
+        cn2 = fmax(cn2, fabs(D2i * eP(g2.mm, c.rho, c.Pcost, i, l, H) * D2));
+        // hinge row i (time i+1) has entry g_v (i - j)+ on variable j
+        if (i > l) {
+          cn1 = fmax(cn1, Ehi * ag1 * (double)(i - l) * D1);
+          cn2 = fmax(cn2, Ehi * ag2 * (double)(i - l) * D2);
+        }
+        // hinge row at this lane: entries on variables j < l
+        if (i < l) rh = fmax(rh, fmax(ag1 * (double)(l - i) * D1i, ag2 * (double)(l - i) * D2i));
+      }
+    }
+    cn1 = fmax(cn1, fmax(Eb1 * D1, fmax(Er1 * D1, shup(Er1, 1) * D1)));
+    cn2 = fmax(cn2, fmax(Eb2 * D2, fmax(Er2 * D2, shup(Er2, 1) * D2)));
+    const double rb1 = Eb1 * D1, rb2 = Eb2 * D2;
+    const double rr1 = Er1 * fmax(D1, shdn(D1, 1)), rr2 = Er2 * fmax(D2, shdn(D2, 1));
+    rh *= Eh;
+    if (in) {
+      D1 *= 1.0 / sqrt(clamp_norm(cn1));
+      D2 *= 1.0 / sqrt(clamp_norm(cn2));
+      Eb1 *= 1.0 / sqrt(clamp_norm(rb1));
+      Eb2 *= 1.0 / sqrt(clamp_norm(rb2));
+    }
+    if (l < H - 1) {
+      Er1 *= 1.0 / sqrt(clamp_norm(rr1));
+      Er2 *= 1.0 / sqrt(clamp_norm(rr2));
+    }
+    if (hv) Eh *= 1.0 / sqrt(clamp_norm(rh));
+  }
+  // ---- K_s (n x n), lane = column cidx
+  const double rho = c.admm_rho, sig = c.admm_sigma;
+  {
+    const int vc = (l < H) ? 0 : 1;
+    const int jc = (l < H) ? l : l - H;
+    const bool incol = l < n;
+    const int srcl = (jc < H) ? jc : 0;
+    const double D1s = __shfl(D1, srcl), D2s = __shfl(D2, srcl);
+    const double Dc = vc == 0 ? D1s : D2s;
+    const double gc = vc == 0 ? gg1 : gg2;
+    const double mmc = vc == 0 ? g1.mm : g2.mm;
+    const double Eh2 = Eh * Eh;
+    for (int r = 0; r < n; ++r) {
+      const int vr = r / H, ir = r - vr * H;
+      const double Dr = vr == 0 ? rdl(D1, ir) : rdl(D2, ir);
+      const double Ebr = vr == 0 ? rdl(Eb1, ir) : rdl(Eb2, ir);
+      const double Err = vr == 0 ? rdl(Er1, ir) : rdl(Er2, ir);
+      const double Errm = (ir >= 1) ? (vr == 0 ? rdl(Er1, ir - 1) : rdl(Er2, ir - 1)) : 0.0;
+      const double gr = vr == 0 ? gg1 : gg2;
+      // hinge part: sum_k Eh_k^2 (k - ir)+ (k - jc)+
+      double hs = 0.0;
+      for (int k = 1; k < H; ++k) {
+        const double e2 = rdl(Eh2, k);
+        if (k > ir && k > jc) hs += e2 * (double)(k - ir) * (double)(k - jc);
+      }
+      if (incol) {
+        double v = 0.0;
+        double ata = gr * gc * hs;
+        if (vr == vc) {
+          v = Dr * eP(mmc, c.rho, c.Pcost, ir, jc, H) * Dc;
+          if (ir == jc) ata += Ebr * Ebr + Err * Err + Errm * Errm;
+          else if (jc == ir + 1) ata += -Err * Err;
+          else if (jc == ir - 1) ata += -Errm * Errm;
+        }
+        v += rho * Dr * Dc * ata + (r == l ? sig : 0.0);
+        wm.scr[r * LD + l] = v;
+      }
+    }
+    wsync();
+    gj_invert(wm.scr, n);
+    for (int r = 0; r < n; ++r)
+      if (incol) Ke_lds[r * n + l] = wm.scr[r * LD + l];
+    wsync();
+  }
+  double* sc = A.sc_e + (size_t)e * 8 * HMAX;
+  if (l < HMAX) {
+    sc[0 * HMAX + l] = D1;
+    sc[1 * HMAX + l] = D2;
+    sc[2 * HMAX + l] = Eb1;
+    sc[3 * HMAX + l] = Er1;
+    sc[4 * HMAX + l] = Eb2;
+    sc[5 * HMAX + l] = Er2;
+    sc[6 * HMAX + l] = Eh;
+    sc[7 * HMAX + l] = hv ? h0 : 0.0;
+  }
+  if (l == 0) {
+    A.gcoef_e[4 * e + 0] = gg1;
+    A.gcoef_e[4 * e + 1] = gg2;
+  }
+  wsync();
+}
+
+// ============================================================ the MPC-step kernel
+struct CompLds {
+  double *pos, *xt, *seed, *u, *hat, *lam, *S, *D, *last, *sc;
+};
+
+__global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
+  extern __shared__ double lds[];
+  __shared__ int s_int[NW * 128];
+  const piadmm_config_t& c = A.cfg;
+  const int H = c.H, H1 = H + 1;
+  const int ci = blockIdx.x;
+  const int w = threadIdx.x >> 6, l = lid();
+  const int a0 = A.comp_ptr[ci];
+  const int na = A.comp_ptr[ci + 1] - a0;
+  const int e = A.comp_edge[ci];
+
+  double* Kx = lds;
+  double* Ke = Kx + 2 * H * H;
+  double* scr_all = Ke + 4 * H * H;
+  double* vec_all = scr_all + NW * 64 * LD;
+  CompLds S;
+  S.pos = vec_all + NW * 512;
+  S.xt = S.pos + 4 * H1;
+  S.seed = S.xt + 6;
+  S.u = S.seed + 4;
+  S.hat = S.u + 2 * H;
+  S.lam = S.hat + 4 * H1;
+  S.S = S.lam + 4 * H1;
+  S.D = S.S + 4 * H1;
+  S.last = S.D + 4 * H1;
+  S.sc = S.last + 4 * H1;
+  WaveMem wm{scr_all + w * 64 * LD, vec_all + w * 512, s_int + w * 128};
+
+  // ---- seeds (casadi/main.py:48-49) and zero per-step state (:52-63)
+  if ((int)threadIdx.x < na) {
+    const int a = a0 + threadIdx.x;
+    const double x = A.xt[3 * a], y = A.xt[3 * a + 1], th = A.xt[3 * a + 2], s = A.spd[a];
+    S.xt[3 * threadIdx.x + 0] = x;
+    S.xt[3 * threadIdx.x + 1] = y;
+    S.xt[3 * threadIdx.x + 2] = th;
+    S.seed[2 * threadIdx.x + 0] = around(x + c.dt * s * cos(th), c.round_decimals);
+    S.seed[2 * threadIdx.x + 1] = around(y + c.dt * s * sin(th), c.round_decimals);
+  }
+  for (int i = threadIdx.x; i < 4 * H1 * 6 + 2 * H; i += blockDim.x) {
+    // pos, hat, lam, S, D, last are contiguous with u in between: clear pos and hat..last
+    if (i < 4 * H1) S.pos[i] = 0.0;
+    else if (i < 4 * H1 + 20 * H1) S.hat[i - 4 * H1] = 0.0;
+  }
+  for (int i = threadIdx.x; i < 32; i += blockDim.x) S.sc[i] = 0.0;
+  __syncthreads();
+
+  // ---- per-step QP setup
+  if (w < na) setup_agent(A, a0 + w, w, Kx + w * H * H, wm);
+  if (w == 0 && e >= 0) setup_pair(A, e, a0, S.seed, Ke, wm);
+  __syncthreads();
+
+  // ---- QP descriptors (registers of the owning wave, live for the whole step)
+  QP<1> qx;
+  double xs_x[1] = {0.0}, zs_x[2] = {0.0, 0.0}, ys_x[2] = {0.0, 0.0};
+  signed char lab_x[2] = {0, 0};
+  bool warm_x = false;
+  int status_x = 0;
+  int nnb = 0;
+  Geo gx;
+  if (w < na) {
+    const int a = a0 + w;
+    const double* sc = A.sc_x + (size_t)a * 4 * HMAX;
+    const int li = l < HMAX ? l : 0;
+    qx.H = H;
+    qx.n = H;
+    qx.D[0] = (l < H) ? sc[li] : 0.0;
+    qx.E[0] = (l < H) ? sc[HMAX + li] : 0.0;
+    qx.E[1] = (l < H - 1) ? sc[2 * HMAX + li] : 0.0;
+    qx.lo[0] = -c.u_max;
+    qx.hi[0] = c.u_max;
+    qx.lo[1] = -c.du_max;
+    qx.hi[1] = c.du_max;
+    qx.valid[0] = l < H;
+    qx.valid[1] = l < H - 1;
+    qx.g1 = qx.g2 = 0.0;
+    qx.beta = 0.0;
+    qx.rho = c.admm_rho;
+    qx.sigma = c.admm_sigma;
+    qx.alpha = c.admm_alpha;
+    qx.tol = c.qp_tol;
+    qx.K = Kx + w * H * H;
+    qx.Pinv = A.Pinv_x + (size_t)a * H * H;
+    qx.PGt = nullptr;
+    qx.GPG = nullptr;
+    qx.vb = wm.vb;
+    qx.scr = wm.scr;
+    qx.ib = wm.ib;
+    nnb = A.nbr_cnt[a];
+    gx = make_geo(S.xt + 3 * w, A.spd[a], c);
+  }
+  QP<2> qe;
+  double xs_e[2] = {0.0, 0.0}, zs_e[5] = {0, 0, 0, 0, 0}, ys_e[5] = {0, 0, 0, 0, 0};
+  signed char lab_e[5] = {0, 0, 0, 0, 0};
+  bool warm_e = false;
+  int status_e = 0;
+  Geo ge1, ge2;
+  if (w == 0 && e >= 0) {
+    const double* sc = A.sc_e + (size_t)e * 8 * HMAX;
+    const int li = l < HMAX ? l : 0;
+    const bool in = l < H;
+    qe.H = H;
+    qe.n = 2 * H;
+    qe.D[0] = in ? sc[0 * HMAX + li] : 0.0;
+    qe.D[1] = in ? sc[1 * HMAX + li] : 0.0;
+    qe.E[0] = in ? sc[2 * HMAX + li] : 0.0;
+    qe.E[1] = (l < H - 1) ? sc[3 * HMAX + li] : 0.0;
+    qe.E[2] = in ? sc[4 * HMAX + li] : 0.0;
+    qe.E[3] = (l < H - 1) ? sc[5 * HMAX + li] : 0.0;
+    qe.E[4] = in ? sc[6 * HMAX + li] : 0.0;
+    qe.lo[0] = qe.lo[2] = -c.u_max;
+    qe.hi[0] = qe.hi[2] = c.u_max;
+    qe.lo[1] = qe.lo[3] = -c.du_max;
+    qe.hi[1] = qe.hi[3] = c.du_max;
+    qe.lo[4] = in ? sc[7 * HMAX + li] : 0.0;
+    qe.hi[4] = INFINITY;
+    qe.valid[0] = qe.valid[2] = in;
+    qe.valid[1] = qe.valid[3] = l < H - 1;
+    qe.valid[4] = in && qe.E[4] != 0.0;
+    qe.g1 = A.gcoef_e[4 * e + 0];
+    qe.g2 = A.gcoef_e[4 * e + 1];
+    qe.beta = c.beta;
+    qe.rho = c.admm_rho;
+    qe.sigma = c.admm_sigma;
+    qe.alpha = c.admm_alpha;
+    qe.tol = c.qp_tol;
+    qe.K = Ke;
+    qe.Pinv = A.Pinv_e + (size_t)e * 4 * H * H;
+    qe.PGt = A.PGt + (size_t)e * 2 * H * H;
+    qe.GPG = A.GPG + (size_t)e * H * H;
+    qe.vb = wm.vb;
+    qe.scr = wm.scr;
+    qe.ib = wm.ib;
+    ge1 = make_geo(S.xt + 0, A.spd[a0], c);
+    ge2 = make_geo(S.xt + 3, A.spd[a0 + 1], c);
+  }
+
+  const bool nonlin_pos = c.pos_model != 0;
+  const double thr = c.collide_sq_thres ? c.dis_thres * c.dis_thres : c.dis_thres;
+  int flag = 0, aliased = 0, iters = 0;
+  bool act = false;
+  double dis_chk = NAN;
+  double* resid = A.resid + (size_t)ci * c.max_outer * 2;
+
+  for (int it = 0; it < c.max_outer; ++it) {
+    iters = it + 1;
+    // -------- x-step: every agent of the component (casadi/main.py:81-106)
+    if (w < na) {
+      const int a = a0 + w;
+      double cx, cy;
+      affine_c(gx, c.dt, H, cx, cy);
+      const bool tl = l <= H;
+      const double* rp = A.ref + (size_t)a * 2 * A.T;
+      const double rx = tl ? rp[t + l] : 0.0;
+      const double ry = tl ? rp[A.T + t + l] : 0.0;
+      double vx = 2.0 * c.Pnorm * (cx - rx), vy = 2.0 * c.Pnorm * (cy - ry);
+      if (nnb > 0 && e >= 0 && tl) {
+        const int d = w;   // agent local 0 owns hat_{v1 v2} (dir 0), agent 1 dir 1
+        vx = vx + c.rho * (cx - S.hat[(d * 2 + 0) * H1 + l] + S.lam[(d * 2 + 0) * H1 + l]);
+        vy = vy + c.rho * (cy - S.hat[(d * 2 + 1) * H1 + l] + S.lam[(d * 2 + 1) * H1 + l]);
+      }
+      const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
+      const double qv = Tt_apply(shdn(wt, 1));
+      qx.q[0] = (l < H) ? qv : 0.0;
+      double ustar[1];
+      status_x |= qp_solve(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, ustar);
+      warm_x = true;
+      const double u = around(ustar[0], c.round_decimals);
+      double px, py, pth;
+      rollout(S.xt + 3 * w, A.spd[a], (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+      if (l <= H) {
+        S.pos[(w * 2 + 0) * H1 + l] = px;
+        S.pos[(w * 2 + 1) * H1 + l] = py;
+      }
+      if (l < H) S.u[w * H + l] = u;
+    }
+    __syncthreads();
+    // -------- collision graph (casadi/main.py:110-118), computed by every wave
+    act = false;
+    if (e >= 0 && na == 2) {
+      bool hit = false;
+      if (l <= H) {
+        const double dx = S.pos[0 * H1 + l] - S.pos[2 * H1 + l];
+        const double dy = S.pos[1 * H1 + l] - S.pos[3 * H1 + l];
+        hit = (dx * dx + dy * dy) < thr;
+      }
+      act = wany(hit);
+    }
+    if (!act && flag == 0 && !c.fixed_iters) break;   // no edge ever: stop (:115-116)
+    flag = 1;
+    // -------- z-step + dual update on the colliding pair (casadi/main.py:121-162)
+    if (act && w == 0) {
+      const bool tl = l <= H;
+      double c1x, c1y, c2x, c2y;
+      affine_c(ge1, c.dt, H, c1x, c1y);
+      affine_c(ge2, c.dt, H, c2x, c2y);
+      double bx[2], by[2];
+      bx[0] = tl ? S.pos[0 * H1 + l] + S.lam[0 * H1 + l] - c1x : 0.0;
+      by[0] = tl ? S.pos[1 * H1 + l] + S.lam[1 * H1 + l] - c1y : 0.0;
+      bx[1] = tl ? S.pos[2 * H1 + l] + S.lam[2 * H1 + l] - c2x : 0.0;
+      by[1] = tl ? S.pos[3 * H1 + l] + S.lam[3 * H1 + l] - c2y : 0.0;
+      const double w1 = tl ? ge1.ax * bx[0] + ge1.ay * by[0] : 0.0;
+      const double w2 = tl ? ge2.ax * bx[1] + ge2.ay * by[1] : 0.0;
+      const double q1 = Tt_apply(shdn(w1, 1)), q2 = Tt_apply(shdn(w2, 1));
+      qe.q[0] = (l < H) ? -c.rho * q1 : 0.0;
+      qe.q[1] = (l < H) ? -c.rho * q2 : 0.0;
+      double uh[2];
+      status_e |= qp_solve(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every, uh);
+      warm_e = true;
+      // hat positions: nonlinear rollout of the rounded pair controls (:153-158)
+      double hx[2], hy[2], hth;
+      for (int v = 0; v < 2; ++v) {
+        const double uv = (l < H) ? around(uh[v], c.round_decimals) : 0.0;
+        rollout(S.xt + 3 * v, A.spd[a0 + v], uv, c, H, true, hx[v], hy[v], hth);
+      }
+      // dual update (plain :161-162 / PI + anti-windup MATLAB :156-188)
+      double px[2], py[2];
+      for (int v = 0; v < 2; ++v) {
+        px[v] = tl ? S.pos[(2 * v + 0) * H1 + l] : 0.0;
+        py[v] = tl ? S.pos[(2 * v + 1) * H1 + l] : 0.0;
+      }
+      double dist = 0.0;
+      {
+        const double dx = px[0] - px[1], dy = py[0] - py[1];
+        dist = sqrt(dx * dx + dy * dy);
+      }
+      const double mind = wmin(tl ? dist : INFINITY);
+      const double kP = c.theta1 - c.theta2 / (1.0 + exp(-mind));
+      const double Wsat = c.windup_sat;
+      for (int v = 0; v < 2; ++v) {
+        double* lam = S.lam + v * 2 * H1;
+        double* Sv = S.S + v * 2 * H1;
+        double* Dv = S.D + v * 2 * H1;
+        double* hat = S.hat + v * 2 * H1;
+        bool changed = false;
+        double lraw[2], lsat[2];
+        for (int xy = 0; xy < 2; ++xy) {
+          const double p = xy == 0 ? px[v] : py[v];
+          const double h = xy == 0 ? hx[v] : hy[v];
+          double lv = tl ? lam[xy * H1 + l] : 0.0;
+          const double err = p - h;
+          if (c.dual_mode == PIADMM_DUAL_PLAIN) {
+            lv = lv + c.rho * err;
+          } else {
+            const double sv = tl ? (Sv[xy * H1 + l] + c.kI * err) + Dv[xy * H1 + l] : 0.0;
+            if (tl) Sv[xy * H1 + l] = sv;
+            lv = sv + kP * err;
+          }
+          lraw[xy] = lv;
+          lsat[xy] = c.windup ? fmin(Wsat, fmax(lv, -Wsat)) : lv;
+          changed |= tl && (lsat[xy] != lraw[xy]);
+          if (tl) hat[xy * H1 + l] = h;
+        }
+        const bool anyc = wany(changed);
+        for (int xy = 0; xy < 2; ++xy) {
+          if (tl) {
+            lam[xy * H1 + l] = lsat[xy];
+            if (c.windup) Dv[xy * H1 + l] = anyc ? lsat[xy] - lraw[xy] : 0.0;
+          }
+        }
+      }
+      // residual contributions of this pair (casadi/main.py:167-173): v1 side only
+      double rr = 0.0, ss = 0.0;
+      if (tl) {
+        const double ex = px[0] - S.hat[0 * H1 + l], ey = py[0] - S.hat[1 * H1 + l];
+        rr = ex * ex + ey * ey;
+        const double fx = c.rho * (S.last[0 * H1 + l] - S.hat[0 * H1 + l]);
+        const double fy = c.rho * (S.last[1 * H1 + l] - S.hat[1 * H1 + l]);
+        ss = fx * fx + fy * fy;
+      }
+      rr = wsum(rr);
+      ss = wsum(ss);
+      if (l == 0) {
+        S.sc[0] = 2.0 * sqrt(rr);
+        S.sc[1] = aliased ? 0.0 : 2.0 * sqrt(ss);
+        S.sc[2] = rdl(dist, 1);
+      }
+    }
+    __syncthreads();
+    // -------- termination (casadi/main.py:164-181; MATLAB :191-210)
+    const double rk = act ? S.sc[0] : 0.0;
+    const double sk = act ? S.sc[1] : 0.0;
+    if (act) dis_chk = S.sc[2];
+    if (threadIdx.x == 0) {
+      resid[2 * it + 0] = rk;
+      resid[2 * it + 1] = sk;
+    }
+    if (!c.fixed_iters && rk <= c.eps_pri && sk <= c.eps_dual &&
+        (!c.term_dist_check || dis_chk > c.dis_thres))
+      break;
+    if (c.alias_dual_residual) {
+      aliased = 1;
+    } else {
+      for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) S.last[i] = S.hat[i];
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+
+  // ---- outputs and propagation (casadi/main.py:185-192)
+  if (threadIdx.x == 0) {
+    A.iters[ci] = iters;
+    for (int it = iters; it < c.max_outer; ++it) resid[2 * it] = resid[2 * it + 1] = NAN;
+    if (e >= 0) A.edge_active[e] = act ? 1 : 0;
+  }
+  if (w < na) {
+    const int a = a0 + w;
+    for (int i = l; i < 2 * H1; i += WAVE) A.pos_old[(size_t)a * 2 * H1 + i] = S.pos[w * 2 * H1 + i];
+    const double u = (l < H) ? S.u[w * H + l] : 0.0;
+    if (l < H) A.u[(size_t)a * H + l] = u;
+    double px, py, pth;
+    rollout(S.xt + 3 * w, A.spd[a], u, c, H, true, px, py, pth);
+    if (l == 1) {
+      A.xt[3 * a + 0] = px;
+      A.xt[3 * a + 1] = py;
+      A.xt[3 * a + 2] = pth;
+    }
+    if (l == 0) A.status[a] = status_x;
+  }
+  if (e >= 0) {
+    for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) {
+      A.hat[(size_t)e * 4 * H1 + i] = S.hat[i];
+      A.lam[(size_t)e * 4 * H1 + i] = S.lam[i];
+    }
+    if (threadIdx.x == 0) A.status[A.N + e] = status_e;
+  }
+}
+
+int launch_mpc_step(const DevArgs& a, int t, hipStream_t s) {
+  const size_t sh = lds_bytes(a.cfg.H);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k_mpc_step, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sh) != hipSuccess)
+      return -1;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_mpc_step, dim3(a.C), dim3(NW * WAVE), sh, s, a, t);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace pd

@@ -1,0 +1,70 @@
+// Internal device/host shared definitions for libpiadmm (not part of the ABI).
+#pragma once
+#include "piadmm.h"
+
+namespace pd {
+
+constexpr int WAVE = 64;
+constexpr int NW = 2;        // waves per workgroup = agents per component (max)
+constexpr int HMAX = 32;     // horizon limit of this version: lane k <-> time index k
+constexpr int LD = 65;       // odd LDS stride of the per-wave matrix scratch
+constexpr int RUIZ_ITERS = 10;
+constexpr int PDAS_STEPS = 4;
+
+// Row slots per lane.  x-step: 0 box, 1 rate.  pair (z-step): 0 box v1, 1 rate v1,
+// 2 box v2, 3 rate v2, 4 hinge (time k+1).  Global row id = slot*H + lane.
+enum RowLab : signed char { FREE = 0, LOWER = 1, UPPER = 2 };        // box / rate rows
+enum HingeLab : signed char { HZERO = 0, HKINK = 1, HLINEAR = 2 };   // hinge rows
+
+struct DevArgs {
+  piadmm_config_t cfg;
+  int N, E, C, T;
+  // scenario (read-only during a step)
+  const double* spd;        // N
+  const double* ref;        // N*2*T
+  const int* comp_ptr;      // C+1 : agents of component c are [comp_ptr[c], comp_ptr[c+1])
+  const int* comp_edge;     // C   : the component's pair index or -1
+  const int* edges;         // E*2
+  const int* nbr_cnt;       // N   : candidate neighbours per agent (|N(i)| in the AL sum)
+  // state
+  double* xt;               // N*3
+  double* u;                // N*H   primal_u
+  double* pos_old;          // N*2*(H+1)
+  double* hat;              // E*2*2*(H+1)
+  double* lam;              // E*2*2*(H+1)
+  unsigned char* edge_active;  // E
+  int* iters;               // C
+  double* resid;            // C*max_outer*2
+  int* status;              // N+E
+  // per-step solver workspace
+  double* Pinv_x;           // N*H*H
+  double* sc_x;             // N*4*HMAX   (D, Ebox, Erate, spare)
+  double* ws_x;             // N*5*HMAX   warm ADMM state (xs, zs0, zs1, ys0, ys1)
+  signed char* lab_x;       // N*2*HMAX
+  double* Pinv_e;           // E*(2H)*(2H)
+  double* PGt;              // E*H*(2H)   row k = P^-1 G_k'
+  double* GPG;              // E*H*H
+  double* sc_e;             // E*8*HMAX   (D1, D2, Eb1, Er1, Eb2, Er2, Eh, h0)
+  double* ws_e;             // E*12*HMAX  (xs0, xs1, zs0..4, ys0..4)
+  signed char* lab_e;       // E*5*HMAX
+  double* gcoef_e;          // E*4        (g1, g2, spare)
+};
+
+// LDS bytes needed by one workgroup for horizon H.
+inline size_t lds_bytes(int H) {
+  size_t d = 0;
+  d += 2 * (size_t)H * H;          // agent K_s^-1 (2 agents)
+  d += 4 * (size_t)H * H;          // pair K_s^-1 (2H x 2H)
+  d += NW * 64 * LD;               // per-wave matrix scratch
+  d += NW * 512;                   // per-wave vector buffers
+  size_t H1 = H + 1;
+  d += 2 * 2 * H1;                 // pos_old
+  d += 2 * 3 + 2 * 2 + 2 * H;      // xt, seeds, u
+  d += 5 * 2 * 2 * H1;             // hat, lam, S, D, last_hat
+  d += 32;                         // scalars
+  return d * sizeof(double);
+}
+
+int launch_mpc_step(const DevArgs& a, int t, hipStream_t s);
+
+}  // namespace pd

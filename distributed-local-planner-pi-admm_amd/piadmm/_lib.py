@@ -1,0 +1,116 @@
+"""ctypes binding of libpiadmm.so (include/piadmm.h).
+
+There is no fallback: if the HIP library is missing or cannot be loaded,
+``load()`` raises, and so does every solver entry point.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .config import PIADMMConfig
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpiadmm.so")
+
+c_i32, c_dbl = ctypes.c_int32, ctypes.c_double
+
+
+class PiadmmConfigC(ctypes.Structure):
+    """Byte-for-byte mirror of ``piadmm_config_t``."""
+    _fields_ = [
+        ("n_agents", c_i32), ("H", c_i32), ("max_outer", c_i32), ("dual_mode", c_i32),
+        ("dt", c_dbl), ("L", c_dbl), ("dis_thres", c_dbl), ("beta", c_dbl), ("Pnorm", c_dbl),
+        ("Pcost", c_dbl), ("rho", c_dbl), ("eps_pri", c_dbl), ("eps_dual", c_dbl),
+        ("u_max", c_dbl), ("du_max", c_dbl),
+        ("kP", c_dbl), ("kI", c_dbl), ("theta1", c_dbl), ("theta2", c_dbl), ("windup_sat", c_dbl),
+        ("windup", c_i32), ("round_decimals", c_i32), ("collide_sq_thres", c_i32),
+        ("alias_dual_residual", c_i32), ("pos_model", c_i32), ("term_dist_check", c_i32),
+        ("fixed_iters", c_i32), ("max_inner", c_i32),
+        ("admm_rho", c_dbl), ("admm_sigma", c_dbl), ("admm_alpha", c_dbl), ("qp_tol", c_dbl),
+        ("polish_every", c_i32), ("device", c_i32),
+    ]
+
+
+def to_c(cfg: PIADMMConfig, n_agents: int, device: int = 0) -> PiadmmConfigC:
+    c = PiadmmConfigC()
+    for name, _ in PiadmmConfigC._fields_:
+        if name == "n_agents":
+            c.n_agents = int(n_agents)
+        elif name == "device":
+            c.device = int(device)
+        else:
+            setattr(c, name, getattr(cfg, name))
+    return c
+
+
+# (name, restype, argtypes) -- every symbol declared in include/piadmm.h
+_P = ctypes.POINTER
+_H = ctypes.c_void_p
+_dp = _P(c_dbl)
+_ip = _P(c_i32)
+SYMBOLS = [
+    ("piadmm_abi_version", c_i32, []),
+    ("piadmm_build_info", ctypes.c_char_p, []),
+    ("piadmm_device_count", c_i32, []),
+    ("piadmm_config_size", c_i32, []),
+    ("piadmm_create", c_i32, [_P(PiadmmConfigC), _P(_H)]),
+    ("piadmm_destroy", c_i32, [_H]),
+    ("piadmm_last_error", ctypes.c_char_p, [_H]),
+    ("piadmm_set_scenario", c_i32, [_H, _dp, _dp, _dp, c_i32, _ip, c_i32]),
+    ("piadmm_set_xt", c_i32, [_H, _dp]),
+    ("piadmm_mpc_step", c_i32, [_H, c_i32, _dp, _dp, _dp, _ip, _ip]),
+    ("piadmm_mpc_steps_async", c_i32, [_H, c_i32, c_i32]),
+    ("piadmm_sync", c_i32, [_H]),
+    ("piadmm_time_steps", c_i32, [_H, c_i32, c_i32, _P(ctypes.c_float)]),
+    ("piadmm_get_state", c_i32, [_H, _dp, _dp, _dp, _dp, _dp, _P(ctypes.c_uint8), _ip]),
+    ("piadmm_n_components", c_i32, [_H]),
+]
+
+_lib = None
+
+
+class PiadmmError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load libpiadmm.so (built by ``make`` / ``__graft_entry__.build()``); raise if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise PiadmmError(f"HIP library not built: {p} (run `make -C distributed-local-planner-pi-admm_amd`)")
+    lib = ctypes.CDLL(p)
+    for name, res, args in SYMBOLS:
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.piadmm_config_size() != ctypes.sizeof(PiadmmConfigC):
+        raise PiadmmError("piadmm_config_t layout mismatch between header and binding")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, handle=None):
+    if rc != 0:
+        msg = load().piadmm_last_error(handle)
+        raise PiadmmError(f"libpiadmm error {rc}: {msg.decode() if msg else ''}")
+
+
+def dptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+def iptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_ip)

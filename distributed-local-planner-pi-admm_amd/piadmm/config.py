@@ -1,0 +1,93 @@
+"""PI-ADMM configuration: the Python mirror of ``piadmm_config_t`` (include/piadmm.h).
+
+The reference keeps its parameters in a ``Bunch`` built in
+``casadi/PI_ADMM_class.py:15-28`` plus driver constants (``casadi/main.py:18-27``)
+and, for the PI anti-windup variant, the MATLAB block
+``matlab_old_files/ADMM_CVX_two_veh_intesection_PI_antiwindup.m:6-25,43``.
+Those become one frozen struct with named presets.  Every reference quirk that
+changes numbers is an explicit flag here, so a preset
+reproduces exactly one reference script.
+
+Field order and types must match ``piadmm_config_t`` byte for byte; the ctypes
+mirror lives in ``piadmm/_lib.py`` and ``tests/test_capi.py`` checks the size.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+# dual-update modes
+DUAL_PLAIN = 0      # lam += rho*(p - hat)            casadi/main.py:161-162
+DUAL_PI = 1         # per-edge PI + back-calculation   ADMM_CVX_..._PI_antiwindup.m:156-188
+
+# position model used for pos_old (quirk B15)
+POS_LINEAR = 0      # Python dynamic_update_local (heading frozen)   casadi/PI_ADMM_class.py:59-69
+POS_NONLINEAR = 1   # MATLAB dynamic_update_local numeric branch      ADMM_CVX_...:312-330
+
+
+@dataclasses.dataclass(frozen=True)
+class PIADMMConfig:
+    # --- problem (casadi/PI_ADMM_class.py:15-28) ---
+    H: int = 15                 # num_ho
+    max_outer: int = 100        # iter_num
+    dt: float = 0.1
+    L: float = 1.0
+    dis_thres: float = 2.0
+    beta: float = 10.0
+    Pnorm: float = 1.0
+    Pcost: float = 1.0
+    rho: float = 2.0
+    eps_pri: float = 20.0
+    eps_dual: float = 1.0
+    u_max: float = math.pi / 6      # nonlcon_function :173-174
+    du_max: float = math.pi / 9     # nonlcon_function :179-180
+    # --- dual update (MATLAB PI anti-windup :20-25,43) ---
+    dual_mode: int = DUAL_PLAIN
+    windup: int = 0             # 1: saturate + back-calculate (:169-188)
+    kP: float = 0.0
+    kI: float = 0.0
+    theta1: float = 5.0
+    theta2: float = 3.0
+    windup_sat: float = 30.0
+    # --- reference quirks ---
+    round_decimals: int = 4     # B6: np.around(.,4) on u, u_hat, seeds; -1 = off
+    collide_sq_thres: int = 0   # B2: 0 = Python (d^2 < dis_thres), 1 = MATLAB (d^2 < dis_thres^2)
+    alias_dual_residual: int = 1  # B4: Python last_iter_hat_pos aliasing -> s_k == 0 after iter 1
+    pos_model: int = POS_LINEAR   # B15: pos_old rollout model
+    term_dist_check: int = 0    # MATLAB extra stop condition dis_vec(2) > dis_thres (:202)
+    fixed_iters: int = 0        # 1: never terminate early (throughput runs)
+    # --- inner QP solver (build's own; not in the reference) ---
+    admm_rho: float = 0.05      # ADMM penalty in the Ruiz-scaled space (tools/qp_sim.py sweep)
+    admm_sigma: float = 1e-6
+    admm_alpha: float = 1.6
+    max_inner: int = 4000       # ADMM iteration cap per QP
+    polish_every: int = 5       # try an active-set polish every k ADMM iterations
+    qp_tol: float = 1e-9        # KKT acceptance tolerance of a polished solution
+
+    def replace(self, **kw) -> "PIADMMConfig":
+        return dataclasses.replace(self, **kw)
+
+    @property
+    def thr_collide(self) -> float:
+        return self.dis_thres ** 2 if self.collide_sq_thres else self.dis_thres
+
+
+def casadi_default(**kw) -> PIADMMConfig:
+    """``casadi/PI_ADMM_class.py:15-28`` + ``casadi/main.py`` (plain dual, rounding, aliasing)."""
+    return PIADMMConfig().replace(**kw)
+
+
+def matlab_pi(**kw) -> PIADMMConfig:
+    """``ADMM_CVX_two_veh_intesection_PI_antiwindup.m:6-25,43``: per-edge PI + back-calculation."""
+    base = PIADMMConfig(
+        H=8, max_outer=100, dt=0.1, L=1.0, dis_thres=2.0, beta=1000.0, Pnorm=5.0,
+        Pcost=1.0, rho=3.5, eps_pri=0.1, eps_dual=0.1, dual_mode=DUAL_PI, windup=1,
+        kP=0.0, kI=3.5, theta1=5.0, theta2=3.0, windup_sat=30.0, round_decimals=-1,
+        collide_sq_thres=1, alias_dual_residual=0, pos_model=POS_NONLINEAR,
+        term_dist_check=1)
+    if "rho" in kw and "kI" not in kw:
+        kw["kI"] = kw["rho"]    # param.kI = param.rho (:21)
+    return base.replace(**kw)
+
+
+PRESETS = {"casadi_default": casadi_default, "matlab_pi": matlab_pi}

@@ -1,0 +1,143 @@
+"""Host driver: the MI355X counterpart of ``PI_ADMM_CASADI`` + the ``casadi/main.py`` loop.
+
+The reference builds a ``PI_ADMM_CASADI`` object (``casadi/PI_ADMM_class.py:12-37``),
+then runs, in Python, ``for num_step ...: for i_iter ...: for i_veh ...: ca.qpsol(...)``
+(``casadi/main.py:43-201``).  Here the object holds a libpiadmm handle and one
+``mpc_step`` call runs that whole ``num_step`` body for every agent on the GPU.
+
+Attribute names follow the reference so scripts read the same:
+``solver.param.num_ho``, ``solver.param.spd``, ``solver.ref_traj`` (2N x T),
+``solver.xt`` (N x 3), ``solver.iter_his``, ``solver.x_vec`` / ``u_vec``.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import types
+
+import numpy as np
+
+from . import _lib
+from .config import PIADMMConfig
+from .scenario import Scenario
+
+
+@dataclasses.dataclass
+class StepResult:
+    xt: np.ndarray         # (N,3) state after propagation (casadi/main.py:189-192)
+    u: np.ndarray          # (N,H) primal_u used for propagation (:187)
+    resid: np.ndarray      # (C, max_outer, 2) (rk, sk) per executed iteration, NaN after
+    iters: np.ndarray      # (C,) outer iterations executed (iter_his, :186)
+    status: np.ndarray     # (N+E,) PIADMM_QP_* flags per agent then per pair
+
+
+class PI_ADMM_MI355X:
+    """Batched PI-ADMM planner on one GPU (one handle, one HIP stream)."""
+
+    def __init__(self, cfg: PIADMMConfig, scenario: Scenario, device: int = 0):
+        self.cfg = cfg
+        self.scn = scenario
+        self.N = scenario.n_agents
+        self.E = scenario.n_edges
+        self.lib = _lib.load()
+        c = _lib.to_c(cfg, self.N, device)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.piadmm_create(ctypes.byref(c), ctypes.byref(h)))
+        self._h = h
+        self.param = types.SimpleNamespace(
+            dt=cfg.dt, L=cfg.L, num_ho=cfg.H, num_veh=self.N, dis_thres=cfg.dis_thres,
+            spd=scenario.spd.copy(), beta=cfg.beta, Pnorm=cfg.Pnorm, Pcost=cfg.Pcost,
+            iter_num=cfg.max_outer, rho=cfg.rho, eps_pri=cfg.eps_pri, eps_dual=cfg.eps_dual)
+        # ref_traj in the reference layout: rows [x_0; y_0; x_1; y_1; ...] (PI_ADMM_class.py:37)
+        self.ref_traj = scenario.ref.reshape(2 * self.N, -1)
+        spd = np.ascontiguousarray(scenario.spd, np.float64)
+        xt0 = np.ascontiguousarray(scenario.xt0, np.float64)
+        ref = np.ascontiguousarray(scenario.ref, np.float64)
+        edges = np.ascontiguousarray(scenario.edges, np.int32).reshape(-1)
+        self._check(self.lib.piadmm_set_scenario(self._h, _lib.dptr(spd), _lib.dptr(xt0), _lib.dptr(ref),
+                                                 ref.shape[2], _lib.iptr(edges) if edges.size else None,
+                                                 self.E))
+        self.C = self.lib.piadmm_n_components(self._h)
+        self.t = 0
+        self.xt = xt0.copy()
+        self.iter_his: list[np.ndarray] = []
+        self.x_vec: list[np.ndarray] = []
+        self.u_vec: list[np.ndarray] = []
+
+    # ------------------------------------------------------------------ core
+    def _check(self, rc):
+        _lib.check(rc, self._h)
+
+    def mpc_step(self, t: int | None = None) -> StepResult:
+        """One ``num_step`` iteration of ``casadi/main.py:43-201`` for all agents."""
+        t = self.t if t is None else t
+        H = self.cfg.H
+        xt = np.empty((self.N, 3))
+        u = np.empty((self.N, H))
+        resid = np.empty((self.C, self.cfg.max_outer, 2))
+        iters = np.empty(self.C, np.int32)
+        status = np.empty(self.N + self.E, np.int32)
+        self._check(self.lib.piadmm_mpc_step(self._h, t, _lib.dptr(xt), _lib.dptr(u), _lib.dptr(resid),
+                                             _lib.iptr(iters), _lib.iptr(status)))
+        self.t = t + 1
+        self.xt = xt
+        self.iter_his.append(iters)
+        self.x_vec.append(xt[:, :2].T.copy())
+        self.u_vec.append(u[:, 0].copy())
+        return StepResult(xt=xt, u=u, resid=resid, iters=iters, status=status)
+
+    def run(self, n_steps: int | None = None) -> list[StepResult]:
+        n = self.scn.n_steps if n_steps is None else n_steps
+        return [self.mpc_step() for _ in range(n)]
+
+    def steps_async(self, t0: int, n_steps: int):
+        """Enqueue MPC steps without host copies (state stays in HBM)."""
+        self._check(self.lib.piadmm_mpc_steps_async(self._h, t0, n_steps))
+
+    def sync(self):
+        self._check(self.lib.piadmm_sync(self._h))
+
+    def time_steps(self, t0: int, n_steps: int) -> float:
+        """hipEvent time (ms) of n_steps MPC steps on the handle's stream."""
+        ms = ctypes.c_float()
+        self._check(self.lib.piadmm_time_steps(self._h, t0, n_steps, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def set_xt(self, xt: np.ndarray):
+        xt = np.ascontiguousarray(xt, np.float64)
+        self._check(self.lib.piadmm_set_xt(self._h, _lib.dptr(xt)))
+        self.xt = xt.copy()
+
+    def state(self) -> dict:
+        H1 = self.cfg.H + 1
+        out = dict(xt=np.empty((self.N, 3)), u=np.empty((self.N, self.cfg.H)),
+                   pos_old=np.empty((self.N, 2, H1)), hat=np.empty((self.E, 2, 2, H1)),
+                   lam=np.empty((self.E, 2, 2, H1)), edge_active=np.empty(self.E, np.uint8),
+                   iters=np.empty(self.C, np.int32))
+        ea = out["edge_active"].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if self.E else None
+        self._check(self.lib.piadmm_get_state(
+            self._h, _lib.dptr(out["xt"]), _lib.dptr(out["u"]), _lib.dptr(out["pos_old"]),
+            _lib.dptr(out["hat"]) if self.E else None, _lib.dptr(out["lam"]) if self.E else None,
+            ea, _lib.iptr(out["iters"])))
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.piadmm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def device_count() -> int:
+    return int(_lib.load().piadmm_device_count())

@@ -1,0 +1,134 @@
+/*
+ * piadmm.h -- C-ABI of the MI355X PI-ADMM consensus solver (libpiadmm.so).
+ *
+ * Drop-in boundary for the reference's per-MPC-step inner loop
+ * (casadi/main.py:43-201 with the PI anti-windup dual update of
+ * matlab_old_files/ADMM_CVX_two_veh_intesection_PI_antiwindup.m:152-188).
+ *
+ * The reference has no plugin API: its only solver seam is CasADi,
+ *   F = ca.qpsol("solver", "osqp", {"x": u, "f": J(u), "g": g(u)}, opts); sol = F(lbg=0)
+ * called once per agent per outer iteration (casadi/main.py:96,101) and once
+ * per colliding pair (casadi/main.py:146,151), with the loop, collision test,
+ * dual update, residuals and propagation in Python around it.  This library
+ * replaces that whole loop for all agents at once: one call = one MPC step
+ * (every outer ADMM iteration of every agent and pair), so the per-call
+ * CasADi graph build + OSQP setup of the reference disappears.
+ *
+ * Conventions
+ *   - return value: 0 on success, a negative PIADMM_E* code on failure;
+ *     piadmm_last_error() gives the message.  Per-agent / per-pair QP status
+ *     comes back in status_out (never silent, unlike the reference's
+ *     error_on_fail=False at casadi/main.py:145).
+ *   - all arrays are row-major fp64 (int32 for indices); the caller owns host
+ *     arrays, the library copies them; the library owns all device memory.
+ *   - a handle is bound to one HIP device and is not thread-safe.
+ *   - multi-GPU = one process per GPU, each with its own handle over its own
+ *     shard of components (no data-path collective: see DESIGN.md).
+ */
+#ifndef PIADMM_H
+#define PIADMM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PIADMM_ABI_VERSION 1
+
+enum {
+  PIADMM_OK = 0,
+  PIADMM_E_ARG = -1,       /* bad argument / unsupported size */
+  PIADMM_E_HIP = -2,       /* HIP runtime error */
+  PIADMM_E_STATE = -3,     /* call out of order (e.g. step before set_scenario) */
+  PIADMM_E_NODEV = -4      /* no HIP device */
+};
+
+/* dual_mode */
+#define PIADMM_DUAL_PLAIN 0  /* lam += rho (p - hat)            casadi/main.py:161-162 */
+#define PIADMM_DUAL_PI 1     /* per-edge PI + back-calculation  ADMM_CVX_..._PI_antiwindup.m:156-188 */
+
+/* status_out codes per agent / pair (bit flags accumulated over one MPC step) */
+#define PIADMM_QP_OK 0
+#define PIADMM_QP_INEXACT 1  /* a QP hit max_inner without a certified polish */
+#define PIADMM_QP_NAN 2      /* a non-finite value was produced */
+
+/* Mirror of the reference parameters: casadi/PI_ADMM_class.py:15-28 (Bunch),
+ * casadi/main.py:26-27, ADMM_CVX_..._PI_antiwindup.m:6-25,43.  Field order is
+ * ABI: the Python dataclass piadmm.config.PIADMMConfig has the same fields. */
+typedef struct piadmm_config {
+  int32_t n_agents;
+  int32_t H;                 /* num_ho (<= 32 in this version) */
+  int32_t max_outer;         /* iter_num */
+  int32_t dual_mode;
+  double dt, L, dis_thres, beta, Pnorm, Pcost, rho, eps_pri, eps_dual, u_max, du_max;
+  double kP, kI, theta1, theta2, windup_sat;
+  int32_t windup;            /* 1: saturation + back-calculation */
+  int32_t round_decimals;    /* 4 (reference np.around) or -1 */
+  int32_t collide_sq_thres;  /* 0: d^2 < dis_thres (Python), 1: d^2 < dis_thres^2 (MATLAB) */
+  int32_t alias_dual_residual; /* 1: Python last_iter_hat_pos aliasing (quirk B4) */
+  int32_t pos_model;         /* 0: linearised pos_old (Python), 1: nonlinear (MATLAB numeric) */
+  int32_t term_dist_check;   /* 1: MATLAB extra stop condition dis_vec(2) > dis_thres */
+  int32_t fixed_iters;       /* 1: run exactly max_outer iterations (throughput runs) */
+  int32_t max_inner;         /* ADMM iteration cap per QP */
+  double admm_rho, admm_sigma, admm_alpha, qp_tol;
+  int32_t polish_every;      /* PDAS polish attempt period (ADMM iterations) */
+  int32_t device;            /* HIP device ordinal */
+} piadmm_config_t;
+
+typedef struct piadmm_ctx* piadmm_handle_t;
+
+/* Library / device queries (no handle). */
+int32_t piadmm_abi_version(void);
+const char* piadmm_build_info(void);           /* e.g. "gfx950 hip 7.2 ..." */
+int32_t piadmm_device_count(void);
+int32_t piadmm_config_size(void);              /* sizeof(piadmm_config_t), for binding checks */
+
+/* Create / destroy.  Replaces PI_ADMM_CASADI.__init__ (casadi/PI_ADMM_class.py:13-37). */
+int32_t piadmm_create(const piadmm_config_t* cfg, piadmm_handle_t* out);
+int32_t piadmm_destroy(piadmm_handle_t h);
+const char* piadmm_last_error(piadmm_handle_t h);
+
+/* Scenario: speeds (N), initial states (N x 3: x, y, theta), reference positions
+ * (N x 2 x T, ref[i][0][t] = x, ref[i][1][t] = y; casadi/PI_ADMM_class.py:33-37)
+ * and candidate pairs (E x 2, v1 < v2).  Components of the pair graph must
+ * have at most 2 agents in this version.  Resets xt to xt0. */
+int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* xt0,
+                            const double* ref, int32_t T, const int32_t* edges, int32_t n_edges);
+
+/* Overwrite the current agent states (N x 3). */
+int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt);
+
+/* One MPC step at reference time index t (casadi/main.py:43-201): seeds,
+ * outer ADMM loop (x-step QPs, collision graph, z-step QPs, dual update,
+ * residuals, termination) and propagation of xt.  Outputs may be NULL:
+ *   xt_out     N x 3        state after propagation
+ *   u_out      N x H        primal_u used for propagation
+ *   resid_out  C x max_outer x 2   (rk, sk) per executed iteration, NaN after
+ *   iters_out  C            outer iterations executed per component
+ *   status_out N + E        PIADMM_QP_* flags per agent then per pair
+ * Blocking: returns after the step and the copies have finished. */
+int32_t piadmm_mpc_step(piadmm_handle_t h, int32_t t, double* xt_out, double* u_out,
+                        double* resid_out, int32_t* iters_out, int32_t* status_out);
+
+/* Enqueue n_steps consecutive MPC steps starting at t0 on the handle's stream
+ * without host copies or synchronisation (device-resident MPC loop). */
+int32_t piadmm_mpc_steps_async(piadmm_handle_t h, int32_t t0, int32_t n_steps);
+int32_t piadmm_sync(piadmm_handle_t h);
+
+/* Device time (ms, hipEvent on the handle's stream) of n_steps MPC steps from t0. */
+int32_t piadmm_time_steps(piadmm_handle_t h, int32_t t0, int32_t n_steps, float* ms_out);
+
+/* State of the last step (any pointer may be NULL):
+ *   xt N x 3, u N x H, pos_old N x 2 x (H+1), hat / lam E x 2 x 2 x (H+1)
+ *   (direction 0 = hat_{v1 v2}, 1 = hat_{v2 v1}), edge_active E, iters C. */
+int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_old,
+                         double* hat, double* lam, uint8_t* edge_active, int32_t* iters);
+
+int32_t piadmm_n_components(piadmm_handle_t h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PIADMM_H */
