@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -221,6 +222,12 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.ws_e, E * 12 * pd::HMAX);
   rc |= dalloc(h, &A.lab_e, E * 5 * pd::HMAX);
   rc |= dalloc(h, &A.gcoef_e, E * 4);
+  rc |= dalloc(h, &A.counters, C * 8);
+  rc |= dalloc(h, &A.rho_x, (size_t)N);
+  rc |= dalloc(h, &A.rho_e, E);
+#ifdef PIADMM_STAMPS
+  rc |= dalloc(h, &A.stamps, C * 32);
+#endif
   if (rc) return PIADMM_E_HIP;
   HIPCHK(h, hipMemcpyAsync(d_spd, spd, N * sizeof(double), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(d_ref, ref, (size_t)N * 2 * T * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -229,6 +236,11 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   if (E) HIPCHK(h, hipMemcpyAsync(d_ed, edges, 2 * E * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(d_nb, nbr.data(), N * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(A.xt, xt0, (size_t)N * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  {
+    std::vector<double> r0((size_t)std::max<size_t>(N, E), h->cfg.admm_rho);
+    HIPCHK(h, hipMemcpyAsync(A.rho_x, r0.data(), (size_t)N * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    if (E) HIPCHK(h, hipMemcpyAsync(A.rho_e, r0.data(), E * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   A.spd = d_spd;
   A.ref = d_ref;
@@ -316,5 +328,47 @@ int32_t piadmm_time_steps(piadmm_handle_t h, int32_t t0, int32_t n_steps, float*
 }
 
 int32_t piadmm_n_components(piadmm_handle_t h) { return h && h->have_scn ? h->C : 0; }
+
+int32_t piadmm_get_counters(piadmm_handle_t h, uint64_t* out) {
+  if (!h || !out) return fail(h, PIADMM_E_ARG, "null argument");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  std::vector<unsigned long long> buf((size_t)h->C * 8);
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  HIPCHK(h, hipMemcpyAsync(buf.data(), h->a.counters, buf.size() * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (int k = 0; k < 8; ++k) out[k] = 0;
+  for (int c = 0; c < h->C; ++c)
+    for (int k = 0; k < 8; ++k) out[k] += buf[(size_t)c * 8 + k];
+  return PIADMM_OK;
+}
+
+int32_t piadmm_get_component_counters(piadmm_handle_t h, uint64_t* out, int32_t n) {
+  if (!h || !out) return fail(h, PIADMM_E_ARG, "null argument");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  if (n < h->C * 8) return fail(h, PIADMM_E_ARG, "buffer too small");
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  HIPCHK(h, hipMemcpyAsync(out, h->a.counters, (size_t)h->C * 8 * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PIADMM_OK;
+}
+
+// Diagnostic builds only: per-component phase cycle sums (C x 32), reset with the counters.
+int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n) {
+  if (!h || !out) return fail(h, PIADMM_E_ARG, "null argument");
+  if (!h->a.stamps) return fail(h, PIADMM_E_STATE, "library built without PIADMM_STAMPS");
+  if (n < h->C * 32) return fail(h, PIADMM_E_ARG, "buffer too small");
+  HIPCHK(h, hipMemcpy(out, h->a.stamps, (size_t)h->C * 32 * 8, hipMemcpyDeviceToHost));
+  return PIADMM_OK;
+}
+
+int32_t piadmm_reset_counters(piadmm_handle_t h) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  HIPCHK(h, hipMemsetAsync(h->a.counters, 0, (size_t)h->C * 8 * 8, h->stream));
+  if (h->a.stamps) HIPCHK(h, hipMemsetAsync(h->a.stamps, 0, (size_t)h->C * 32 * 8, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PIADMM_OK;
+}
 
 }  // extern "C"

@@ -23,6 +23,22 @@
 
 namespace pd {
 
+// Diagnostic phase stamps (separate build, never in the measured library).
+#ifdef PIADMM_STAMPS
+__device__ unsigned long long* g_stamps;
+#define STAMP_T() __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(slot, t0)                                                                   \
+  do {                                                                                        \
+    const unsigned long long _d = __builtin_amdgcn_s_memtime() - (t0);                       \
+    if (__lane_id() == 0 && g_stamps) atomicAdd(&g_stamps[blockIdx.x * 32 + (slot)], _d);   \
+  } while (0)
+#else
+#define STAMP_T() 0ull
+#define STAMP_ADD(slot, t0) ((void)(t0))
+#endif
+enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL, ST_ZSTEP, ST_ZQP, ST_ZRED,
+                 ST_KERNEL, ST_RED_GEMV, ST_RED_S, ST_RED_CHOL, ST_RED_X, ST_ADMM, ST_XQ, ST_TERM };
+
 // ============================================================ wave primitives
 __device__ __forceinline__ int lid() { return (int)__lane_id(); }
 
@@ -111,10 +127,10 @@ __device__ __forceinline__ double around(double x, int d) {
 // sum_{k=0}^{H} (k-1-i)+ (k-1-j)+ = (T'T)_{ij}, exact in integers.
 __device__ __forceinline__ double TT(int i, int j, int H) {
   const int a = max(i, j), b = min(i, j);
-  const long long n = H - 1 - a;
+  const int n = H - 1 - a;
   if (n < 0) return 0.0;
-  const long long d = a - b;
-  const long long s = n * (n + 1) * (2 * n + 1) / 6 + d * n * (n + 1) / 2;
+  const int d = a - b;
+  const int s = n * (n + 1) * (2 * n + 1) / 6 + d * (n * (n + 1) / 2);   // < 2^31 for H <= 64
   return (double)s;
 }
 // (D2'D2)_{ij}, D2 = second difference (H-2) x H  (cost_smooth, PI_ADMM_class.py:123)
@@ -185,7 +201,8 @@ __device__ __forceinline__ void rollout(const double* xt3, double s, double u, c
   // per-lane rates at time k = lane
   double xd, yd;
   if (nonlinear) {
-    const double sk = sin(my_th), ck = cos(my_th);
+    double sk, ck;
+    sincos(my_th, &sk, &ck);
     xd = -s * sk * my_th + (s * ck + s * my_th * sk);
     yd = s * ck * my_th + (s * sk - s * my_th * ck);
   } else {
@@ -208,23 +225,23 @@ __device__ __forceinline__ void rollout(const double* xt3, double s, double u, c
 }
 
 // ============================================================ in-wave dense kernels
-// In-place Gauss-Jordan inverse of an SPD matrix held in LDS (stride LD), lane = column.
-__device__ __forceinline__ void gj_invert(double* m, int n) {
+// In-place Gauss-Jordan inverse of an SPD matrix held in LDS (stride ld), lane = column.
+__device__ __forceinline__ void gj_invert(double* m, int n, int ld) {
   const int l = lid();
   for (int p = 0; p < n; ++p) {
-    const double colp = (l < n) ? m[l * LD + p] : 0.0;   // a_lp
+    const double colp = (l < n) ? m[l * ld + p] : 0.0;   // a_lp
     const double ip = 1.0 / rdl(colp, p);
-    const double rpj = (l < n) ? ((l == p) ? ip : m[p * LD + l] * ip) : 0.0;
+    const double rpj = (l < n) ? ((l == p) ? ip : m[p * ld + l] * ip) : 0.0;
     wsync();
     for (int i = 0; i < n; ++i) {
       if (i == p) continue;
       const double aip = rdl(colp, i);
       if (l < n) {
-        if (l == p) m[i * LD + p] = -aip * ip;
-        else m[i * LD + l] -= aip * rpj;
+        if (l == p) m[i * ld + p] = -aip * ip;
+        else m[i * ld + l] -= aip * rpj;
       }
     }
-    if (l < n) m[p * LD + l] = rpj;
+    if (l < n) m[p * ld + l] = rpj;
     wsync();
   }
 }
@@ -237,6 +254,8 @@ __device__ __forceinline__ double clamp_norm(double v) {
 // ============================================================ QP solver
 // Generalised QP  min 1/2 x'Px + q'x + sum_r phi_r(a_r'x)  with box rows
 // (indicator of [lo,hi]) and, for the pair, hinge rows beta*max(0, h - a'x).
+//   x-step (NV=1): P = coefP*mm*T'T + 2 D2'D2 + 2 Pcost I          (PI_ADMM_class.py:114-135)
+//   pair   (NV=2): P = blockdiag(rho*mm_v*T'T + 2 Pcost I)          (PI_ADMM_class.py:145-169)
 template <int NV>
 struct QP {
   static constexpr int NR = (NV == 1) ? 2 : 5;
@@ -247,18 +266,112 @@ struct QP {
   double lo[NR], hi[NR];
   bool valid[NR];
   double g1, g2;          // hinge coefficients (pair only)
+  double mm[NV];          // |M|^2 factors (ax^2 + ay^2) per vehicle
+  double coefP;           // x-step: 2 Pnorm + rho |N| ; pair: rho
+  double Pcost2;          // 2 Pcost
   double beta, rho, sigma, alpha, tol;
-  const double* K;        // LDS  n x n  scaled (P_s + sigma I + rho A_s'A_s)^-1
-  const double* Pinv;     // HBM  n x n  unscaled P^-1
+  double* K;              // LDS  n x n  scaled (P_s + sigma I + rho A_s'A_s)^-1
+  const double* Pinv;     // n x n unscaled P^-1 (LDS for the x-step, HBM for the pair)
   const double* PGt;      // HBM  H x n  row k = P^-1 G_k'
   const double* GPG;      // HBM  H x H
   double* vb;             // per-wave LDS vectors (512 doubles)
-  double* scr;            // per-wave LDS matrix scratch
-  int* ib;                // per-wave LDS ints (128)
+  double* fac;            // LDS factor region: L (lower), S (upper), stride fld
+  double* fdiag;          // LDS [2*64]: S_aa, 1/L_aa of the cached factor
+  int* ib;                // per-wave LDS ints: [0,64) current W ids, [64,128) cached W ids
+  int* fstate;            // LDS int: m of the cached factor (-1: none)
+  int fld;                // stride of fac
+  int mmax;               // capacity of fac (rows)
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
 };
 
+template <int NV>
+__device__ constexpr int NR_HINGE() { return NV == 2 ? 4 : 0; }
+
+// Unscaled P x (var lanes), matrix-free: T'T via two double scans, D2'D2 via neighbours.
+template <int NV>
+__device__ __forceinline__ void P_mul(const QP<NV>& P, const double* x, double* px) {
+  const bool in = lid() < P.H;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double tx = T_apply(x[v]);
+    const double tt = Tt_apply(in ? tx : 0.0);       // T rows live on hinge lanes < H only
+    double r = P.coefP * P.mm[v] * tt + P.Pcost2 * x[v];
+    if constexpr (NV == 1) {
+      // (D2 x)_r = x_r - 2 x_{r+1} + x_{r+2}, r <= H-3 ; (D2' w)_j = w_j - 2 w_{j-1} + w_{j-2}
+      const double d2 = (lid() <= P.H - 3) ? x[v] - 2.0 * shdn(x[v], 1) + shdn(x[v], 2) : 0.0;
+      r += 2.0 * (d2 - 2.0 * shup(d2, 1) + shup(d2, 2));
+    }
+    px[v] = in ? r : 0.0;
+  }
+}
+
+// Build K_s = D P D + sigma I + rho A_s'A_s in LDS scratch m (stride ld, lane = column),
+// invert it in place and copy it to P.K (stride n).
+template <int NV>
+__device__ __forceinline__ double P_entry(const QP<NV>& P, int v, int i, int j) {
+  const double mmv = (NV == 2 && v) ? P.mm[NV - 1] : P.mm[0];
+  double e = P.coefP * mmv * TT(i, j, P.H) + (i == j ? P.Pcost2 : 0.0);
+  if constexpr (NV == 1) e += 2.0 * D2D2(i, j, P.H);
+  return e;
+}
+
+template <int NV>
+__device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
+  const int l = lid();
+  const int H = P.H, n = P.n;
+  const int vc = (NV == 2 && l >= H) ? 1 : 0;
+  const int jc = l - vc * H;
+  const bool incol = l < n;
+  const int src = (jc >= 0 && jc < H) ? jc : 0;
+  double Dsh[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) Dsh[v] = __shfl(P.D[v], src);
+  const double Dc = (NV == 2 && vc == 1) ? Dsh[NV - 1] : Dsh[0];
+  const double gc = (vc == 0) ? P.g1 : P.g2;
+  const double Eh2 = (NV == 2 && P.valid[NR_HINGE<NV>()]) ? P.E[NR_HINGE<NV>()] * P.E[NR_HINGE<NV>()] : 0.0;
+  for (int r = 0; r < n; ++r) {
+    const int vr = (NV == 2 && r >= H) ? 1 : 0;
+    const int ir = r - vr * H;
+    double Dr, Ebr, Err, Errm;
+    if (NV == 2 && vr) {
+      Dr = rdl(P.D[NV - 1], ir);
+      Ebr = rdl(P.E[(2 * NV - 2) % QP<NV>::NR], ir);
+      Err = rdl(P.E[(2 * NV - 1) % QP<NV>::NR], ir);
+      Errm = (ir >= 1) ? rdl(P.E[(2 * NV - 1) % QP<NV>::NR], ir - 1) : 0.0;
+    } else {
+      Dr = rdl(P.D[0], ir);
+      Ebr = rdl(P.E[0], ir);
+      Err = rdl(P.E[1], ir);
+      Errm = (ir >= 1) ? rdl(P.E[1], ir - 1) : 0.0;
+    }
+    double hs = 0.0;
+    if constexpr (NV == 2) {
+      const double gr = (vr == 0) ? P.g1 : P.g2;
+      for (int k = 1; k < H; ++k) {
+        const double e2 = rdl(Eh2, k);
+        if (k > ir && k > jc) hs += e2 * (double)(k - ir) * (double)(k - jc);
+      }
+      hs *= gr * gc;
+    }
+    if (incol) {
+      double ata = hs, v = 0.0;
+      if (vr == vc) {
+        v = Dr * P_entry(P, vr, ir, jc) * Dc;
+        if (ir == jc) ata += Ebr * Ebr + Err * Err + Errm * Errm;
+        else if (jc == ir + 1) ata += -Err * Err;
+        else if (jc == ir - 1) ata += -Errm * Errm;
+      }
+      v += P.rho * Dr * Dc * ata + (r == l ? P.sigma : 0.0);
+      m[r * ld + l] = v;
+    }
+  }
+  wsync();
+  gj_invert(m, n, ld);
+  for (int r = 0; r < n; ++r)
+    if (incol) P.K[r * n + l] = m[r * ld + l];
+  wsync();
+}
 template <int NV>
 __device__ __forceinline__ void A_mul(const QP<NV>& P, const double* x, double* ax) {
 #pragma unroll
@@ -431,35 +544,70 @@ __device__ __forceinline__ double pcol(const QP<NV>& P, int id, int i) {
   return s;
 }
 
-// Solve L L' x = b in place (lane a holds b_a, a < m).  L lower in scr, linv = 1/L_aa.
-__device__ __forceinline__ double chol_solve(const double* L, double linv, double b, int m) {
+// Solve L L' x = b (lane a holds b_a, a < m).  L lower in fac (stride ld), linv = 1/L_aa.
+__device__ __forceinline__ double chol_solve(const double* L, int ld, double linv, double b, int m) {
   const int l = lid();
-  // forward
-  for (int k = 0; k < m; ++k) {
+  for (int k = 0; k < m; ++k) {       // forward, column-oriented
+    const double Llk = (l > k && l < m) ? L[l * ld + k] : 0.0;
     const double zk = rdl(b * linv, k);
     if (l == k) b = zk;
-    if (l > k && l < m) b -= L[l * LD + k] * zk;
+    b -= Llk * zk;
   }
-  // backward with L'
-  for (int k = m - 1; k >= 0; --k) {
+  for (int k = m - 1; k >= 0; --k) {  // backward with L'
+    const double Lkl = (l < k) ? L[k * ld + l] : 0.0;
     const double xk = rdl(b * linv, k);
     if (l == k) b = xk;
-    if (l < k) b -= L[k * LD + l] * xk;
+    b -= Lkl * xk;
   }
   return (l < m) ? b : 0.0;
 }
 
+// Left-looking Cholesky of S + delta I.  S is stored in the upper triangle of fac
+// (row a, columns b >= a) with its diagonal in sdiag (lane a); L goes to the strict
+// lower triangle and the diagonal.  Returns false if a pivot is not positive.
+__device__ __forceinline__ bool chol_factor(double* fac, int ld, double sdiag, double delta, int m, double& linv) {
+  const int l = lid();
+  for (int k = 0; k < m; ++k) {
+    double acc = 0.0;
+    if (l >= k && l < m) {
+      const double* ri = fac + l * ld;
+      const double* rk = fac + k * ld;
+      int j = 0;
+      for (; j + 4 <= k; j += 4)
+        acc += ri[j] * rk[j] + ri[j + 1] * rk[j + 1] + ri[j + 2] * rk[j + 2] + ri[j + 3] * rk[j + 3];
+      for (; j < k; ++j) acc += ri[j] * rk[j];
+    }
+    const double sik = (l == k) ? sdiag + delta : ((l > k && l < m) ? fac[k * ld + l] : 0.0);
+    const double d = sik - acc;
+    const double piv = rdl(d, k);
+    if (!(piv > 0.0) || !isfinite(piv)) return false;
+    const double lkk = sqrt(piv);
+    const double inv = 1.0 / lkk;
+    wsync();
+    if (l == k) {
+      fac[k * ld + k] = lkk;
+      linv = inv;
+    }
+    if (l > k && l < m) fac[l * ld + k] = d * inv;
+    wsync();
+  }
+  return true;
+}
+
 // One PDAS reduced solve for labels lab; returns false on numerical failure.
+// The Cholesky factor of S = A_W P^-1 A_W' is cached per wave and reused when the
+// working set W is unchanged (P is fixed for the whole MPC step).
 template <int NV>
 __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char* lab, double* x, double* y) {
   constexpr int NR = QP<NV>::NR;
   const int l = lid();
   const int H = P.H;
-  double* vb_q = P.vb;             // [0,64)   gemv buffer
+  const int ld = P.fld;
   double* vb_b = P.vb + 64;        // [64,128) rhs b of W rows
   double* vb_lam = P.vb + 128;     // [128,192)
   double* vb_ax = P.vb + 192;      // [192,512) A x0 by row id (<= 5*32 = 160)
-  (void)vb_q;
+  int* ids = P.ib;                 // current W
+  int* cids = P.ib + 64;           // W of the cached factor
   // q~ = q - beta G'(1_linear)
   double qt[NV];
 #pragma unroll
@@ -473,7 +621,9 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     }
   }
   double x0[NV];
+  unsigned long long t_rs = STAMP_T();
   gemv_sym(P, P.Pinv, qt, x0);
+  STAMP_ADD(ST_RED_GEMV, t_rs);
 #pragma unroll
   for (int v = 0; v < NV; ++v) x0[v] = -x0[v];
   // working set, compacted in slot-major order
@@ -490,12 +640,12 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
   }
   double ax0[NR];
   A_mul(P, x0, ax0);
-  if (m > WAVE) return false;
+  if (m > P.mmax) return false;
 #pragma unroll
   for (int s = 0; s < NR; ++s) {
     if (l < H) vb_ax[s * H + l] = ax0[s];
     if (inW[s]) {
-      P.ib[pos[s]] = s * H + l;
+      ids[pos[s]] = s * H + l;
       vb_b[pos[s]] = P.hinge(s) ? P.lo[s] : (lab[s] == LOWER ? P.lo[s] : P.hi[s]);
     }
   }
@@ -507,70 +657,75 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     for (int s = 0; s < NR; ++s) y[s] = (P.hinge(s) && P.valid[s] && lab[s] == HLINEAR) ? -P.beta : 0.0;
     return true;
   }
-  const int myid = (l < m) ? P.ib[l] : 0;
+  const int myid = (l < m) ? ids[l] : 0;
   const double rhs = (l < m) ? (vb_ax[myid] - vb_b[l]) : 0.0;
-  // S (full, symmetric) into scr: lane a = row a
-  double sdiag = 0.0;
-  for (int b = 0; b < m; ++b) {
-    const int idb = P.ib[b];
+  const bool cached = (P.fstate[0] == m) && wall(l >= m || cids[l] == myid);
+  double sdiag, linv;
+  if (cached) {
+    sdiag = (l < m) ? P.fdiag[l] : 0.0;
+    linv = (l < m) ? P.fdiag[64 + l] : 0.0;
+  } else {
+    // S (upper triangle) into fac: lane a = row a, columns b >= a
+    unsigned long long t_s = STAMP_T();
+    sdiag = 0.0;
+    for (int b = 0; b < m; ++b) {
+      const int idb = rdli(myid, b);
+      if (l <= b && l < m) {
+        const double sv = s_entry(P, myid, idb);
+        if (b == l) sdiag = sv;
+        else P.fac[l * ld + b] = sv;
+      }
+    }
+    STAMP_ADD(ST_RED_S, t_s);
+    unsigned long long t_c = STAMP_T();
+    const double dmax = wmax(l < m ? sdiag : 0.0);
+    const double delta = 1e-14 * dmax;
+    wsync();
+    linv = 0.0;
+    const bool fok = chol_factor(P.fac, ld, sdiag, delta, m, linv);
+    STAMP_ADD(ST_RED_CHOL, t_c);
+    if (!fok) {
+      if (l == 0) P.fstate[0] = -1;
+      wsync();
+      return false;
+    }
     if (l < m) {
-      const double sv = s_entry(P, myid, idb);
-      P.scr[l * LD + b] = sv;
-      if (b == l) sdiag = sv;
+      P.fdiag[l] = sdiag;
+      P.fdiag[64 + l] = linv;
+      cids[l] = myid;
     }
-  }
-  const double dmax = wmax(l < m ? sdiag : 0.0);
-  const double delta = 1e-14 * dmax;
-  wsync();
-  // Cholesky of S + delta I into the lower triangle (upper triangle keeps S)
-  double linv = 0.0;
-  if (l < m) P.scr[l * LD + l] = sdiag + delta;
-  wsync();
-  for (int k = 0; k < m; ++k) {
-    const double v = (l < m) ? P.scr[l * LD + k] : 0.0;
-    const double piv = rdl(v, k);
-    if (!(piv > 0.0) || !isfinite(piv)) return false;
-    const double inv = 1.0 / sqrt(piv);
-    const double lk = v * inv;
-    if (l == k) {
-      P.scr[k * LD + k] = piv * inv;   // sqrt(piv)
-      linv = inv;
-    }
-    if (l > k && l < m) P.scr[l * LD + k] = lk;
-    wsync();
-    for (int j = k + 1; j < m; ++j) {
-      const double ljk = rdl(lk, j);
-      if (l >= j && l < m) P.scr[l * LD + j] -= lk * ljk;
-    }
+    if (l == 0) P.fstate[0] = m;
     wsync();
   }
-  double lamv = chol_solve(P.scr, linv, rhs, m);
+  double lamv = chol_solve(P.fac, ld, linv, rhs, m);
   // one step of iterative refinement against the unregularised S
   {
     double sl = 0.0;
     for (int b = 0; b < m; ++b) {
       const double lb = rdl(lamv, b);
       if (l < m) {
-        const double sab = (b == l) ? sdiag : (b > l ? P.scr[l * LD + b] : P.scr[b * LD + l]);
+        const double sab = (b == l) ? sdiag : (b > l ? P.fac[l * ld + b] : P.fac[b * ld + l]);
         sl += sab * lb;
       }
     }
     const double r = (l < m) ? rhs - sl : 0.0;
-    lamv += chol_solve(P.scr, linv, r, m);
+    lamv += chol_solve(P.fac, ld, linv, r, m);
   }
   if (!isfinite(lamv)) return false;
+  unsigned long long t_x = STAMP_T();
   // x = x0 - sum_a (P^-1 a_a) lam_a
   double xv[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) xv[v] = x0[v];
   for (int a = 0; a < m; ++a) {
-    const int ida = P.ib[a];
+    const int ida = rdli(myid, a);
     const double la = rdl(lamv, a);
     if (l < H) {
 #pragma unroll
       for (int v = 0; v < NV; ++v) xv[v] -= pcol(P, ida, v * H + l) * la;
     }
   }
+  STAMP_ADD(ST_RED_X, t_x);
   if (l < m) vb_lam[l] = lamv;
   wsync();
 #pragma unroll
@@ -625,11 +780,15 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
 }
 
 template <int NV>
-__device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y) {
+__device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y, int& nsolve) {
   constexpr int NR = QP<NV>::NR;
   signed char nl[NR];
   for (int it = 0; it < PDAS_STEPS; ++it) {
-    if (!reduced_solve(P, lab, x, y)) return false;
+    ++nsolve;
+    unsigned long long t_r = STAMP_T();
+    const bool rs_ok = reduced_solve(P, lab, x, y);
+    STAMP_ADD(NV == 1 ? ST_XRED : ST_ZRED, t_r);
+    if (!rs_ok) return false;
     if (kkt_check(P, lab, x, y, nl)) return true;
     bool same = true;
 #pragma unroll
@@ -641,22 +800,98 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
   return false;
 }
 
-// Solve one QP.  (xs, zs, ys) is the warm ADMM state (scaled), lab the warm labels.
-// Returns PIADMM_QP_* flags; x_out = unscaled minimiser.
+// OSQP-style adaptive rho (in the scaled space): rho *= sqrt((|r_prim|/|Ax,z|) / (|r_dual|/|Px,A'y,q|)).
+// Returns the proposed factor (1 when inside [0.2, 5]).
 template <int NV>
-__device__ __forceinline__ int qp_solve(const QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
-                        bool warm_lab, int max_inner, int polish_every, double* x_out) {
+__device__ __forceinline__ double rho_ratio(const QP<NV>& P, const double* xs, const double* zs, const double* ys) {
+  constexpr int NR = QP<NV>::NR;
+  double xu[NV], ax[NR], px[NV], w[NR], aty[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xu[v] = P.D[v] * xs[v];
+  A_mul(P, xu, ax);
+  P_mul(P, xu, px);
+#pragma unroll
+  for (int s = 0; s < NR; ++s) w[s] = P.valid[s] ? P.E[s] * ys[s] : 0.0;
+  At_mul(P, w, aty);
+  double rp = 0.0, na = 0.0, rd = 0.0, nd = 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (!P.valid[s]) continue;
+    const double a = P.E[s] * ax[s];
+    rp = fmax(rp, fabs(a - zs[s]));
+    na = fmax(na, fmax(fabs(a), fabs(zs[s])));
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    if (lid() >= P.H) continue;
+    const double ps = P.D[v] * px[v], qs = P.D[v] * P.q[v], as = P.D[v] * aty[v];
+    rd = fmax(rd, fabs(ps + qs + as));
+    nd = fmax(nd, fmax(fabs(ps), fmax(fabs(qs), fabs(as))));
+  }
+  rp = wmax(rp);
+  na = wmax(na);
+  rd = wmax(rd);
+  nd = wmax(nd);
+  const double num = rp / fmax(na, 1e-30), den = rd / fmax(nd, 1e-30);
+  const double ratio = sqrt(num / fmax(den, 1e-30));
+  return (ratio > 5.0 || ratio < 0.2) ? ratio : 1.0;
+}
+
+// Solve one QP.  (xs, zs, ys) is the warm ADMM state (scaled), lab the warm labels.
+// P.rho may be adapted (K^-1 rebuilt in the scratch kscr, stride kld) and persists.
+// Returns PIADMM_QP_* flags; x_out = unscaled minimiser.
+#ifndef PIADMM_ADAPT_EVERY
+#define PIADMM_ADAPT_EVERY 25
+#endif
+constexpr int ADAPT_EVERY = PIADMM_ADAPT_EVERY;
+template <int NV>
+__device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
+                                        bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
+                                        double* x_out, int& n_admm, int& n_pdas) {
   constexpr int NR = QP<NV>::NR;
   double x[NV], y[NR];
   bool ok = false;
-  if (warm_lab) ok = pdas(P, lab, x, y);
-  for (int it = 1; !ok && it <= max_inner; ++it) {
-    admm_iter(P, xs, zs, ys);
-    const bool try_polish = (it % polish_every == 0) && (it <= 20 * polish_every || it % (10 * polish_every) == 0);
-    if (try_polish) {
+  signed char flab[NR];   // labels a PDAS attempt already failed from
 #pragma unroll
-      for (int s = 0; s < NR; ++s) lab[s] = label_scaled(P, s, zs[s] + ys[s] / P.rho);
-      ok = pdas(P, lab, x, y);
+  for (int s = 0; s < NR; ++s) flab[s] = -1;
+  if (warm_lab) {
+#pragma unroll
+    for (int s = 0; s < NR; ++s) flab[s] = lab[s];
+    ok = pdas(P, lab, x, y, n_pdas);
+  }
+  signed char plab[NR];
+#pragma unroll
+  for (int s = 0; s < NR; ++s) plab[s] = -1;
+  for (int it = 1; !ok && it <= max_inner; ++it) {
+    unsigned long long t_a = STAMP_T();
+    admm_iter(P, xs, zs, ys);
+    STAMP_ADD(ST_ADMM, t_a);
+    ++n_admm;
+    if (it % ADAPT_EVERY == 0) {
+      const double f = rho_ratio(P, xs, zs, ys);
+      if (f != 1.0) {
+        P.rho = fmin(fmax(P.rho * f, 1e-6), 1e6);
+        build_K(P, kscr, kld);
+        if (lid() == 0) P.fstate[0] = -1;   // the scratch may have held the cached factor
+        wsync();
+      }
+    }
+    if (it % polish_every == 0) {
+      // polish when the ADMM active-set estimate has not moved since the last check
+      // (or every 8 periods), and never twice from the same labels
+      bool same = true, tried = true;
+#pragma unroll
+      for (int s = 0; s < NR; ++s) {
+        lab[s] = label_scaled(P, s, zs[s] + ys[s] / P.rho);
+        same &= (lab[s] == plab[s]);
+        tried &= (lab[s] == flab[s]);
+        plab[s] = lab[s];
+      }
+      if ((wall(same) || it % (8 * polish_every) == 0) && !wall(tried)) {
+#pragma unroll
+        for (int s = 0; s < NR; ++s) flab[s] = lab[s];
+        ok = pdas(P, lab, x, y, n_pdas);
+      }
     }
   }
   int st = PIADMM_QP_OK;
@@ -687,122 +922,144 @@ __device__ __forceinline__ int qp_solve(const QP<NV>& P, double* xs, double* zs,
   if (!wall(fin)) st |= PIADMM_QP_NAN;
   return st;
 }
-
 // ============================================================ per-step setup
+// Ruiz equilibration of [P A'; A 0] (OSQP-style, RUIZ_ITERS sweeps): fills P.D and P.E.
+template <int NV>
+__device__ __forceinline__ void ruiz(QP<NV>& P) {
+  constexpr int NR = QP<NV>::NR;
+  const int l = lid(), H = P.H;
+  const bool in = l < H;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    P.D[v] = in ? 1.0 : 0.0;
+    P.E[2 * v] = in ? 1.0 : 0.0;
+    P.E[2 * v + 1] = (l < H - 1) ? 1.0 : 0.0;
+  }
+  if constexpr (NV == 2) P.E[4] = P.valid[4] ? 1.0 : 0.0;
+  const double ag[2] = {fabs(P.g1), fabs(P.g2)};
+  for (int it = 0; it < RUIZ_ITERS; ++it) {
+    double cn[NV], rn[NR];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) cn[v] = 0.0;
+    double rh = 0.0;
+    for (int i = 0; i < H; ++i) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const double Di = rdl(P.D[v], i);
+        if (in) cn[v] = fmax(cn[v], fabs(Di * P_entry(P, v, i, l) * P.D[v]));
+        if constexpr (NV == 2) {
+          const double Ehi = rdl(P.E[4], i);
+          // hinge row i (time i+1): entry g_v (i - j)+ on variable j of vehicle v
+          if (in && i > l) cn[v] = fmax(cn[v], Ehi * ag[v] * (double)(i - l) * P.D[v]);
+          if (in && i < l) rh = fmax(rh, ag[v] * (double)(l - i) * Di);
+        }
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const double Eb = P.E[2 * v], Er = P.E[2 * v + 1];
+      cn[v] = fmax(cn[v], fmax(Eb * P.D[v], fmax(Er * P.D[v], shup(Er, 1) * P.D[v])));
+      rn[2 * v] = Eb * P.D[v];
+      rn[2 * v + 1] = Er * fmax(P.D[v], shdn(P.D[v], 1));
+    }
+    if constexpr (NV == 2) rn[4] = rh * P.E[4];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (in) {
+        P.D[v] *= 1.0 / sqrt(clamp_norm(cn[v]));
+        P.E[2 * v] *= 1.0 / sqrt(clamp_norm(rn[2 * v]));
+      }
+      if (l < H - 1) P.E[2 * v + 1] *= 1.0 / sqrt(clamp_norm(rn[2 * v + 1]));
+    }
+    if constexpr (NV == 2) {
+      if (P.valid[4]) P.E[4] *= 1.0 / sqrt(clamp_norm(rn[4]));
+    }
+  }
+}
+
 struct WaveMem {
-  double* scr;
   double* vb;
   int* ib;
 };
 
-// x-step QP of agent a (cost_function_primal, PI_ADMM_class.py:114-135):
-// P = (2 Pnorm + rho |N|) M'M + 2 D2'D2 + 2 Pcost I;  A = [I; D1].
-__device__ __forceinline__ double xP(const Geo& g, double coefAL, double Pcost, int i, int j, int H) {
-  return coefAL * g.mm * TT(i, j, H) + 2.0 * D2D2(i, j, H) + (i == j ? 2.0 * Pcost : 0.0);
+__device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, double rho0, QP<1>& P) {
+  const int l = lid();
+  P.H = H;
+  P.n = H;
+  P.lo[0] = -c.u_max;
+  P.hi[0] = c.u_max;
+  P.lo[1] = -c.du_max;
+  P.hi[1] = c.du_max;
+  P.valid[0] = l < H;
+  P.valid[1] = l < H - 1;
+  P.g1 = P.g2 = 0.0;
+  P.Pcost2 = 2.0 * c.Pcost;
+  P.beta = 0.0;
+  P.rho = rho0;
+  P.sigma = c.admm_sigma;
+  P.alpha = c.admm_alpha;
+  P.tol = c.qp_tol;
+  P.PGt = nullptr;
+  P.GPG = nullptr;
 }
 
-__device__ __forceinline__ void setup_agent(const DevArgs& A, int a, int ai, double* Kx_lds, const WaveMem& wm) {
+// x-step QP of agent a (cost_function_primal, PI_ADMM_class.py:114-135, constraints :172-192):
+// scaling, K_s^-1 (LDS) and P^-1 (LDS) for the whole MPC step.
+__device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, const Geo& g, double* xfac,
+                                            double* Px_lds) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, l = lid();
-  const Geo g = make_geo(A.xt + 3 * a, A.spd[a], c);
-  const double coefAL = 2.0 * c.Pnorm + c.rho * (double)A.nbr_cnt[a];
   const bool in = l < H;
-  // Ruiz equilibration of [P A'; A 0] (OSQP-style)
-  double D = in ? 1.0 : 0.0, Eb = in ? 1.0 : 0.0, Er = (l < H - 1) ? 1.0 : 0.0;
-  for (int it = 0; it < RUIZ_ITERS; ++it) {
-    double cn = 0.0;
-    for (int i = 0; i < H; ++i) {
-      const double Di = rdl(D, i);
-      if (in) cn = fmax(cn, fabs(Di * xP(g, coefAL, c.Pcost, i, l, H) * D));
-    }
-    const double Erm = shup(Er, 1);
-    cn = fmax(cn, fmax(Eb * D, fmax(Er * D, Erm * D)));
-    const double rb = Eb * D;
-    const double rr = Er * fmax(D, shdn(D, 1));
-    if (in) {
-      D *= 1.0 / sqrt(clamp_norm(cn));
-      Eb *= 1.0 / sqrt(clamp_norm(rb));
-    }
-    if (l < H - 1) Er *= 1.0 / sqrt(clamp_norm(rr));
-  }
-  // K_s = D P D + sigma I + rho A_s'A_s  (lane = column j)
-  const double rho = c.admm_rho, sig = c.admm_sigma;
-  for (int i = 0; i < H; ++i) {
-    const double Di = rdl(D, i), Ebi = rdl(Eb, i), Eri = rdl(Er, i);
-    const double Erim = (i >= 1) ? rdl(Er, i - 1) : 0.0;
-    if (in) {
-      double v = Di * xP(g, coefAL, c.Pcost, i, l, H) * D;
-      double ata = 0.0;
-      if (i == l) ata = Ebi * Ebi + Eri * Eri + Erim * Erim;
-      else if (l == i + 1) ata = -Eri * Eri;
-      else if (l == i - 1) ata = -Erim * Erim;
-      v += rho * Di * D * ata + (i == l ? sig : 0.0);
-      wm.scr[i * LD + l] = v;
-    }
-  }
-  wsync();
-  gj_invert(wm.scr, H);
+  P.coefP = 2.0 * c.Pnorm + c.rho * (double)A.nbr_cnt[a];
+  P.mm[0] = g.mm;
+  ruiz(P);
+  build_K(P, xfac, HMAX + 1);
   for (int i = 0; i < H; ++i)
-    if (in) Kx_lds[i * H + l] = wm.scr[i * LD + l];
+    if (in) xfac[i * (HMAX + 1) + l] = P_entry(P, 0, i, l);
   wsync();
-  // P^-1 (unscaled) for the polish
+  gj_invert(xfac, H, HMAX + 1);
   for (int i = 0; i < H; ++i)
-    if (in) wm.scr[i * LD + l] = xP(g, coefAL, c.Pcost, i, l, H);
-  wsync();
-  gj_invert(wm.scr, H);
-  double* Pi = A.Pinv_x + (size_t)a * H * H;
-  for (int i = 0; i < H; ++i)
-    if (in) Pi[i * H + l] = wm.scr[i * LD + l];
-  double* sc = A.sc_x + (size_t)a * 4 * HMAX;
-  if (l < HMAX) {
-    sc[0 * HMAX + l] = D;
-    sc[1 * HMAX + l] = Eb;
-    sc[2 * HMAX + l] = Er;
-  }
+    if (in) Px_lds[i * H + l] = xfac[i * (HMAX + 1) + l];
   wsync();
 }
 
-// Pair (z-step) QP of cost_function_edge (PI_ADMM_class.py:145-169), heading frozen
-// at xt (MATLAB symbolic dynamic_update_edge, ADMM_CVX_..._PI_antiwindup.m:378-397).
-// Variables [uh_1; uh_2]; P = blockdiag(rho M_v'M_v + 2 Pcost I); hinge rows
-// G_k = [g1 T(k+1,.), g2 T(k+1,.)],  h_k = D^2 + |dbar|^2 - 2 dbar'(c2 - c1)_{k+1}.
-__device__ __forceinline__ double eP(double mmv, double rho, double Pcost, int i, int j, int H) {
-  return rho * mmv * TT(i, j, H) + (i == j ? 2.0 * Pcost : 0.0);
-}
-
-__device__ __forceinline__ void setup_pair(const DevArgs& A, int e, int a1, const double* seeds, double* Ke_lds,
-                           const WaveMem& wm) {
+// Pair (z-step) QP of cost_function_edge (PI_ADMM_class.py:145-169), heading frozen at
+// xt (MATLAB symbolic dynamic_update_edge, ADMM_CVX_..._PI_antiwindup.m:378-397).
+// Variables [uh_1; uh_2]; hinge rows G_k = [g1 T(k+1,.), g2 T(k+1,.)],
+// h_k = D^2 + |dbar|^2 - 2 dbar'(c2 - c1)_{k+1}.  Builds the polish tables P^-1 (HBM),
+// PGt = P^-1 G' (HBM), GPG = G P^-1 G' (HBM) and K_s^-1 (LDS).
+__device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, const Geo& g1, const Geo& g2,
+                                           double c1x, double c1y, double c2x, double c2y, const double* seeds,
+                                           double* scr, double* Ke_lds) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, n = 2 * H, l = lid();
   const bool in = l < H;
-  const int a2 = a1 + 1;
-  const Geo g1 = make_geo(A.xt + 3 * a1, A.spd[a1], c);
-  const Geo g2 = make_geo(A.xt + 3 * a2, A.spd[a2], c);
-  double c1x, c1y, c2x, c2y;
-  affine_c(g1, c.dt, H, c1x, c1y);
-  affine_c(g2, c.dt, H, c2x, c2y);
   const double dbx = seeds[2] - seeds[0], dby = seeds[3] - seeds[1];
   const double dd = dbx * dbx + dby * dby;
-  const double gg1 = -2.0 * (dbx * g1.ax + dby * g1.ay);
-  const double gg2 = 2.0 * (dbx * g2.ax + dby * g2.ay);
+  P.g1 = -2.0 * (dbx * g1.ax + dby * g1.ay);
+  P.g2 = 2.0 * (dbx * g2.ax + dby * g2.ay);
   const double Dsq = c.dis_thres * c.dis_thres;
   const double h_time = Dsq + dd - 2.0 * (dbx * (c2x - c1x) + dby * (c2y - c1y));
-  const double h0 = shdn(h_time, 1);                 // hinge lane k <-> time k+1
-  const bool hv = (l >= 1) && in && (gg1 != 0.0 || gg2 != 0.0);
+  P.lo[4] = shdn(h_time, 1);                 // hinge lane k <-> time k+1
+  P.hi[4] = INFINITY;
+  P.valid[4] = (l >= 1) && in && (P.g1 != 0.0 || P.g2 != 0.0);
+  if (!P.valid[4]) P.lo[4] = 0.0;
+  P.coefP = c.rho;
+  P.mm[0] = g1.mm;
+  P.mm[1] = g2.mm;
 
-  // ---- P_v^-1 blocks, PGt = P^-1 G', GPG = G P^-1 G'  (PGt staged in Ke region)
+  // ---- P_v^-1 blocks, PGt = P^-1 G', GPG = G P^-1 G'  (PGt staged in the Ke region)
   double* PGt_l = Ke_lds;          // H x n (temporarily)
   double* Pi = A.Pinv_e + (size_t)e * n * n;
   for (int v = 0; v < 2; ++v) {
-    const double mmv = v == 0 ? g1.mm : g2.mm;
-    const double gv = v == 0 ? gg1 : gg2;
+    const double gv = v == 0 ? P.g1 : P.g2;
     for (int i = 0; i < H; ++i)
-      if (in) wm.scr[i * LD + l] = eP(mmv, c.rho, c.Pcost, i, l, H);
+      if (in) scr[i * LD + l] = P_entry(P, v, i, l);
     wsync();
-    gj_invert(wm.scr, H);
+    gj_invert(scr, H, LD);
     for (int i = 0; i < H; ++i) {
       if (in) {
-        Pi[(v * H + i) * n + v * H + l] = wm.scr[i * LD + l];
+        Pi[(v * H + i) * n + v * H + l] = scr[i * LD + l];
         Pi[(v * H + i) * n + (1 - v) * H + l] = 0.0;
       }
     }
@@ -810,12 +1067,11 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, int a1, cons
     double acc1 = 0.0, Y = 0.0;
     for (int k = 0; k < H; ++k) {
       if (in) PGt_l[k * n + v * H + l] = gv * Y;
-      if (in) acc1 += wm.scr[l * LD + k];
+      if (in) acc1 += scr[l * LD + k];
       Y += acc1;
     }
     wsync();
   }
-  // GPG[a][b] = sum_i G_a[i] PGt[b][i]; lane b
   {
     double* Gg = A.GPG + (size_t)e * H * H;
     double* Pg = A.PGt + (size_t)e * H * n;
@@ -823,115 +1079,18 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, int a1, cons
     double B = 0.0, Z = 0.0;
     for (int a = 0; a < H; ++a) {
       if (in) Gg[a * H + l] = Z;
-      const double wa = gg1 * PGt_l[b * n + a] + gg2 * PGt_l[b * n + H + a];
+      const double wa = P.g1 * PGt_l[b * n + a] + P.g2 * PGt_l[b * n + H + a];
       B += wa;
       Z += B;
     }
     for (int k = 0; k < H; ++k) {
-      Pg[k * n + l] = PGt_l[k * n + l];
-      if (l + 64 < n) Pg[k * n + l + 64] = PGt_l[k * n + l + 64];
+      if (l < n) Pg[k * n + l] = PGt_l[k * n + l];
     }
     wsync();
   }
-  // ---- Ruiz equilibration
-  double D1 = in ? 1.0 : 0.0, D2 = D1;
-  double Eb1 = D1, Eb2 = D1, Er1 = (l < H - 1) ? 1.0 : 0.0, Er2 = Er1, Eh = hv ? 1.0 : 0.0;
-  const double ag1 = fabs(gg1), ag2 = fabs(gg2);
-  for (int it = 0; it < RUIZ_ITERS; ++it) {
-    double cn1 = 0.0, cn2 = 0.0, rh = 0.0;
-    for (int i = 0; i < H; ++i) {
-      const double D1i = rdl(D1, i), D2i = rdl(D2, i), Ehi = rdl(Eh, i);
-      if (in) {
-        cn1 = fmax(cn1, fabs(D1i * eP(g1.mm, c.rho, c.Pcost, i, l, H) * D1));
-        cn2 = fmax(cn2, fabs(D2i * eP(g2.mm, c.rho, c.Pcost, i, l, H) * D2));
-        // hinge row i (time i+1) has entry g_v (i - j)+ on variable j
-        if (i > l) {
-          cn1 = fmax(cn1, Ehi * ag1 * (double)(i - l) * D1);
-          cn2 = fmax(cn2, Ehi * ag2 * (double)(i - l) * D2);
-        }
-        // hinge row at this lane: entries on variables j < l
-        if (i < l) rh = fmax(rh, fmax(ag1 * (double)(l - i) * D1i, ag2 * (double)(l - i) * D2i));
-      }
-    }
-    cn1 = fmax(cn1, fmax(Eb1 * D1, fmax(Er1 * D1, shup(Er1, 1) * D1)));
-    cn2 = fmax(cn2, fmax(Eb2 * D2, fmax(Er2 * D2, shup(Er2, 1) * D2)));
-    const double rb1 = Eb1 * D1, rb2 = Eb2 * D2;
-    const double rr1 = Er1 * fmax(D1, shdn(D1, 1)), rr2 = Er2 * fmax(D2, shdn(D2, 1));
-    rh *= Eh;
-    if (in) {
-      D1 *= 1.0 / sqrt(clamp_norm(cn1));
-      D2 *= 1.0 / sqrt(clamp_norm(cn2));
-      Eb1 *= 1.0 / sqrt(clamp_norm(rb1));
-      Eb2 *= 1.0 / sqrt(clamp_norm(rb2));
-    }
-    if (l < H - 1) {
-      Er1 *= 1.0 / sqrt(clamp_norm(rr1));
-      Er2 *= 1.0 / sqrt(clamp_norm(rr2));
-    }
-    if (hv) Eh *= 1.0 / sqrt(clamp_norm(rh));
-  }
-  // ---- K_s (n x n), lane = column cidx
-  const double rho = c.admm_rho, sig = c.admm_sigma;
-  {
-    const int vc = (l < H) ? 0 : 1;
-    const int jc = (l < H) ? l : l - H;
-    const bool incol = l < n;
-    const int srcl = (jc < H) ? jc : 0;
-    const double D1s = __shfl(D1, srcl), D2s = __shfl(D2, srcl);
-    const double Dc = vc == 0 ? D1s : D2s;
-    const double gc = vc == 0 ? gg1 : gg2;
-    const double mmc = vc == 0 ? g1.mm : g2.mm;
-    const double Eh2 = Eh * Eh;
-    for (int r = 0; r < n; ++r) {
-      const int vr = r / H, ir = r - vr * H;
-      const double Dr = vr == 0 ? rdl(D1, ir) : rdl(D2, ir);
-      const double Ebr = vr == 0 ? rdl(Eb1, ir) : rdl(Eb2, ir);
-      const double Err = vr == 0 ? rdl(Er1, ir) : rdl(Er2, ir);
-      const double Errm = (ir >= 1) ? (vr == 0 ? rdl(Er1, ir - 1) : rdl(Er2, ir - 1)) : 0.0;
-      const double gr = vr == 0 ? gg1 : gg2;
-      // hinge part: sum_k Eh_k^2 (k - ir)+ (k - jc)+
-      double hs = 0.0;
-      for (int k = 1; k < H; ++k) {
-        const double e2 = rdl(Eh2, k);
-        if (k > ir && k > jc) hs += e2 * (double)(k - ir) * (double)(k - jc);
-      }
-      if (incol) {
-        double v = 0.0;
-        double ata = gr * gc * hs;
-        if (vr == vc) {
-          v = Dr * eP(mmc, c.rho, c.Pcost, ir, jc, H) * Dc;
-          if (ir == jc) ata += Ebr * Ebr + Err * Err + Errm * Errm;
-          else if (jc == ir + 1) ata += -Err * Err;
-          else if (jc == ir - 1) ata += -Errm * Errm;
-        }
-        v += rho * Dr * Dc * ata + (r == l ? sig : 0.0);
-        wm.scr[r * LD + l] = v;
-      }
-    }
-    wsync();
-    gj_invert(wm.scr, n);
-    for (int r = 0; r < n; ++r)
-      if (incol) Ke_lds[r * n + l] = wm.scr[r * LD + l];
-    wsync();
-  }
-  double* sc = A.sc_e + (size_t)e * 8 * HMAX;
-  if (l < HMAX) {
-    sc[0 * HMAX + l] = D1;
-    sc[1 * HMAX + l] = D2;
-    sc[2 * HMAX + l] = Eb1;
-    sc[3 * HMAX + l] = Er1;
-    sc[4 * HMAX + l] = Eb2;
-    sc[5 * HMAX + l] = Er2;
-    sc[6 * HMAX + l] = Eh;
-    sc[7 * HMAX + l] = hv ? h0 : 0.0;
-  }
-  if (l == 0) {
-    A.gcoef_e[4 * e + 0] = gg1;
-    A.gcoef_e[4 * e + 1] = gg2;
-  }
-  wsync();
+  ruiz(P);
+  build_K(P, scr, LD);
 }
-
 // ============================================================ the MPC-step kernel
 struct CompLds {
   double *pos, *xt, *seed, *u, *hat, *lam, *S, *D, *last, *sc;
@@ -939,7 +1098,7 @@ struct CompLds {
 
 __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   extern __shared__ double lds[];
-  __shared__ int s_int[NW * 128];
+  __shared__ int s_int[NW * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1;
   const int ci = blockIdx.x;
@@ -948,12 +1107,16 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   const int na = A.comp_ptr[ci + 1] - a0;
   const int e = A.comp_edge[ci];
 
-  double* Kx = lds;
-  double* Ke = Kx + 2 * H * H;
-  double* scr_all = Ke + 4 * H * H;
-  double* vec_all = scr_all + NW * 64 * LD;
+  // ---- LDS carve (lds_bytes() in piadmm_internal.h)
+  double* Kx = lds;                                      // 2 x H*H   agent K_s^-1
+  double* Px = Kx + 2 * H * H;                           // 2 x H*H   agent P^-1
+  double* Ke = Px + 2 * H * H;                           // 4*H*H     pair K_s^-1
+  double* scr = Ke + 4 * H * H;                          // 64 x LD   pair scratch (wave 0)
+  double* xfac_all = scr + 64 * LD;                      // NW x HMAX x (HMAX+1)
+  double* vec_all = xfac_all + NW * HMAX * (HMAX + 1);   // NW x 512
+  double* fdiag_all = vec_all + NW * 512;                // NW x 256
   CompLds S;
-  S.pos = vec_all + NW * 512;
+  S.pos = fdiag_all + NW * 256;
   S.xt = S.pos + 4 * H1;
   S.seed = S.xt + 6;
   S.u = S.seed + 4;
@@ -963,7 +1126,18 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   S.D = S.S + 4 * H1;
   S.last = S.D + 4 * H1;
   S.sc = S.last + 4 * H1;
-  WaveMem wm{scr_all + w * 64 * LD, vec_all + w * 512, s_int + w * 128};
+  WaveMem wm{vec_all + w * 512, s_int + w * 272};
+  double* xfac = xfac_all + w * HMAX * (HMAX + 1);
+  double* xdiag = fdiag_all + w * 256;
+  double* zdiag = xdiag + 128;
+  int* xids = wm.ib;
+  int* zids = wm.ib + 128;
+  int* xfs = wm.ib + 256;
+  int* zfs = wm.ib + 257;
+  if (l == 0) {
+    xfs[0] = -1;
+    zfs[0] = -1;
+  }
 
   // ---- seeds (casadi/main.py:48-49) and zero per-step state (:52-63)
   if ((int)threadIdx.x < na) {
@@ -975,20 +1149,13 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     S.seed[2 * threadIdx.x + 0] = around(x + c.dt * s * cos(th), c.round_decimals);
     S.seed[2 * threadIdx.x + 1] = around(y + c.dt * s * sin(th), c.round_decimals);
   }
-  for (int i = threadIdx.x; i < 4 * H1 * 6 + 2 * H; i += blockDim.x) {
-    // pos, hat, lam, S, D, last are contiguous with u in between: clear pos and hat..last
-    if (i < 4 * H1) S.pos[i] = 0.0;
-    else if (i < 4 * H1 + 20 * H1) S.hat[i - 4 * H1] = 0.0;
-  }
+  for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) S.pos[i] = 0.0;
+  for (int i = threadIdx.x; i < 20 * H1; i += blockDim.x) S.hat[i] = 0.0;   // hat, lam, S, D, last
   for (int i = threadIdx.x; i < 32; i += blockDim.x) S.sc[i] = 0.0;
   __syncthreads();
+  unsigned long long t_k = STAMP_T();
 
-  // ---- per-step QP setup
-  if (w < na) setup_agent(A, a0 + w, w, Kx + w * H * H, wm);
-  if (w == 0 && e >= 0) setup_pair(A, e, a0, S.seed, Ke, wm);
-  __syncthreads();
-
-  // ---- QP descriptors (registers of the owning wave, live for the whole step)
+  // ---- per-step QP setup (registers of the owning wave stay live for the whole step)
   QP<1> qx;
   double xs_x[1] = {0.0}, zs_x[2] = {0.0, 0.0}, ys_x[2] = {0.0, 0.0};
   signed char lab_x[2] = {0, 0};
@@ -996,36 +1163,25 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   int status_x = 0;
   int nnb = 0;
   Geo gx;
+  double cx_own = 0.0, cy_own = 0.0;
   if (w < na) {
+    unsigned long long t0 = STAMP_T();
     const int a = a0 + w;
-    const double* sc = A.sc_x + (size_t)a * 4 * HMAX;
-    const int li = l < HMAX ? l : 0;
-    qx.H = H;
-    qx.n = H;
-    qx.D[0] = (l < H) ? sc[li] : 0.0;
-    qx.E[0] = (l < H) ? sc[HMAX + li] : 0.0;
-    qx.E[1] = (l < H - 1) ? sc[2 * HMAX + li] : 0.0;
-    qx.lo[0] = -c.u_max;
-    qx.hi[0] = c.u_max;
-    qx.lo[1] = -c.du_max;
-    qx.hi[1] = c.du_max;
-    qx.valid[0] = l < H;
-    qx.valid[1] = l < H - 1;
-    qx.g1 = qx.g2 = 0.0;
-    qx.beta = 0.0;
-    qx.rho = c.admm_rho;
-    qx.sigma = c.admm_sigma;
-    qx.alpha = c.admm_alpha;
-    qx.tol = c.qp_tol;
-    qx.K = Kx + w * H * H;
-    qx.Pinv = A.Pinv_x + (size_t)a * H * H;
-    qx.PGt = nullptr;
-    qx.GPG = nullptr;
-    qx.vb = wm.vb;
-    qx.scr = wm.scr;
-    qx.ib = wm.ib;
-    nnb = A.nbr_cnt[a];
     gx = make_geo(S.xt + 3 * w, A.spd[a], c);
+    affine_c(gx, c.dt, H, cx_own, cy_own);
+    qp_common(c, H, A.rho_x[a], qx);
+    qx.K = Kx + w * H * H;
+    qx.Pinv = Px + w * H * H;
+    qx.vb = wm.vb;
+    qx.fac = xfac;
+    qx.fdiag = xdiag;
+    qx.ib = xids;
+    qx.fstate = xfs;
+    qx.fld = HMAX + 1;
+    qx.mmax = HMAX;
+    nnb = A.nbr_cnt[a];
+    setup_agent(A, a, qx, gx, xfac, Px + w * H * H);
+    STAMP_ADD(ST_SETUP_X, t0);
   }
   QP<2> qe;
   double xs_e[2] = {0.0, 0.0}, zs_e[5] = {0, 0, 0, 0, 0}, ys_e[5] = {0, 0, 0, 0, 0};
@@ -1033,32 +1189,25 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   bool warm_e = false;
   int status_e = 0;
   Geo ge1, ge2;
+  double c1x = 0.0, c1y = 0.0, c2x = 0.0, c2y = 0.0;
   if (w == 0 && e >= 0) {
-    const double* sc = A.sc_e + (size_t)e * 8 * HMAX;
-    const int li = l < HMAX ? l : 0;
+    unsigned long long t0 = STAMP_T();
     const bool in = l < H;
+    ge1 = make_geo(S.xt + 0, A.spd[a0], c);
+    ge2 = make_geo(S.xt + 3, A.spd[a0 + 1], c);
+    affine_c(ge1, c.dt, H, c1x, c1y);
+    affine_c(ge2, c.dt, H, c2x, c2y);
     qe.H = H;
     qe.n = 2 * H;
-    qe.D[0] = in ? sc[0 * HMAX + li] : 0.0;
-    qe.D[1] = in ? sc[1 * HMAX + li] : 0.0;
-    qe.E[0] = in ? sc[2 * HMAX + li] : 0.0;
-    qe.E[1] = (l < H - 1) ? sc[3 * HMAX + li] : 0.0;
-    qe.E[2] = in ? sc[4 * HMAX + li] : 0.0;
-    qe.E[3] = (l < H - 1) ? sc[5 * HMAX + li] : 0.0;
-    qe.E[4] = in ? sc[6 * HMAX + li] : 0.0;
     qe.lo[0] = qe.lo[2] = -c.u_max;
     qe.hi[0] = qe.hi[2] = c.u_max;
     qe.lo[1] = qe.lo[3] = -c.du_max;
     qe.hi[1] = qe.hi[3] = c.du_max;
-    qe.lo[4] = in ? sc[7 * HMAX + li] : 0.0;
-    qe.hi[4] = INFINITY;
     qe.valid[0] = qe.valid[2] = in;
     qe.valid[1] = qe.valid[3] = l < H - 1;
-    qe.valid[4] = in && qe.E[4] != 0.0;
-    qe.g1 = A.gcoef_e[4 * e + 0];
-    qe.g2 = A.gcoef_e[4 * e + 1];
+    qe.Pcost2 = 2.0 * c.Pcost;
     qe.beta = c.beta;
-    qe.rho = c.admm_rho;
+    qe.rho = A.rho_e[e];
     qe.sigma = c.admm_sigma;
     qe.alpha = c.admm_alpha;
     qe.tol = c.qp_tol;
@@ -1067,50 +1216,69 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     qe.PGt = A.PGt + (size_t)e * 2 * H * H;
     qe.GPG = A.GPG + (size_t)e * H * H;
     qe.vb = wm.vb;
-    qe.scr = wm.scr;
-    qe.ib = wm.ib;
-    ge1 = make_geo(S.xt + 0, A.spd[a0], c);
-    ge2 = make_geo(S.xt + 3, A.spd[a0 + 1], c);
+    qe.fac = scr;
+    qe.fdiag = zdiag;
+    qe.ib = zids;
+    qe.fstate = zfs;
+    qe.fld = LD;
+    qe.mmax = WAVE;
+    setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke);
+    STAMP_ADD(ST_SETUP_Z, t0);
   }
+  __syncthreads();
 
   const bool nonlin_pos = c.pos_model != 0;
   const double thr = c.collide_sq_thres ? c.dis_thres * c.dis_thres : c.dis_thres;
   int flag = 0, aliased = 0, iters = 0;
+  int n_xqp = 0, n_zqp = 0, n_admm_x = 0, n_admm_z = 0, n_pdas_x = 0, n_pdas_z = 0, n_inexact = 0;
   bool act = false;
   double dis_chk = NAN;
   double* resid = A.resid + (size_t)ci * c.max_outer * 2;
+  // reference positions of the own agent at time lanes (fixed for the step)
+  double rx_own = 0.0, ry_own = 0.0;
+  if (w < na && l <= H) {
+    const double* rp = A.ref + (size_t)(a0 + w) * 2 * A.T;
+    rx_own = rp[t + l];
+    ry_own = rp[A.T + t + l];
+  }
 
   for (int it = 0; it < c.max_outer; ++it) {
     iters = it + 1;
     // -------- x-step: every agent of the component (casadi/main.py:81-106)
     if (w < na) {
+      unsigned long long t_xs = STAMP_T();
       const int a = a0 + w;
-      double cx, cy;
-      affine_c(gx, c.dt, H, cx, cy);
       const bool tl = l <= H;
-      const double* rp = A.ref + (size_t)a * 2 * A.T;
-      const double rx = tl ? rp[t + l] : 0.0;
-      const double ry = tl ? rp[A.T + t + l] : 0.0;
-      double vx = 2.0 * c.Pnorm * (cx - rx), vy = 2.0 * c.Pnorm * (cy - ry);
+      double vx = 2.0 * c.Pnorm * (cx_own - rx_own), vy = 2.0 * c.Pnorm * (cy_own - ry_own);
       if (nnb > 0 && e >= 0 && tl) {
         const int d = w;   // agent local 0 owns hat_{v1 v2} (dir 0), agent 1 dir 1
-        vx = vx + c.rho * (cx - S.hat[(d * 2 + 0) * H1 + l] + S.lam[(d * 2 + 0) * H1 + l]);
-        vy = vy + c.rho * (cy - S.hat[(d * 2 + 1) * H1 + l] + S.lam[(d * 2 + 1) * H1 + l]);
+        vx = vx + c.rho * (cx_own - S.hat[(d * 2 + 0) * H1 + l] + S.lam[(d * 2 + 0) * H1 + l]);
+        vy = vy + c.rho * (cy_own - S.hat[(d * 2 + 1) * H1 + l] + S.lam[(d * 2 + 1) * H1 + l]);
       }
       const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
       const double qv = Tt_apply(shdn(wt, 1));
       qx.q[0] = (l < H) ? qv : 0.0;
+      STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
-      status_x |= qp_solve(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, ustar);
+      unsigned long long t_q = STAMP_T();
+      const int stx = qp_solve(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+                               HMAX + 1, ustar, n_admm_x, n_pdas_x);
+      STAMP_ADD(ST_XQP, t_q);
+      status_x |= stx;
+      ++n_xqp;
+      n_inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
       warm_x = true;
       const double u = around(ustar[0], c.round_decimals);
       double px, py, pth;
+      unsigned long long t_r = STAMP_T();
       rollout(S.xt + 3 * w, A.spd[a], (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+      STAMP_ADD(ST_XROLL, t_r);
       if (l <= H) {
         S.pos[(w * 2 + 0) * H1 + l] = px;
         S.pos[(w * 2 + 1) * H1 + l] = py;
       }
       if (l < H) S.u[w * H + l] = u;
+      STAMP_ADD(ST_XSTEP, t_xs);
     }
     __syncthreads();
     // -------- collision graph (casadi/main.py:110-118), computed by every wave
@@ -1128,10 +1296,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     flag = 1;
     // -------- z-step + dual update on the colliding pair (casadi/main.py:121-162)
     if (act && w == 0) {
+      unsigned long long t_z = STAMP_T();
       const bool tl = l <= H;
-      double c1x, c1y, c2x, c2y;
-      affine_c(ge1, c.dt, H, c1x, c1y);
-      affine_c(ge2, c.dt, H, c2x, c2y);
       double bx[2], by[2];
       bx[0] = tl ? S.pos[0 * H1 + l] + S.lam[0 * H1 + l] - c1x : 0.0;
       by[0] = tl ? S.pos[1 * H1 + l] + S.lam[1 * H1 + l] - c1y : 0.0;
@@ -1143,7 +1309,13 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
       qe.q[0] = (l < H) ? -c.rho * q1 : 0.0;
       qe.q[1] = (l < H) ? -c.rho * q2 : 0.0;
       double uh[2];
-      status_e |= qp_solve(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every, uh);
+      unsigned long long t_zq = STAMP_T();
+      const int ste = qp_solve(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every, scr, LD, uh,
+                               n_admm_z, n_pdas_z);
+      STAMP_ADD(ST_ZQP, t_zq);
+      status_e |= ste;
+      ++n_zqp;
+      n_inexact += (ste & PIADMM_QP_INEXACT) ? 1 : 0;
       warm_e = true;
       // hat positions: nonlinear rollout of the rounded pair controls (:153-158)
       double hx[2], hy[2], hth;
@@ -1213,6 +1385,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
         S.sc[1] = aliased ? 0.0 : 2.0 * sqrt(ss);
         S.sc[2] = rdl(dist, 1);
       }
+      STAMP_ADD(ST_ZSTEP, t_z);
     }
     __syncthreads();
     // -------- termination (casadi/main.py:164-181; MATLAB :191-210)
@@ -1234,7 +1407,29 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     __syncthreads();
   }
   __syncthreads();
+  STAMP_ADD(ST_KERNEL, t_k);
 
+  // ---- work counters (accumulated across launches; one workgroup owns row ci)
+  {
+    __shared__ int s_cnt[NW][8];
+    if (l == 0) {
+      s_cnt[w][0] = n_xqp; s_cnt[w][1] = n_zqp; s_cnt[w][2] = n_admm_x; s_cnt[w][3] = n_admm_z;
+      s_cnt[w][4] = n_pdas_x; s_cnt[w][5] = n_pdas_z; s_cnt[w][6] = n_inexact; s_cnt[w][7] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long* cn = A.counters + (size_t)ci * 8;
+      cn[0] += (unsigned long long)iters;
+      for (int k = 0; k < 6; ++k) {
+        unsigned long long sum = 0;
+        for (int ww = 0; ww < NW; ++ww) sum += (unsigned long long)s_cnt[ww][k];
+        cn[k + 1] += sum;
+      }
+      unsigned long long inex = 0;
+      for (int ww = 0; ww < NW; ++ww) inex += (unsigned long long)s_cnt[ww][6];
+      cn[7] += inex;
+    }
+  }
   // ---- outputs and propagation (casadi/main.py:185-192)
   if (threadIdx.x == 0) {
     A.iters[ci] = iters;
@@ -1253,8 +1448,12 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
       A.xt[3 * a + 1] = py;
       A.xt[3 * a + 2] = pth;
     }
-    if (l == 0) A.status[a] = status_x;
+    if (l == 0) {
+      A.status[a] = status_x;
+      A.rho_x[a] = qx.rho;
+    }
   }
+  if (w == 0 && e >= 0 && l == 0) A.rho_e[e] = qe.rho;
   if (e >= 0) {
     for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) {
       A.hat[(size_t)e * 4 * H1 + i] = S.hat[i];
@@ -1267,6 +1466,13 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
 int launch_mpc_step(const DevArgs& a, int t, hipStream_t s) {
   const size_t sh = lds_bytes(a.cfg.H);
   static bool attr = false;
+#ifdef PIADMM_STAMPS
+  static unsigned long long* last = nullptr;
+  if (a.stamps != last) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &a.stamps, sizeof(void*)) != hipSuccess) return -1;
+    last = a.stamps;
+  }
+#endif
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k_mpc_step, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sh) != hipSuccess)

@@ -48,15 +48,22 @@ struct DevArgs {
   double* ws_e;             // E*12*HMAX  (xs0, xs1, zs0..4, ys0..4)
   signed char* lab_e;       // E*5*HMAX
   double* gcoef_e;          // E*4        (g1, g2, spare)
+  unsigned long long* counters;  // C*8  accumulated work counters (see piadmm_get_counters)
+  unsigned long long* stamps;    // C*32 phase cycle sums (diagnostic build -DPIADMM_STAMPS only)
+  double* rho_x;            // N   ADMM penalty per agent QP (adapted, persists across steps)
+  double* rho_e;            // E   ADMM penalty per pair QP
 };
 
-// LDS bytes needed by one workgroup for horizon H.
+// LDS bytes needed by one workgroup for horizon H (must match the carve in k_mpc_step).
 inline size_t lds_bytes(int H) {
   size_t d = 0;
   d += 2 * (size_t)H * H;          // agent K_s^-1 (2 agents)
+  d += 2 * (size_t)H * H;          // agent P^-1 (2 agents)
   d += 4 * (size_t)H * H;          // pair K_s^-1 (2H x 2H)
-  d += NW * 64 * LD;               // per-wave matrix scratch
+  d += 64 * LD;                    // pair matrix scratch (wave 0)
+  d += NW * HMAX * (HMAX + 1);     // per-wave x-step scratch / Cholesky factor
   d += NW * 512;                   // per-wave vector buffers
+  d += NW * 256;                   // per-wave factor diagonals (x, z)
   size_t H1 = H + 1;
   d += 2 * 2 * H1;                 // pos_old
   d += 2 * 3 + 2 * 2 + 2 * H;      // xt, seeds, u

@@ -67,6 +67,10 @@ SYMBOLS = [
     ("piadmm_time_steps", c_i32, [_H, c_i32, c_i32, _P(ctypes.c_float)]),
     ("piadmm_get_state", c_i32, [_H, _dp, _dp, _dp, _dp, _dp, _P(ctypes.c_uint8), _ip]),
     ("piadmm_n_components", c_i32, [_H]),
+    ("piadmm_get_counters", c_i32, [_H, _P(ctypes.c_uint64)]),
+    ("piadmm_reset_counters", c_i32, [_H]),
+    ("piadmm_get_component_counters", c_i32, [_H, _P(ctypes.c_uint64), c_i32]),
+    ("piadmm_debug_stamps", c_i32, [_H, _P(ctypes.c_uint64), c_i32]),
 ]
 
 _lib = None
@@ -81,7 +85,8 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # PIADMM_LIB selects another build of the same library (e.g. the stamps build)
+    p = path or os.environ.get("PIADMM_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise PiadmmError(f"HIP library not built: {p} (run `make -C distributed-local-planner-pi-admm_amd`)")
     lib = ctypes.CDLL(p)

@@ -103,6 +103,21 @@ class PI_ADMM_MI355X:
         self._check(self.lib.piadmm_time_steps(self._h, t0, n_steps, ctypes.byref(ms)))
         return float(ms.value)
 
+    COUNTER_NAMES = ("outer_iters", "x_qps", "z_qps", "admm_x", "admm_z", "pdas_x", "pdas_z", "inexact")
+
+    def counters(self) -> dict:
+        buf = (ctypes.c_uint64 * 8)()
+        self._check(self.lib.piadmm_get_counters(self._h, buf))
+        return dict(zip(self.COUNTER_NAMES, (int(v) for v in buf)))
+
+    def component_counters(self) -> np.ndarray:
+        buf = (ctypes.c_uint64 * (8 * self.C))()
+        self._check(self.lib.piadmm_get_component_counters(self._h, buf, 8 * self.C))
+        return np.array(buf, dtype=np.int64).reshape(self.C, 8)
+
+    def reset_counters(self):
+        self._check(self.lib.piadmm_reset_counters(self._h))
+
     def set_xt(self, xt: np.ndarray):
         xt = np.ascontiguousarray(xt, np.float64)
         self._check(self.lib.piadmm_set_xt(self._h, _lib.dptr(xt)))

@@ -127,6 +127,20 @@ int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_o
 
 int32_t piadmm_n_components(piadmm_handle_t h);
 
+/* Work counters accumulated over all steps since the last reset, summed over
+ * components: [0] outer iterations executed (per component), [1] x-step QPs,
+ * [2] z-step (pair) QPs, [3] ADMM iterations in x-step QPs, [4] ADMM iterations
+ * in pair QPs, [5] PDAS reduced KKT solves (x), [6] PDAS reduced solves (pair),
+ * [7] QPs that ended without a certified polish (PIADMM_QP_INEXACT). */
+int32_t piadmm_get_counters(piadmm_handle_t h, uint64_t* out8);
+int32_t piadmm_reset_counters(piadmm_handle_t h);
+/* The same counters per component (C x 8 uint64, n >= 8*C). */
+int32_t piadmm_get_component_counters(piadmm_handle_t h, uint64_t* out, int32_t n);
+
+/* Diagnostic builds (-DPIADMM_STAMPS, libpiadmm_stamps.so) only: per-component
+ * cycle sums of the kernel phases (C x 32 uint64); PIADMM_E_STATE otherwise. */
+int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif

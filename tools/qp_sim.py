@@ -58,6 +58,10 @@ def classify(gq, w, rho):
     return s
 
 
+REG = [1e-13, 1]   # relative regularisation of S, refinement steps
+DEP_TOL = [1e-10]  # relative pivot below which a working-set row counts as dependent
+
+
 def reduced_solve(gq, Pinv, sets):
     """Equality-constrained QP of a label vector via the Schur complement on P^-1."""
     hm = gq.hinge
@@ -73,14 +77,25 @@ def reduced_solve(gq, Pinv, sets):
     b = np.where(gq.hinge[rows], gq.l[rows], np.where(sets[rows] == LOWER, gq.l[rows], gq.u[rows]))
     V = Pinv @ AW.T
     S = AW @ V
-    try:
-        L = np.linalg.cholesky(S + 1e-13 * np.trace(S) / rows.size * np.eye(rows.size))
-    except np.linalg.LinAlgError:
-        return x0, y, False
+    # Cholesky that drops rows linearly dependent on the earlier ones (pivot collapse)
+    m = rows.size
+    L = np.zeros((m, m))
+    keep = np.ones(m, bool)
+    for k in range(m):
+        d = S[k, k] - L[k, :k] @ L[k, :k]
+        if d <= DEP_TOL[0] * S[k, k]:
+            keep[k] = False
+            continue
+        L[k, k] = np.sqrt(d)
+        L[k + 1:, k] = (S[k + 1:, k] - L[k + 1:, :k] @ L[k, :k]) / L[k, k]
     rhs = AW @ x0 - b
-    lam = np.linalg.solve(L.T, np.linalg.solve(L, rhs))
-    for _ in range(2):      # refinement against the unregularised S
-        lam += np.linalg.solve(L.T, np.linalg.solve(L, rhs - S @ lam))
+    idx = np.nonzero(keep)[0]
+    Lk = L[np.ix_(idx, idx)]
+    lam = np.zeros(m)
+    lam[idx] = np.linalg.solve(Lk.T, np.linalg.solve(Lk, rhs[idx]))
+    for _ in range(REG[1]):
+        r = rhs[idx] - S[np.ix_(idx, idx)] @ lam[idx]
+        lam[idx] += np.linalg.solve(Lk.T, np.linalg.solve(Lk, r))
     x = x0 - V @ lam
     y[rows] = lam
     return x, y, True
@@ -142,7 +157,7 @@ def scale_problem(gq, mode):
 
 
 def admm(gq, rho_s, sigma, alpha, iters, D, E, state=None, Pinv=None, polish_every=10,
-         rho_scale=None):
+         rho_scale=None, adapt_every=0, stats=None):
     """OSQP iteration in the scaled space.  Returns (x, y, its, polished_ok, pdas_steps)."""
     Ps = D[:, None] * gq.P * D[None, :]
     qs = D * gq.q
@@ -171,6 +186,20 @@ def admm(gq, rho_s, sigma, alpha, iters, D, E, state=None, Pinv=None, polish_eve
         zn[hm] = np.where(v[hm] >= hh, v[hm], np.where(v[hm] <= hh - bb, v[hm] + bb, hh))
         ys = ys + rho * (v - ys / rho - zn)
         zs = zn
+        if adapt_every and it % adapt_every == 0:
+            # OSQP adaptive rho (scaled space): sqrt(prim/dual) of normalised residuals
+            Ax = As @ xs
+            rp = np.max(np.abs(Ax - zs)) / max(np.max(np.abs(Ax)), np.max(np.abs(zs)), 1e-30)
+            Px = Ps @ xs
+            Aty = As.T @ ys
+            rd = np.max(np.abs(Px + qs + Aty)) / max(np.max(np.abs(Px)), np.max(np.abs(Aty)), np.max(np.abs(qs)), 1e-30)
+            ratio = np.sqrt(rp / max(rd, 1e-30))
+            if ratio > 5.0 or ratio < 0.2:
+                rho = np.clip(rho * ratio, 1e-6, 1e6)
+                K = Ps + sigma * np.eye(gq.n) + As.T @ (rho[:, None] * As)
+                Kinv = np.linalg.inv(K)
+                if stats is not None:
+                    stats['refac'] = stats.get('refac', 0) + 1
         if Pinv is not None and it % polish_every == 0:
             # unscale: x = D xs, y = E ys, prox input w = a'x + y/c with c = rho E^2 in unscaled units
             x = D * xs

@@ -1,0 +1,27 @@
+"""Per-phase cycle breakdown of k_mpc_step (diagnostic stamps build)."""
+import os, sys, ctypes
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'distributed-local-planner-pi-admm_amd'))
+os.environ.setdefault('PIADMM_LIB', os.path.join(ROOT, 'distributed-local-planner-pi-admm_amd/piadmm/libpiadmm_stamps.so'))
+import numpy as np
+from piadmm import config, scenario
+from piadmm.solver import PI_ADMM_MI355X
+NAMES = ['setup_x', 'setup_z', 'xstep', 'xqp', 'xred', 'xroll', 'zstep', 'zqp', 'zred', 'kernel',
+         'red_gemv', 'red_S', 'red_chol', 'red_x', 'admm', 'xq', 'term']
+tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+H = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+cfg = config.matlab_pi(H=H, fixed_iters=1, max_outer=100)
+scn = scenario.tiled(tiles, H, n_steps=steps)
+s = PI_ADMM_MI355X(cfg, scn)
+s.reset_counters()
+ms = s.time_steps(0, steps)
+cnt = s.counters()
+buf = (ctypes.c_uint64 * (s.C * 32))()
+s._check(s.lib.piadmm_debug_stamps(s._h, buf, s.C * 32))
+st = np.array(buf, dtype=np.float64).reshape(s.C, 32)
+print(f"tiles={tiles} H={H} steps={steps} event_ms={ms:.3f} counters={cnt}")
+tot = st[:, 9].mean()
+for i, n in enumerate(NAMES):
+    v = st[:, i].mean()
+    print(f"  {n:10s} mean cycles/comp/step {v/steps:14.0f}  ({100*v/tot:6.1f}% of kernel)  max {st[:, i].max()/steps:14.0f}")
