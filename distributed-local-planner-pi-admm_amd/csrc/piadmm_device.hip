@@ -1234,6 +1234,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   bool act = false;
   double dis_chk = NAN;
   double* resid = A.resid + (size_t)ci * c.max_outer * 2;
+  for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
   // reference positions of the own agent at time lanes (fixed for the step)
   double rx_own = 0.0, ry_own = 0.0;
   if (w < na && l <= H) {
@@ -1433,7 +1434,6 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   // ---- outputs and propagation (casadi/main.py:185-192)
   if (threadIdx.x == 0) {
     A.iters[ci] = iters;
-    for (int it = iters; it < c.max_outer; ++it) resid[2 * it] = resid[2 * it + 1] = NAN;
     if (e >= 0) A.edge_active[e] = act ? 1 : 0;
   }
   if (w < na) {

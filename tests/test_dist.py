@@ -1,0 +1,66 @@
+"""Multi-rank path on CPU (gloo, world_size 2): sharded runs equal the unsharded run.
+
+Each rank owns whole components (piadmm.dist.shard), runs its shard through the
+oracle (the CPU stand-in for one GPU) and the shards are gathered; the result
+must equal one process running all agents, because no component straddles ranks.
+The same harness (barrier + max-over-ranks timing) is what bench.py uses.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as tdist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import sys
+    from conftest import PKG, ROOT
+    sys.path[:0] = [ROOT, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import piadmm_oracle as O
+    from piadmm import config, dist, scenario
+    scn = scenario.tiled(5, 10, n_steps=30, seed=2)
+    sub = dist.shard(scn, rank, world)
+    cfg = config.matlab_pi(H=10)
+    orc = O.Oracle(cfg, sub)
+    for _ in range(3):
+        orc.run(10)
+    a0, a1 = dist.shard_bounds(scn, rank, world)
+    mine = {"a0": a0, "xt": orc.xt}
+    gathered = [None] * world
+    tdist.all_gather_object(gathered, mine)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)              # bench.py's max-over-ranks timer
+    tdist.barrier()
+    if rank == 0:
+        xt = np.zeros((scn.n_agents, 3))
+        for g in gathered:
+            xt[g["a0"]:g["a0"] + g["xt"].shape[0]] = g["xt"]
+        np.save(out, xt)
+        assert float(t) == float(world)
+    tdist.destroy_process_group()
+
+
+def test_two_rank_shards_match_single_process(tmp_path):
+    out = str(tmp_path / "xt.npy")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    from oracle import piadmm_oracle as O
+    from piadmm import config, scenario
+    scn = scenario.tiled(5, 10, n_steps=30, seed=2)
+    orc = O.Oracle(config.matlab_pi(H=10), scn)
+    for _ in range(3):
+        orc.run(10)
+    np.testing.assert_array_equal(np.load(out), orc.xt)

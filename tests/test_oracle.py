@@ -1,0 +1,196 @@
+"""The oracle (CPU restatement) against the reference's own numerics and golden fixtures.
+
+Pinning chain ("Oracle and parity"):
+  * rollouts: bit-exact against the reference's own ``dynamic_update_local`` /
+    ``dynamic_update_edge`` numeric branches, executed on seeded inputs
+    (tests/golden/ref_rollouts.npz, oracle/gen_ref_rollouts.py);
+  * QP solutions: KKT certificates + an independent SciPy solve (the reference's
+    OSQP answers do not exist anywhere: parity against reference outputs is unpinned);
+  * loop semantics: regression against committed oracle runs + structural
+    invariants (tiling, aliasing quirk B4, rounding B6, collision threshold B2).
+"""
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLD
+
+from oracle import piadmm_oracle as O
+from oracle import qp_exact
+from piadmm import config, scenario
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+# ---------------------------------------------------------------- rollouts vs reference
+def test_rollouts_bit_exact_vs_reference():
+    d = load("ref_rollouts.npz")
+    assert len(d["H"]) >= 10
+    for c in range(len(d["H"])):
+        H = int(d["H"][c])
+        for i in range(2):
+            xt, u, s = d["xt"][c][i], d["u"][c][i][:H], d["spd"][c][i]
+            x, y, th = O.rollout_linear(xt, u, s, 0.1, 1.0)
+            np.testing.assert_array_equal(x, d["loc_x"][c][i][:H + 1])
+            np.testing.assert_array_equal(y, d["loc_y"][c][i][:H + 1])
+            np.testing.assert_array_equal(th, d["loc_th"][c][i][:H + 1])
+            x, y, th = O.rollout_nonlinear(xt, u, s, 0.1, 1.0)
+            np.testing.assert_array_equal(x, d["edge_x"][c][i][:H + 1])
+            np.testing.assert_array_equal(y, d["edge_y"][c][i][:H + 1])
+            np.testing.assert_array_equal(th, d["edge_th"][c][i][:H + 1])
+
+
+def test_affine_form_matches_reference_linear_rollout():
+    """c + M u (the QP's dynamics) equals the reference's linearised rollout."""
+    d = load("ref_rollouts.npz")
+    for c in range(len(d["H"])):
+        H = int(d["H"][c])
+        for i in range(2):
+            cc, M = O.rollout_affine(d["xt"][c][i], d["spd"][c][i], 0.1, 1.0, H)
+            p = cc + M @ d["u"][c][i][:H]
+            np.testing.assert_allclose(p[0], d["loc_x"][c][i][:H + 1], rtol=0, atol=1e-11)
+            np.testing.assert_allclose(p[1], d["loc_y"][c][i][:H + 1], rtol=0, atol=1e-11)
+
+
+# ---------------------------------------------------------------- QP solver
+def _kkt_ok(P, q, A, l, u, x, y, tol=1e-8):
+    st, inf, comp = qp_exact.kkt_residuals(P, q, A, l, u, x, y)
+    sc = 1.0 + np.abs(q).max()
+    return st <= tol * sc and inf <= tol and comp <= tol * sc
+
+
+def test_xstep_qp_fixtures():
+    d = load("qp_xstep.npz")
+    for k in range(len(d["H"])):
+        H = int(d["H"][k])
+        m = 2 * H - 1
+        P, q, A = d["P"][k][:H, :H], d["q"][k][:H], d["A"][k][:m, :H]
+        lo, hi = d["l"][k][:m], d["u"][k][:m]
+        x, y, _ = qp_exact.solve(P, q, A, lo, hi, np.zeros(H))
+        assert _kkt_ok(P, q, A, lo, hi, x, y)
+        np.testing.assert_allclose(x, d["x"][k][:H], rtol=0, atol=1e-10)
+
+
+def test_pair_qp_fixtures():
+    d = load("qp_pair.npz")
+    H = int(d["H"])
+    for k in range(d["P"].shape[0]):
+        P, q, A, lo, hi = d["P"][k], d["q"][k], d["A"][k], d["l"][k], d["u"][k]
+        x0 = np.zeros(3 * H)
+        x0[2 * H:] = np.maximum(0.0, lo[-H:])
+        x, y, _ = qp_exact.solve(P, q, A, lo, hi, x0)
+        assert _kkt_ok(P, q, A, lo, hi, x, y)
+        np.testing.assert_allclose(x[:2 * H], d["x"][k][:2 * H], rtol=0, atol=1e-9)
+
+
+def test_qp_against_independent_scipy_solver():
+    """An independent solver (SciPy SLSQP) agrees with the active-set oracle."""
+    opt = pytest.importorskip("scipy.optimize")
+    d = load("qp_xstep.npz")
+    for k in (0, 4):
+        H = int(d["H"][k])
+        m = 2 * H - 1
+        P, q, A = d["P"][k][:H, :H], d["q"][k][:H], d["A"][k][:m, :H]
+        lo, hi = d["l"][k][:m], d["u"][k][:m]
+        cons = [{"type": "ineq", "fun": lambda x, A=A, hi=hi: hi - A @ x, "jac": lambda x, A=A: -A},
+                {"type": "ineq", "fun": lambda x, A=A, lo=lo: A @ x - lo, "jac": lambda x, A=A: A}]
+        r = opt.minimize(lambda x: 0.5 * x @ P @ x + q @ x, np.zeros(H), jac=lambda x: P @ x + q,
+                         constraints=cons, method="SLSQP", options={"ftol": 1e-14, "maxiter": 500})
+        np.testing.assert_allclose(r.x, d["x"][k][:H], atol=2e-5)
+
+
+def test_qp_rejects_infeasible_start():
+    P = np.eye(2)
+    with pytest.raises(qp_exact.QPError):
+        qp_exact.solve(P, np.zeros(2), np.eye(2), -np.ones(2), np.ones(2), np.array([5.0, 0.0]))
+
+
+# ---------------------------------------------------------------- loop semantics
+@pytest.mark.parametrize("name", ["casadi_default_H10", "casadi_default_H15", "matlab_pi_H10", "matlab_pi_H8"])
+def test_oracle_runs_reproduce_fixtures(name):
+    d = load(f"run_{name}.npz")
+    cfg = config.PRESETS[str(d["preset"])](**eval(str(d["cfg_kw"])))   # fixture written by oracle/gen_golden.py
+    scn = scenario.Scenario(spd=d["spd"], xt0=d["xt0"], ref=d["ref"], edges=d["edges"], n_steps=d["xt"].shape[0])
+    orc = O.Oracle(cfg, scn)
+    for s in range(d["xt"].shape[0]):
+        r = orc.mpc_step()
+        np.testing.assert_allclose(r.xt, d["xt"][s], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(r.u, d["u"][s], rtol=1e-10, atol=1e-10)
+        np.testing.assert_array_equal(r.iters, d["iters"][s])
+
+
+def test_tiles_reduce_to_the_two_vehicle_reference():
+    """K unperturbed tiles give K copies of the 2-vehicle run (no coupling across tiles)."""
+    cfg = config.matlab_pi(H=10)
+    single = O.Oracle(cfg, scenario.intersection(10)).run(20)
+    tiles = O.Oracle(cfg, scenario.tiled(3, 10, perturb=False)).run(20)
+    for a, b in zip(single, tiles):
+        for k in range(3):
+            np.testing.assert_array_equal(b.xt[2 * k:2 * k + 2], a.xt)
+            np.testing.assert_array_equal(b.iters[k], a.iters[0])
+
+
+def test_alias_quirk_B4_zeroes_dual_residual_after_first_iteration():
+    """casadi/main.py:63,180 aliases last_iter_hat_pos to hat_pos_old: s_k == 0 from iteration 2.
+
+    matlab_pi H=10 keeps the pair active for several outer iterations around steps 28-31.
+    """
+    cfg = config.matlab_pi(H=10, fixed_iters=1, max_outer=6)
+    alias = O.Oracle(cfg.replace(alias_dual_residual=1), scenario.intersection(10)).run(32)
+    copy = O.Oracle(cfg, scenario.intersection(10)).run(32)
+    active_later = 0
+    for ra, rc in zip(alias, copy):
+        for it in range(1, 6):
+            assert ra.resid[0][it][1] == 0.0
+            if rc.resid[0][it][0] > 0.0:          # the pair was active in that iteration
+                active_later += 1
+                assert rc.resid[0][it][1] > 0.0   # copied history: a real dual residual
+    assert active_later > 0
+
+
+def test_rounding_quirk_B6():
+    r = O.Oracle(config.casadi_default(H=10), scenario.intersection(10)).run(3)[-1]
+    np.testing.assert_array_equal(np.around(r.u * 1e4), r.u * 1e4)
+
+
+def test_collision_threshold_quirk_B2():
+    """Python compares squared distance with dis_thres (B2); MATLAB with dis_thres^2."""
+    assert config.casadi_default().thr_collide == 2.0
+    assert config.matlab_pi().thr_collide == 4.0
+
+
+def test_pi_dual_update_matches_matlab_statement_order():
+    """ADMM_CVX_..._PI_antiwindup.m:160-188 written out literally for one pair."""
+    rng = np.random.default_rng(5)
+    cfg = config.matlab_pi(H=6, windup_sat=1.5)
+    H1 = 7
+    p1, p2 = rng.normal(0, 2, (2, H1)), rng.normal(0, 2, (2, H1))
+    hat = rng.normal(0, 2, (2, 2, H1))
+    lam, S, D = rng.normal(0, 1, (2, 2, H1)), rng.normal(0, 1, (2, 2, H1)), rng.normal(0, 0.1, (2, 2, H1))
+    dist = np.sqrt(np.sum((p1 - p2) ** 2, axis=0))
+    # literal MATLAB
+    kP = cfg.theta1 - cfg.theta2 / (1 + np.exp(-np.min(dist)))
+    e1, e2 = p1 - hat[0], p2 - hat[1]
+    S1 = S[0] + cfg.kI * e1 + D[0]
+    S2 = S[1] + cfg.kI * e2 + D[1]
+    l1, l2 = S1 + kP * e1, S2 + kP * e2
+    exp_lam, exp_D = [], []
+    for lv in (l1, l2):
+        sat = np.minimum(cfg.windup_sat, np.maximum(lv, -cfg.windup_sat))
+        exp_D.append(sat - lv if np.sum(lv != sat) > 0 else np.zeros_like(lv))
+        exp_lam.append(sat)
+    O.dual_update(cfg, p1, p2, hat, lam, S, D, dist)
+    np.testing.assert_array_equal(lam[0], exp_lam[0])
+    np.testing.assert_array_equal(lam[1], exp_lam[1])
+    np.testing.assert_array_equal(D[0], exp_D[0])
+    np.testing.assert_array_equal(D[1], exp_D[1])
+    np.testing.assert_array_equal(S[0], S1)
+
+
+def test_empty_candidate_graph_terminates_after_one_iteration():
+    scn = scenario.intersection(10)
+    scn.edges = np.zeros((0, 2), np.int32)
+    r = O.Oracle(config.casadi_default(H=10), scn).mpc_step()
+    assert list(r.iters) == [1, 1]
