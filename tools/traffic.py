@@ -1,0 +1,53 @@
+"""Summarise the rocprofv3 passes of tools/profile.sh into profiles/ (kernel stats + HBM traffic).
+
+traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes for pd::k_mpc_step, using
+MI355X_MICROARCH.md's gfx950 correction (FETCH_SIZE reads 1/2 of the bytes of wide
+streaming reads; this kernel's 8-byte scattered reads are uncalibrated, so the raw values
+are kept next to the corrected one).
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+out, tag = sys.argv[1], sys.argv[2]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+prof = os.path.join(ROOT, "profiles")
+os.makedirs(prof, exist_ok=True)
+
+
+def rows(pattern):
+    fs = glob.glob(os.path.join(out, pattern), recursive=True)
+    if not fs:
+        return []
+    with open(fs[0]) as f:
+        return list(csv.DictReader(f))
+
+
+stats = glob.glob(os.path.join(out, "trace", "**", "*kernel_stats.csv"), recursive=True)
+if stats:
+    shutil.copy(stats[0], os.path.join(prof, f"kernel_stats_{tag}.csv"))
+
+
+def pmc(name):
+    vals = []
+    for r in rows(os.path.join(name.lower().split("_")[0], "**", "*counter_collection.csv")):
+        if "k_mpc_step" in r.get("Kernel_Name", "") and r.get("Counter_Name") == name:
+            vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+fetch = pmc("FETCH_SIZE")
+write = pmc("WRITE_SIZE")
+res = {"workload": "tiled128_H30_matlab_pi_fixed100", "kernel": "pd::k_mpc_step",
+       "launches_fetch": len(fetch), "launches_write": len(write)}
+if fetch and write:
+    f = sum(fetch) / len(fetch)
+    w = sum(write) / len(write)
+    res.update(fetch_size_kb_raw=f, write_size_kb_raw=w,
+               hbm_bytes_per_launch=(2.0 * f + w) * 1024.0,
+               note="traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE 1/2 correction)")
+json.dump(res, open(os.path.join(prof, f"traffic_{tag}.json"), "w"), indent=1)
+print(json.dumps(res))
