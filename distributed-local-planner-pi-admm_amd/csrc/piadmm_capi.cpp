@@ -217,7 +217,7 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.lab_x, (size_t)N * 2 * pd::HMAX);
   rc |= dalloc(h, &A.Pinv_e, E * 4 * H * H);
   rc |= dalloc(h, &A.PGt, E * 2 * H * H);
-  rc |= dalloc(h, &A.GPG, E * H * H);
+  rc |= dalloc(h, &A.GPG, E * 2 * H * H);
   rc |= dalloc(h, &A.sc_e, E * 8 * pd::HMAX);
   rc |= dalloc(h, &A.ws_e, E * 12 * pd::HMAX);
   rc |= dalloc(h, &A.lab_e, E * 5 * pd::HMAX);
@@ -225,6 +225,9 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.counters, C * 8);
   rc |= dalloc(h, &A.rho_x, (size_t)N);
   rc |= dalloc(h, &A.rho_e, E);
+  rc |= dalloc(h, &A.Kx_cache, (size_t)N * H * H);
+  rc |= dalloc(h, &A.xcache_rho, (size_t)N);
+  rc |= dalloc(h, &A.ecache, E);
 #ifdef PIADMM_STAMPS
   rc |= dalloc(h, &A.stamps, C * 32);
 #endif
@@ -241,6 +244,7 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
     HIPCHK(h, hipMemcpyAsync(A.rho_x, r0.data(), (size_t)N * sizeof(double), hipMemcpyHostToDevice, h->stream));
     if (E) HIPCHK(h, hipMemcpyAsync(A.rho_e, r0.data(), E * sizeof(double), hipMemcpyHostToDevice, h->stream));
   }
+  HIPCHK(h, hipMemsetAsync(A.xcache_rho, 0xff, (size_t)N * sizeof(double), h->stream));   // NaN: no cache
   HIPCHK(h, hipStreamSynchronize(h->stream));
   A.spd = d_spd;
   A.ref = d_ref;

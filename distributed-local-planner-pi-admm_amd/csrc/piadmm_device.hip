@@ -60,11 +60,23 @@ __device__ __forceinline__ double rdl(double v, int k) {
 }
 __device__ __forceinline__ int rdli(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
+// DPP move of a double (two 32-bit halves); lanes whose source is outside the row/wave read 0.
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b & 0xffffffffull), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, true);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+constexpr int DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138;
+
 __device__ __forceinline__ double shup(double v, int o) {
+  if (o == 1) return dppd<DPP_WAVE_SHR1>(v);          // lane l <- lane l-1, lane 0 <- 0
   double t = __shfl_up(v, (unsigned)o);
   return lid() >= o ? t : 0.0;
 }
 __device__ __forceinline__ double shdn(double v, int o) {
+  if (o == 1) return dppd<DPP_WAVE_SHL1>(v);          // lane l <- lane l+1, lane 63 <- 0
   double t = __shfl_down(v, (unsigned)o);
   return lid() + o < WAVE ? t : 0.0;
 }
@@ -86,30 +98,38 @@ __device__ __forceinline__ double wmin(double v) {
 __device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
 __device__ __forceinline__ bool wall(bool p) { return __ballot(!p) == 0ull; }
 
+// Inclusive prefix / suffix sums over lanes 0..31 (H <= 32: every scanned vector lives there;
+// lanes 32..63 of the result are unspecified).  Four DPP row shifts inside each 16-lane row,
+// then one readlane to carry across the two rows.
 __device__ __forceinline__ double scan_incl(double v) {
+  v += dppd<0x111>(v);   // row_shr:1
+  v += dppd<0x112>(v);   // row_shr:2
+  v += dppd<0x114>(v);   // row_shr:4
+  v += dppd<0x118>(v);   // row_shr:8
+  const double c = rdl(v, 15);
   const int l = lid();
-#pragma unroll
-  for (int o = 1; o < WAVE; o <<= 1) {
-    double t = __shfl_up(v, (unsigned)o);
-    if (l >= o) v += t;
-  }
-  return v;
+  return (l >= 16 && l < 32) ? v + c : v;
 }
 __device__ __forceinline__ double scan_incl_rev(double v) {
-  const int l = lid();
-#pragma unroll
-  for (int o = 1; o < WAVE; o <<= 1) {
-    double t = __shfl_down(v, (unsigned)o);
-    if (l + o < WAVE) v += t;
-  }
-  return v;
+  v += dppd<0x101>(v);   // row_shl:1
+  v += dppd<0x102>(v);   // row_shl:2
+  v += dppd<0x104>(v);   // row_shl:4
+  v += dppd<0x108>(v);   // row_shl:8
+  const double c = rdl(v, 16);
+  return (lid() < 16) ? v + c : v;
 }
 // T(t, j) = (t-1-j)+ is the rollout's double integrator (casadi/PI_ADMM_class.py:59-69:
 // theta accumulates u, x/y accumulate theta).  "hinge lane" k holds time t = k+1.
 // T_apply : var lanes u_j        -> hinge lanes (T u)_{k+1} = sum_{j<=k-1} (k-j) u_j
 // Tt_apply: hinge lanes w_k      -> var lanes   sum_{k>=j+1} (k-j) w_k
-__device__ __forceinline__ double T_apply(double u) { return shup(scan_incl(scan_incl(u)), 1); }
-__device__ __forceinline__ double Tt_apply(double w) { return shdn(scan_incl_rev(scan_incl_rev(w)), 1); }
+__device__ __forceinline__ double T_apply(double u) {
+  const double r = scan_incl(scan_incl(u));
+  return shup(lid() < 32 ? r : 0.0, 1);
+}
+__device__ __forceinline__ double Tt_apply(double w) {
+  const double r = scan_incl_rev(scan_incl_rev(w));
+  return shdn(lid() < 32 ? r : 0.0, 1);
+}
 
 // ============================================================ reference arithmetic
 __device__ __forceinline__ double pow10i(int d) {
@@ -159,7 +179,10 @@ __device__ __forceinline__ Geo make_geo(const double* xt3, double s, const piadm
   g.cs = cos(g.th0);
   g.ax = (-s * g.sn * c.dt) * (s / c.L * c.dt);
   g.ay = (s * g.cs * c.dt) * (s / c.L * c.dt);
-  g.mm = g.ax * g.ax + g.ay * g.ay;
+  // |M_x|^2 + |M_y|^2 = (dt s a)^2 (sin^2 + cos^2): written without the trig so that the
+  // x-step P (and the pair P blocks) depend on the speed only and can be cached per scenario
+  const double msc = s * c.dt * (s / c.L * c.dt);
+  g.mm = msc * msc;
   g.xdot0 = -s * g.sn * g.th0 + (s * g.cs + s * g.th0 * g.sn);
   g.ydot0 = s * g.cs * g.th0 + (s * g.sn - s * g.th0 * g.cs);
   return g;
@@ -190,14 +213,9 @@ __device__ __forceinline__ void rollout(const double* xt3, double s, double u, c
   const int l = lid();
   const double th0 = xt3[2];
   const double sn0 = sin(th0), cs0 = cos(th0);
-  // theta sequence (sequential, literal order)
-  double th = th0, my_th = (l == 0) ? th0 : 0.0;
-  for (int k = 0; k < H; ++k) {
-    const double uk = rdl(u, k);
-    const double theta_dot = s / c.L * uk;
-    th = th + theta_dot * c.dt;
-    if (l == k + 1) my_th = th;
-  }
+  // theta_k = theta_0 + sum_{j<k} (s/L u_j) dt  (wave prefix scan)
+  const double inc = (l < H) ? (s / c.L * u) * c.dt : 0.0;
+  const double my_th = th0 + shup(scan_incl(inc), 1);
   // per-lane rates at time k = lane
   double xd, yd;
   if (nonlinear) {
@@ -209,17 +227,9 @@ __device__ __forceinline__ void rollout(const double* xt3, double s, double u, c
     xd = -s * sn0 * my_th + (s * cs0 + s * th0 * sn0);
     yd = s * cs0 * my_th + (s * sn0 - s * th0 * cs0);
   }
-  double x = xt3[0], y = xt3[1];
-  px = (l == 0) ? x : 0.0;
-  py = (l == 0) ? y : 0.0;
-  for (int k = 0; k < H; ++k) {
-    x = x + rdl(xd, k) * c.dt;
-    y = y + rdl(yd, k) * c.dt;
-    if (l == k + 1) {
-      px = x;
-      py = y;
-    }
-  }
+  const double xi = (l < H) ? xd * c.dt : 0.0, yi = (l < H) ? yd * c.dt : 0.0;
+  px = xt3[0] + shup(scan_incl(xi), 1);
+  py = xt3[1] + shup(scan_incl(yi), 1);
   pth = my_th;
   if (l > H) px = py = pth = 0.0;
 }
@@ -228,18 +238,33 @@ __device__ __forceinline__ void rollout(const double* xt3, double s, double u, c
 // In-place Gauss-Jordan inverse of an SPD matrix held in LDS (stride ld), lane = column.
 __device__ __forceinline__ void gj_invert(double* m, int n, int ld) {
   const int l = lid();
+  const int lc = (l < n) ? l : n - 1;     // lanes >= n mirror column n-1 and never store
   for (int p = 0; p < n; ++p) {
-    const double colp = (l < n) ? m[l * ld + p] : 0.0;   // a_lp
+    const double colp = m[lc * ld + p];   // a_lp (lane = row here)
     const double ip = 1.0 / rdl(colp, p);
-    const double rpj = (l < n) ? ((l == p) ? ip : m[p * ld + l] * ip) : 0.0;
+    const double rpj = (l == p) ? ip : m[p * ld + lc] * ip;
     wsync();
-    for (int i = 0; i < n; ++i) {
-      if (i == p) continue;
-      const double aip = rdl(colp, i);
-      if (l < n) {
-        if (l == p) m[i * ld + p] = -aip * ip;
-        else m[i * ld + l] -= aip * rpj;
+    // every row i (row p included: it is overwritten below) -= a_ip * new row p;
+    // column p becomes -a_ip / a_pp.  Branch-free so the compiler can batch the LDS traffic.
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+      double v[4], a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = rdl(colp, i + u);
+        v[u] = m[(i + u) * ld + lc];
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double nv = (l == p) ? -a[u] * ip : v[u] - a[u] * rpj;
+        if (l < n) m[(i + u) * ld + l] = nv;
+      }
+    }
+    for (; i < n; ++i) {
+      const double a = rdl(colp, i);
+      const double v = m[i * ld + lc];
+      const double nv = (l == p) ? -a * ip : v - a * rpj;
+      if (l < n) m[i * ld + l] = nv;
     }
     if (l < n) m[p * ld + l] = rpj;
     wsync();
@@ -272,8 +297,8 @@ struct QP {
   double beta, rho, sigma, alpha, tol;
   double* K;              // LDS  n x n  scaled (P_s + sigma I + rho A_s'A_s)^-1
   const double* Pinv;     // n x n unscaled P^-1 (LDS for the x-step, HBM for the pair)
-  const double* PGt;      // HBM  H x n  row k = P^-1 G_k'
-  const double* GPG;      // HBM  H x H
+  const double* PGt;      // HBM  H x n  row k = P_v^-1 T(k+1,.)' per vehicle block (unscaled by g)
+  const double* GPG;      // HBM  2 x H x H  Z_v = T P_v^-1 T' (GPG = g1^2 Z_1 + g2^2 Z_2)
   double* vb;             // per-wave LDS vectors (512 doubles)
   double* fac;            // LDS factor region: L (lower), S (upper), stride fld
   double* fdiag;          // LDS [2*64]: S_aa, 1/L_aa of the cached factor
@@ -287,6 +312,13 @@ struct QP {
 
 template <int NV>
 __device__ constexpr int NR_HINGE() { return NV == 2 ? 4 : 0; }
+
+// Hinge rows sit at their kink at most optima (beta = 1000 makes them near-equalities);
+// like OSQP's larger rho on equality rows they get HINGE_RHO x rho (tools/qp_sim.py sweep:
+// pair-QP ADMM iterations mean 29.6 -> 20.3, max 880 -> 295).
+constexpr double HINGE_RHO = 3.0;
+template <int NV>
+__device__ __forceinline__ double rrow(const QP<NV>& P, int s) { return P.hinge(s) ? P.rho * HINGE_RHO : P.rho; }
 
 // Unscaled P x (var lanes), matrix-free: T'T via two double scans, D2'D2 via neighbours.
 template <int NV>
@@ -352,7 +384,7 @@ __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
         const double e2 = rdl(Eh2, k);
         if (k > ir && k > jc) hs += e2 * (double)(k - ir) * (double)(k - jc);
       }
-      hs *= gr * gc;
+      hs *= gr * gc * HINGE_RHO;
     }
     if (incol) {
       double ata = hs, v = 0.0;
@@ -435,7 +467,7 @@ __device__ __forceinline__ double prox_s(const QP<NV>& P, int s, double v) {
   const double e = P.E[s];
   if (P.hinge(s)) {
     const double hs = e * P.lo[s];
-    const double thr = (P.beta / e) / P.rho;
+    const double thr = (P.beta / e) / rrow(P, s);
     return v >= hs ? v : (v <= hs - thr ? v + thr : hs);
   }
   return fmin(fmax(v, e * P.lo[s]), e * P.hi[s]);
@@ -448,7 +480,7 @@ __device__ __forceinline__ signed char label_scaled(const QP<NV>& P, int s, doub
   if (!P.valid[s]) return 0;
   if (P.hinge(s)) {
     const double hs = e * P.lo[s];
-    const double thr = (P.beta / e) / P.rho;
+    const double thr = (P.beta / e) / rrow(P, s);
     return v >= hs ? HZERO : (v <= hs - thr ? HLINEAR : HKINK);
   }
   return v <= e * P.lo[s] ? LOWER : (v >= e * P.hi[s] ? UPPER : FREE);
@@ -459,7 +491,7 @@ __device__ __forceinline__ void admm_iter(const QP<NV>& P, double* xs, double* z
   constexpr int NR = QP<NV>::NR;
   double w[NR], t[NV], rhs[NV], xt[NV], xu[NV], a[NR];
 #pragma unroll
-  for (int s = 0; s < NR; ++s) w[s] = P.valid[s] ? P.E[s] * (P.rho * zs[s] - ys[s]) : 0.0;
+  for (int s = 0; s < NR; ++s) w[s] = P.valid[s] ? P.E[s] * (rrow(P, s) * zs[s] - ys[s]) : 0.0;
   At_mul(P, w, t);
 #pragma unroll
   for (int v = 0; v < NV; ++v) rhs[v] = P.sigma * xs[v] - P.D[v] * P.q[v] + P.D[v] * t[v];
@@ -475,10 +507,11 @@ __device__ __forceinline__ void admm_iter(const QP<NV>& P, double* xs, double* z
       zs[s] = ys[s] = 0.0;
       continue;
     }
+    const double rs = rrow(P, s);
     const double zr = P.alpha * (P.E[s] * a[s]) + (1.0 - P.alpha) * zs[s];
-    const double vin = zr + ys[s] / P.rho;
+    const double vin = zr + ys[s] / rs;
     const double zn = prox_s(P, s, vin);
-    ys[s] += P.rho * (zr - zn);
+    ys[s] += rs * (zr - zn);
     zs[s] = zn;
   }
 }
@@ -509,6 +542,10 @@ __device__ __forceinline__ RowT row_terms(const QP<NV>& P, int id) {
   return r;
 }
 
+// hinge coefficient of variable i (vehicle 1: g1, vehicle 2: g2); PGt/GPG hold unscaled tables
+template <int NV>
+__device__ __forceinline__ double gvar(const QP<NV>& P, int i) { return i < P.H ? P.g1 : P.g2; }
+
 template <int NV>
 __device__ __forceinline__ double s_entry(const QP<NV>& P, int ia, int ibd) {
   const RowT a = row_terms(P, ia), b = row_terms(P, ibd);
@@ -523,22 +560,23 @@ __device__ __forceinline__ double s_entry(const QP<NV>& P, int ia, int ibd) {
     return s;
   }
   if (a.hk < 0) {
-    double s = a.c0 * P.PGt[b.hk * n + a.i0];
-    if (a.c1 != 0.0) s += a.c1 * P.PGt[b.hk * n + a.i1];
+    double s = a.c0 * gvar(P, a.i0) * P.PGt[b.hk * n + a.i0];
+    if (a.c1 != 0.0) s += a.c1 * gvar(P, a.i1) * P.PGt[b.hk * n + a.i1];
     return s;
   }
   if (b.hk < 0) {
-    double s = b.c0 * P.PGt[a.hk * n + b.i0];
-    if (b.c1 != 0.0) s += b.c1 * P.PGt[a.hk * n + b.i1];
+    double s = b.c0 * gvar(P, b.i0) * P.PGt[a.hk * n + b.i0];
+    if (b.c1 != 0.0) s += b.c1 * gvar(P, b.i1) * P.PGt[a.hk * n + b.i1];
     return s;
   }
-  return P.GPG[a.hk * P.H + b.hk];
+  const int HH = P.H * P.H;
+  return P.g1 * P.g1 * P.GPG[a.hk * P.H + b.hk] + P.g2 * P.g2 * P.GPG[HH + a.hk * P.H + b.hk];
 }
 // (P^-1 a_id) at variable index i
 template <int NV>
 __device__ __forceinline__ double pcol(const QP<NV>& P, int id, int i) {
   const RowT a = row_terms(P, id);
-  if (a.hk >= 0) return P.PGt[a.hk * P.n + i];
+  if (a.hk >= 0) return gvar(P, i) * P.PGt[a.hk * P.n + i];
   double s = a.c0 * P.Pinv[a.i0 * P.n + i];
   if (a.c1 != 0.0) s += a.c1 * P.Pinv[a.i1 * P.n + i];
   return s;
@@ -760,7 +798,7 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
       continue;
     }
     const double tp = P.tol * (1.0 + fabs(P.lo[s]));
-    const double c = P.rho * P.E[s] * P.E[s];
+    const double c = rrow(P, s) * P.E[s] * P.E[s];
     const double wv = ax[s] + y[s] / c;
     if (P.hinge(s)) {
       const double h = P.lo[s];
@@ -882,7 +920,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       bool same = true, tried = true;
 #pragma unroll
       for (int s = 0; s < NR; ++s) {
-        lab[s] = label_scaled(P, s, zs[s] + ys[s] / P.rho);
+        lab[s] = label_scaled(P, s, zs[s] + ys[s] / rrow(P, s));
         same &= (lab[s] == plab[s]);
         tried &= (lab[s] == flab[s]);
         plab[s] = lab[s];
@@ -911,7 +949,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
 #pragma unroll
     for (int v = 0; v < NV; ++v) x[v] = P.D[v] * xs[v];
 #pragma unroll
-    for (int s = 0; s < NR; ++s) lab[s] = label_scaled(P, s, zs[s] + ys[s] / P.rho);
+    for (int s = 0; s < NR; ++s) lab[s] = label_scaled(P, s, zs[s] + ys[s] / rrow(P, s));
   }
   bool fin = true;
 #pragma unroll
@@ -1012,14 +1050,45 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
   const bool in = l < H;
   P.coefP = 2.0 * c.Pnorm + c.rho * (double)A.nbr_cnt[a];
   P.mm[0] = g.mm;
+  double* Kc = A.Kx_cache + (size_t)a * H * H;
+  double* Pc = A.Pinv_x + (size_t)a * H * H;
+  double* sc = A.sc_x + (size_t)a * 4 * HMAX;
+  const int li = l < HMAX ? l : 0;
+  // P depends on the agent's speed only (make_geo): K_s^-1, P^-1 and the scaling are
+  // cached in HBM per scenario and rebuilt only when the ADMM penalty differs.
+  if (A.xcache_rho[a] == P.rho) {
+    P.D[0] = in ? sc[li] : 0.0;
+    P.E[0] = in ? sc[HMAX + li] : 0.0;
+    P.E[1] = (l < H - 1) ? sc[2 * HMAX + li] : 0.0;
+    for (int i = 0; i < H; ++i) {
+      if (in) {
+        P.K[i * H + l] = Kc[i * H + l];
+        Px_lds[i * H + l] = Pc[i * H + l];
+      }
+    }
+    wsync();
+    return;
+  }
   ruiz(P);
   build_K(P, xfac, HMAX + 1);
   for (int i = 0; i < H; ++i)
     if (in) xfac[i * (HMAX + 1) + l] = P_entry(P, 0, i, l);
   wsync();
   gj_invert(xfac, H, HMAX + 1);
-  for (int i = 0; i < H; ++i)
-    if (in) Px_lds[i * H + l] = xfac[i * (HMAX + 1) + l];
+  for (int i = 0; i < H; ++i) {
+    if (in) {
+      const double v = xfac[i * (HMAX + 1) + l];
+      Px_lds[i * H + l] = v;
+      Pc[i * H + l] = v;
+      Kc[i * H + l] = P.K[i * H + l];
+    }
+  }
+  if (l < HMAX) {
+    sc[0 * HMAX + l] = P.D[0];
+    sc[1 * HMAX + l] = P.E[0];
+    sc[2 * HMAX + l] = P.E[1];
+  }
+  if (l == 0) A.xcache_rho[a] = P.rho;
   wsync();
 }
 
@@ -1048,44 +1117,45 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
   P.mm[0] = g1.mm;
   P.mm[1] = g2.mm;
 
-  // ---- P_v^-1 blocks, PGt = P^-1 G', GPG = G P^-1 G'  (PGt staged in the Ke region)
-  double* PGt_l = Ke_lds;          // H x n (temporarily)
-  double* Pi = A.Pinv_e + (size_t)e * n * n;
-  for (int v = 0; v < 2; ++v) {
-    const double gv = v == 0 ? P.g1 : P.g2;
-    for (int i = 0; i < H; ++i)
-      if (in) scr[i * LD + l] = P_entry(P, v, i, l);
-    wsync();
-    gj_invert(scr, H, LD);
-    for (int i = 0; i < H; ++i) {
-      if (in) {
-        Pi[(v * H + i) * n + v * H + l] = scr[i * LD + l];
-        Pi[(v * H + i) * n + (1 - v) * H + l] = 0.0;
+  // ---- P_v^-1 blocks (HBM), Y = P_v^-1 T' (PGt, unscaled by g) and Z_v = T P_v^-1 T' (GPG):
+  // speed-only, so built once per scenario; g1, g2 scale them on the fly (s_entry, pcol)
+  if (!A.ecache[e]) {
+    double* Yl = Ke_lds;             // H x n staging (the Ke region is rebuilt below)
+    double* Pi = A.Pinv_e + (size_t)e * n * n;
+    for (int v = 0; v < 2; ++v) {
+      for (int i = 0; i < H; ++i)
+        if (in) scr[i * LD + l] = P_entry(P, v, i, l);
+      wsync();
+      gj_invert(scr, H, LD);
+      for (int i = 0; i < H; ++i) {
+        if (in) {
+          Pi[(v * H + i) * n + v * H + l] = scr[i * LD + l];
+          Pi[(v * H + i) * n + (1 - v) * H + l] = 0.0;
+        }
       }
+      // lane i: Y_k = sum_{j<=k-1} (k-j) Pinv_v[i][j]
+      double acc1 = 0.0, Y = 0.0;
+      for (int k = 0; k < H; ++k) {
+        if (in) Yl[k * n + v * H + l] = Y;
+        if (in) acc1 += scr[l * LD + k];
+        Y += acc1;
+      }
+      wsync();
     }
-    // lane i: Y_k = sum_{j<=k-1} (k-j) Pinv_v[i][j]
-    double acc1 = 0.0, Y = 0.0;
-    for (int k = 0; k < H; ++k) {
-      if (in) PGt_l[k * n + v * H + l] = gv * Y;
-      if (in) acc1 += scr[l * LD + k];
-      Y += acc1;
-    }
-    wsync();
-  }
-  {
-    double* Gg = A.GPG + (size_t)e * H * H;
+    double* Zg = A.GPG + (size_t)e * 2 * H * H;
     double* Pg = A.PGt + (size_t)e * H * n;
     const int b = in ? l : 0;
-    double B = 0.0, Z = 0.0;
-    for (int a = 0; a < H; ++a) {
-      if (in) Gg[a * H + l] = Z;
-      const double wa = P.g1 * PGt_l[b * n + a] + P.g2 * PGt_l[b * n + H + a];
-      B += wa;
-      Z += B;
+    for (int v = 0; v < 2; ++v) {
+      double B = 0.0, Z = 0.0;
+      for (int a = 0; a < H; ++a) {
+        if (in) Zg[v * H * H + a * H + l] = Z;
+        B += Yl[b * n + v * H + a];
+        Z += B;
+      }
     }
-    for (int k = 0; k < H; ++k) {
-      if (l < n) Pg[k * n + l] = PGt_l[k * n + l];
-    }
+    for (int k = 0; k < H; ++k)
+      if (l < n) Pg[k * n + l] = Yl[k * n + l];
+    if (l == 0) A.ecache[e] = 1;
     wsync();
   }
   ruiz(P);
@@ -1214,7 +1284,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     qe.K = Ke;
     qe.Pinv = A.Pinv_e + (size_t)e * 4 * H * H;
     qe.PGt = A.PGt + (size_t)e * 2 * H * H;
-    qe.GPG = A.GPG + (size_t)e * H * H;
+    qe.GPG = A.GPG + (size_t)e * 2 * H * H;
     qe.vb = wm.vb;
     qe.fac = scr;
     qe.fdiag = zdiag;
@@ -1451,6 +1521,11 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     if (l == 0) {
       A.status[a] = status_x;
       A.rho_x[a] = qx.rho;
+    }
+    if (A.xcache_rho[a] != qx.rho) {       // adaptive rho rebuilt K_s^-1 in LDS: refresh the cache
+      double* Kc = A.Kx_cache + (size_t)a * H * H;
+      for (int i = l; i < H * H; i += WAVE) Kc[i] = qx.K[i];
+      if (l == 0) A.xcache_rho[a] = qx.rho;
     }
   }
   if (w == 0 && e >= 0 && l == 0) A.rho_e[e] = qe.rho;

@@ -43,7 +43,7 @@ struct DevArgs {
   signed char* lab_x;       // N*2*HMAX
   double* Pinv_e;           // E*(2H)*(2H)
   double* PGt;              // E*H*(2H)   row k = P^-1 G_k'
-  double* GPG;              // E*H*H
+  double* GPG;              // E*2*H*H    Z_v = T P_v^-1 T'
   double* sc_e;             // E*8*HMAX   (D1, D2, Eb1, Er1, Eb2, Er2, Eh, h0)
   double* ws_e;             // E*12*HMAX  (xs0, xs1, zs0..4, ys0..4)
   signed char* lab_e;       // E*5*HMAX
@@ -52,6 +52,9 @@ struct DevArgs {
   unsigned long long* stamps;    // C*32 phase cycle sums (diagnostic build -DPIADMM_STAMPS only)
   double* rho_x;            // N   ADMM penalty per agent QP (adapted, persists across steps)
   double* rho_e;            // E   ADMM penalty per pair QP
+  double* Kx_cache;         // N*H*H agent K_s^-1 for the penalty xcache_rho[a] (per scenario)
+  double* xcache_rho;       // N   penalty of the cached agent setup (NaN: none)
+  int* ecache;              // E   1 when the pair's speed-only tables are built
 };
 
 // LDS bytes needed by one workgroup for horizon H (must match the carve in k_mpc_step).
