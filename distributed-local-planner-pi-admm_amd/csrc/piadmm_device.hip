@@ -37,7 +37,8 @@ __device__ unsigned long long* g_stamps;
 #define STAMP_ADD(slot, t0) ((void)(t0))
 #endif
 enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL, ST_ZSTEP, ST_ZQP, ST_ZRED,
-                 ST_KERNEL, ST_RED_GEMV, ST_RED_S, ST_RED_CHOL, ST_RED_X, ST_ADMM, ST_XQ, ST_TERM };
+                 ST_KERNEL, ST_RED_GEMV, ST_RED_S, ST_RED_CHOL, ST_RED_X, ST_ADMM, ST_XQ, ST_TERM,
+                 ST_SZ_RUIZ, ST_SZ_KMAT, ST_SZ_GJ, ST_SZ_PRE };
 
 // ============================================================ wave primitives
 __device__ __forceinline__ int lid() { return (int)__lane_id(); }
@@ -350,6 +351,7 @@ __device__ __forceinline__ double P_entry(const QP<NV>& P, int v, int i, int j) 
 
 template <int NV>
 __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
+  unsigned long long t_km = STAMP_T();
   const int l = lid();
   const int H = P.H, n = P.n;
   const int vc = (NV == 2 && l >= H) ? 1 : 0;
@@ -399,7 +401,10 @@ __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
     }
   }
   wsync();
+  if (NV == 2) STAMP_ADD(ST_SZ_KMAT, t_km);
+  unsigned long long t_gj = STAMP_T();
   gj_invert(m, n, ld);
+  if (NV == 2) STAMP_ADD(ST_SZ_GJ, t_gj);
   for (int r = 0; r < n; ++r)
     if (incol) P.K[r * n + l] = m[r * ld + l];
   wsync();
@@ -1103,6 +1108,7 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, n = 2 * H, l = lid();
   const bool in = l < H;
+  unsigned long long t_pre = STAMP_T();
   const double dbx = seeds[2] - seeds[0], dby = seeds[3] - seeds[1];
   const double dd = dbx * dbx + dby * dby;
   P.g1 = -2.0 * (dbx * g1.ax + dby * g1.ay);
@@ -1158,7 +1164,10 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
     if (l == 0) A.ecache[e] = 1;
     wsync();
   }
+  STAMP_ADD(ST_SZ_PRE, t_pre);
+  unsigned long long t_r = STAMP_T();
   ruiz(P);
+  STAMP_ADD(ST_SZ_RUIZ, t_r);
   build_K(P, scr, LD);
 }
 // ============================================================ the MPC-step kernel
