@@ -215,9 +215,7 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.sc_x, (size_t)N * 4 * pd::HMAX);
   rc |= dalloc(h, &A.ws_x, (size_t)N * 5 * pd::HMAX);
   rc |= dalloc(h, &A.lab_x, (size_t)N * 2 * pd::HMAX);
-  rc |= dalloc(h, &A.Pinv_e, E * 4 * H * H);
-  rc |= dalloc(h, &A.PGt, E * 2 * H * H);
-  rc |= dalloc(h, &A.GPG, E * 2 * H * H);
+  rc |= dalloc(h, &A.tab_e, E * 8 * H * H);
   rc |= dalloc(h, &A.sc_e, E * 8 * pd::HMAX);
   rc |= dalloc(h, &A.ws_e, E * 12 * pd::HMAX);
   rc |= dalloc(h, &A.lab_e, E * 5 * pd::HMAX);

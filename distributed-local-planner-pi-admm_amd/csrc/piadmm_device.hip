@@ -240,29 +240,29 @@ __device__ __forceinline__ void rollout(const double* xt3, double s, double u, c
 __device__ __forceinline__ void gj_invert(double* m, int n, int ld) {
   const int l = lid();
   const int lc = (l < n) ? l : n - 1;     // lanes >= n mirror column n-1 and never store
+  constexpr int U = 8;
   for (int p = 0; p < n; ++p) {
-    const double colp = m[lc * ld + p];   // a_lp (lane = row here)
-    const double ip = 1.0 / rdl(colp, p);
+    const double ip = 1.0 / m[p * ld + p];                 // uniform address: LDS broadcast
     const double rpj = (l == p) ? ip : m[p * ld + lc] * ip;
-    wsync();
     // every row i (row p included: it is overwritten below) -= a_ip * new row p;
-    // column p becomes -a_ip / a_pp.  Branch-free so the compiler can batch the LDS traffic.
+    // column p becomes -a_ip / a_pp.  a_ip is read as an LDS broadcast: within a group all
+    // reads come before lane p's writes of the same rows, and later groups touch later rows.
     int i = 0;
-    for (; i + 4 <= n; i += 4) {
-      double v[4], a[4];
+    for (; i + U <= n; i += U) {
+      double v[U], a[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a[u] = rdl(colp, i + u);
+      for (int u = 0; u < U; ++u) {
+        a[u] = m[(i + u) * ld + p];
         v[u] = m[(i + u) * ld + lc];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const double nv = (l == p) ? -a[u] * ip : v[u] - a[u] * rpj;
         if (l < n) m[(i + u) * ld + l] = nv;
       }
     }
     for (; i < n; ++i) {
-      const double a = rdl(colp, i);
+      const double a = m[i * ld + p];
       const double v = m[i * ld + lc];
       const double nv = (l == p) ? -a * ip : v - a * rpj;
       if (l < n) m[i * ld + l] = nv;
@@ -289,17 +289,16 @@ struct QP {
   double q[NV];
   double D[NV];
   double E[NR];
-  double lo[NR], hi[NR];
-  bool valid[NR];
+  double h0;              // hinge lower bound (pair only; 0 on invalid lanes)
+  double umax, dumax;     // box / rate bounds (uniform)
   double g1, g2;          // hinge coefficients (pair only)
   double mm[NV];          // |M|^2 factors (ax^2 + ay^2) per vehicle
   double coefP;           // x-step: 2 Pnorm + rho |N| ; pair: rho
   double Pcost2;          // 2 Pcost
   double beta, rho, sigma, alpha, tol;
   double* K;              // LDS  n x n  scaled (P_s + sigma I + rho A_s'A_s)^-1
-  const double* Pinv;     // n x n unscaled P^-1 (LDS for the x-step, HBM for the pair)
-  const double* PGt;      // HBM  H x n  row k = P_v^-1 T(k+1,.)' per vehicle block (unscaled by g)
-  const double* GPG;      // HBM  2 x H x H  Z_v = T P_v^-1 T' (GPG = g1^2 Z_1 + g2^2 Z_2)
+  const double* Pinv;     // n x n unscaled P^-1 (LDS for the x-step); for the pair the HBM
+                          // table block DevArgs::tab_e: P^-1 | PGt (+4H^2) | GPG (+6H^2)
   double* vb;             // per-wave LDS vectors (512 doubles)
   double* fac;            // LDS factor region: L (lower), S (upper), stride fld
   double* fdiag;          // LDS [2*64]: S_aa, 1/L_aa of the cached factor
@@ -309,6 +308,16 @@ struct QP {
   int mmax;               // capacity of fac (rows)
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
+  // Row s of vehicle v = s / 2: even = box (lanes < H), odd = rate (lanes < H-1), 4 = hinge
+  // (lanes 1..H-1 when the pair's geometry couples them).  Bounds are recomputed, not stored,
+  // to keep the per-lane register state of the two live QPs small.
+  __device__ __forceinline__ bool valid(int s) const {
+    const int l = lid();
+    if (hinge(s)) return l >= 1 && l < H && (g1 != 0.0 || g2 != 0.0);
+    return (s & 1) ? l < H - 1 : l < H;
+  }
+  __device__ __forceinline__ double lo(int s) const { return hinge(s) ? h0 : ((s & 1) ? -dumax : -umax); }
+  __device__ __forceinline__ double hi(int s) const { return hinge(s) ? INFINITY : ((s & 1) ? dumax : umax); }
 };
 
 template <int NV>
@@ -363,7 +372,16 @@ __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
   for (int v = 0; v < NV; ++v) Dsh[v] = __shfl(P.D[v], src);
   const double Dc = (NV == 2 && vc == 1) ? Dsh[NV - 1] : Dsh[0];
   const double gc = (vc == 0) ? P.g1 : P.g2;
-  const double Eh2 = (NV == 2 && P.valid[NR_HINGE<NV>()]) ? P.E[NR_HINGE<NV>()] * P.E[NR_HINGE<NV>()] : 0.0;
+  // hinge block of A_s'A_s: sum_{k > max(i,j)} e2_k (k-i)(k-j) = S2 - (i+j) S1 + i j S0 with
+  // suffix sums S0..S2 of e2_k k^0..2 taken at lane max(i,j)+1 (one bpermute each per row)
+  double hS0 = 0.0, hS1 = 0.0, hS2 = 0.0;
+  if constexpr (NV == 2) {
+    const double Eh2 = P.valid(NR_HINGE<NV>()) ? P.E[NR_HINGE<NV>()] * P.E[NR_HINGE<NV>()] : 0.0;
+    const double kd = (double)l;
+    hS0 = scan_incl_rev(Eh2);
+    hS1 = scan_incl_rev(Eh2 * kd);
+    hS2 = scan_incl_rev(Eh2 * kd * kd);
+  }
   for (int r = 0; r < n; ++r) {
     const int vr = (NV == 2 && r >= H) ? 1 : 0;
     const int ir = r - vr * H;
@@ -382,10 +400,10 @@ __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
     double hs = 0.0;
     if constexpr (NV == 2) {
       const double gr = (vr == 0) ? P.g1 : P.g2;
-      for (int k = 1; k < H; ++k) {
-        const double e2 = rdl(Eh2, k);
-        if (k > ir && k > jc) hs += e2 * (double)(k - ir) * (double)(k - jc);
-      }
+      const int M = max(ir, jc) + 1;
+      const int ms = (M < H) ? M : 0;
+      const double s0 = __shfl(hS0, ms), s1 = __shfl(hS1, ms), s2 = __shfl(hS2, ms);
+      if (M < H) hs = s2 - (double)(ir + jc) * s1 + (double)ir * (double)jc * s0;
       hs *= gr * gc * HINGE_RHO;
     }
     if (incol) {
@@ -414,12 +432,12 @@ __device__ __forceinline__ void A_mul(const QP<NV>& P, const double* x, double* 
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const double xn = shdn(x[v], 1);
-    ax[2 * v] = P.valid[2 * v] ? x[v] : 0.0;
-    ax[2 * v + 1] = P.valid[2 * v + 1] ? xn - x[v] : 0.0;
+    ax[2 * v] = P.valid(2 * v) ? x[v] : 0.0;
+    ax[2 * v + 1] = P.valid(2 * v + 1) ? xn - x[v] : 0.0;
   }
   if constexpr (NV == 2) {
     const double th = T_apply(P.g1 * x[0] + P.g2 * x[1]);
-    ax[4] = P.valid[4] ? th : 0.0;
+    ax[4] = P.valid(4) ? th : 0.0;
   }
 }
 
@@ -428,12 +446,12 @@ __device__ __forceinline__ void At_mul(const QP<NV>& P, const double* w, double*
   const bool in = lid() < P.H;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    const double wr = P.valid[2 * v + 1] ? w[2 * v + 1] : 0.0;
-    const double wb = P.valid[2 * v] ? w[2 * v] : 0.0;
+    const double wr = P.valid(2 * v + 1) ? w[2 * v + 1] : 0.0;
+    const double wb = P.valid(2 * v) ? w[2 * v] : 0.0;
     out[v] = wb - wr + shup(wr, 1);
   }
   if constexpr (NV == 2) {
-    const double tt = Tt_apply(P.valid[4] ? w[4] : 0.0);
+    const double tt = Tt_apply(P.valid(4) ? w[4] : 0.0);
     out[0] += P.g1 * tt;
     out[1] += P.g2 * tt;
   }
@@ -443,7 +461,11 @@ __device__ __forceinline__ void At_mul(const QP<NV>& P, const double* w, double*
 }
 
 // y = M r with M (n x n, symmetric) at row-major base (LDS or HBM), r at var lanes.
-template <int NV, typename Ptr>
+// BD: M is block-diagonal in the NV vehicle blocks (the pair's P^-1), only those are read.
+// Loads are issued GEMV_U deep before their first use so that the pair's L2-resident
+// tables cost one latency per batch, not one per column.
+constexpr int GEMV_U = 8;
+template <bool BD, int NV, typename Ptr>
 __device__ __forceinline__ void gemv_sym(const QP<NV>& P, Ptr M, const double* r, double* y) {
   const int l = lid();
   const int H = P.H, n = P.n;
@@ -456,10 +478,39 @@ __device__ __forceinline__ void gemv_sym(const QP<NV>& P, Ptr M, const double* r
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = 0.0;
   const int lc = (l < H) ? l : 0;
-  for (int j = 0; j < n; ++j) {
-    const double rj = P.vb[j];
+  if constexpr (BD) {
+    for (int j0 = 0; j0 < H; j0 += GEMV_U) {
+      double mv[NV][GEMV_U], rv[NV][GEMV_U];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) acc[v] += M[j * n + v * H + lc] * rj;
+      for (int u = 0; u < GEMV_U; ++u) {
+        const int j = min(j0 + u, H - 1);
+        const bool ok = j0 + u < H;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          mv[v][u] = M[(v * H + j) * n + v * H + lc];
+          rv[v][u] = ok ? P.vb[v * H + j] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] += mv[v][u] * rv[v][u];
+    }
+  } else {
+    for (int j0 = 0; j0 < n; j0 += GEMV_U) {
+      double mv[NV][GEMV_U], rv[GEMV_U];
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u) {
+        const int j = min(j0 + u, n - 1);
+        rv[u] = (j0 + u < n) ? P.vb[j] : 0.0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) mv[v][u] = M[j * n + v * H + lc];
+      }
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] += mv[v][u] * rv[u];
+    }
   }
   wsync();
 #pragma unroll
@@ -471,24 +522,24 @@ template <int NV>
 __device__ __forceinline__ double prox_s(const QP<NV>& P, int s, double v) {
   const double e = P.E[s];
   if (P.hinge(s)) {
-    const double hs = e * P.lo[s];
+    const double hs = e * P.lo(s);
     const double thr = (P.beta / e) / rrow(P, s);
     return v >= hs ? v : (v <= hs - thr ? v + thr : hs);
   }
-  return fmin(fmax(v, e * P.lo[s]), e * P.hi[s]);
+  return fmin(fmax(v, e * P.lo(s)), e * P.hi(s));
 }
 
 // label from a prox input in scaled units (ADMM state)
 template <int NV>
 __device__ __forceinline__ signed char label_scaled(const QP<NV>& P, int s, double v) {
   const double e = P.E[s];
-  if (!P.valid[s]) return 0;
+  if (!P.valid(s)) return 0;
   if (P.hinge(s)) {
-    const double hs = e * P.lo[s];
+    const double hs = e * P.lo(s);
     const double thr = (P.beta / e) / rrow(P, s);
     return v >= hs ? HZERO : (v <= hs - thr ? HLINEAR : HKINK);
   }
-  return v <= e * P.lo[s] ? LOWER : (v >= e * P.hi[s] ? UPPER : FREE);
+  return v <= e * P.lo(s) ? LOWER : (v >= e * P.hi(s) ? UPPER : FREE);
 }
 
 template <int NV>
@@ -496,11 +547,11 @@ __device__ __forceinline__ void admm_iter(const QP<NV>& P, double* xs, double* z
   constexpr int NR = QP<NV>::NR;
   double w[NR], t[NV], rhs[NV], xt[NV], xu[NV], a[NR];
 #pragma unroll
-  for (int s = 0; s < NR; ++s) w[s] = P.valid[s] ? P.E[s] * (rrow(P, s) * zs[s] - ys[s]) : 0.0;
+  for (int s = 0; s < NR; ++s) w[s] = P.valid(s) ? P.E[s] * (rrow(P, s) * zs[s] - ys[s]) : 0.0;
   At_mul(P, w, t);
 #pragma unroll
   for (int v = 0; v < NV; ++v) rhs[v] = P.sigma * xs[v] - P.D[v] * P.q[v] + P.D[v] * t[v];
-  gemv_sym(P, P.K, rhs, xt);
+  gemv_sym<false>(P, P.K, rhs, xt);
 #pragma unroll
   for (int v = 0; v < NV; ++v) xu[v] = P.D[v] * xt[v];
   A_mul(P, xu, a);
@@ -508,7 +559,7 @@ __device__ __forceinline__ void admm_iter(const QP<NV>& P, double* xs, double* z
   for (int v = 0; v < NV; ++v) xs[v] = P.alpha * xt[v] + (1.0 - P.alpha) * xs[v];
 #pragma unroll
   for (int s = 0; s < NR; ++s) {
-    if (!P.valid[s]) {
+    if (!P.valid(s)) {
       zs[s] = ys[s] = 0.0;
       continue;
     }
@@ -551,40 +602,39 @@ __device__ __forceinline__ RowT row_terms(const QP<NV>& P, int id) {
 template <int NV>
 __device__ __forceinline__ double gvar(const QP<NV>& P, int i) { return i < P.H ? P.g1 : P.g2; }
 
+// Gather form: an entry of S = A_W P^-1 A_W' is sum_t c[t] P.Pinv[o[t]] over at most four
+// terms (the pair's PGt / GPG follow P^-1 in the same per-edge block at +4H^2 / +6H^2),
+// so a batch of entries issues all its loads before the first use.
+struct Gather4 {
+  int o[4];
+  double c[4];
+};
 template <int NV>
-__device__ __forceinline__ double s_entry(const QP<NV>& P, int ia, int ibd) {
+__device__ __forceinline__ Gather4 s_gather(const QP<NV>& P, int ia, int ibd) {
   const RowT a = row_terms(P, ia), b = row_terms(P, ibd);
-  const int n = P.n;
+  const int n = P.n, HH = P.H * P.H;
+  Gather4 g;
   if (a.hk < 0 && b.hk < 0) {
-    double s = a.c0 * b.c0 * P.Pinv[a.i0 * n + b.i0];
-    if (b.c1 != 0.0) s += a.c0 * b.c1 * P.Pinv[a.i0 * n + b.i1];
-    if (a.c1 != 0.0) {
-      s += a.c1 * b.c0 * P.Pinv[a.i1 * n + b.i0];
-      if (b.c1 != 0.0) s += a.c1 * b.c1 * P.Pinv[a.i1 * n + b.i1];
-    }
-    return s;
+    g.o[0] = a.i0 * n + b.i0; g.c[0] = a.c0 * b.c0;
+    g.o[1] = a.i0 * n + b.i1; g.c[1] = a.c0 * b.c1;
+    g.o[2] = a.i1 * n + b.i0; g.c[2] = a.c1 * b.c0;
+    g.o[3] = a.i1 * n + b.i1; g.c[3] = a.c1 * b.c1;
+    return g;
   }
-  if (a.hk < 0) {
-    double s = a.c0 * gvar(P, a.i0) * P.PGt[b.hk * n + a.i0];
-    if (a.c1 != 0.0) s += a.c1 * gvar(P, a.i1) * P.PGt[b.hk * n + a.i1];
-    return s;
+  g.o[2] = g.o[3] = 0;
+  g.c[2] = g.c[3] = 0.0;
+  if (a.hk < 0 || b.hk < 0) {
+    const RowT& bx = (a.hk < 0) ? a : b;
+    const int hk = (a.hk < 0) ? b.hk : a.hk;
+    const int base = 4 * HH + hk * n;
+    g.o[0] = base + bx.i0; g.c[0] = bx.c0 * gvar(P, bx.i0);
+    g.o[1] = base + bx.i1; g.c[1] = bx.c1 * gvar(P, bx.i1);
+    return g;
   }
-  if (b.hk < 0) {
-    double s = b.c0 * gvar(P, b.i0) * P.PGt[a.hk * n + b.i0];
-    if (b.c1 != 0.0) s += b.c1 * gvar(P, b.i1) * P.PGt[a.hk * n + b.i1];
-    return s;
-  }
-  const int HH = P.H * P.H;
-  return P.g1 * P.g1 * P.GPG[a.hk * P.H + b.hk] + P.g2 * P.g2 * P.GPG[HH + a.hk * P.H + b.hk];
-}
-// (P^-1 a_id) at variable index i
-template <int NV>
-__device__ __forceinline__ double pcol(const QP<NV>& P, int id, int i) {
-  const RowT a = row_terms(P, id);
-  if (a.hk >= 0) return gvar(P, i) * P.PGt[a.hk * P.n + i];
-  double s = a.c0 * P.Pinv[a.i0 * P.n + i];
-  if (a.c1 != 0.0) s += a.c1 * P.Pinv[a.i1 * P.n + i];
-  return s;
+  const int base = 6 * HH + a.hk * P.H + b.hk;
+  g.o[0] = base; g.c[0] = P.g1 * P.g1;
+  g.o[1] = base + HH; g.c[1] = P.g2 * P.g2;
+  return g;
 }
 
 // Solve L L' x = b (lane a holds b_a, a < m).  L lower in fac (stride ld), linv = 1/L_aa.
@@ -656,7 +706,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
 #pragma unroll
   for (int v = 0; v < NV; ++v) qt[v] = P.q[v];
   if constexpr (NV == 2) {
-    const double lin = (P.valid[4] && lab[4] == HLINEAR) ? 1.0 : 0.0;
+    const double lin = (P.valid(4) && lab[4] == HLINEAR) ? 1.0 : 0.0;
     const double tt = Tt_apply(lin);
     if (l < H) {
       qt[0] -= P.beta * P.g1 * tt;
@@ -665,7 +715,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
   }
   double x0[NV];
   unsigned long long t_rs = STAMP_T();
-  gemv_sym(P, P.Pinv, qt, x0);
+  gemv_sym<true>(P, P.Pinv, qt, x0);
   STAMP_ADD(ST_RED_GEMV, t_rs);
 #pragma unroll
   for (int v = 0; v < NV; ++v) x0[v] = -x0[v];
@@ -676,7 +726,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
   const unsigned long long ltmask = (l == 0) ? 0ull : (~0ull >> (64 - l));
 #pragma unroll
   for (int s = 0; s < NR; ++s) {
-    inW[s] = P.valid[s] && (P.hinge(s) ? (lab[s] == HKINK) : (lab[s] != FREE));
+    inW[s] = P.valid(s) && (P.hinge(s) ? (lab[s] == HKINK) : (lab[s] != FREE));
     const unsigned long long bm = __ballot(inW[s]);
     pos[s] = m + __popcll(bm & ltmask);
     m += __popcll(bm);
@@ -689,7 +739,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     if (l < H) vb_ax[s * H + l] = ax0[s];
     if (inW[s]) {
       ids[pos[s]] = s * H + l;
-      vb_b[pos[s]] = P.hinge(s) ? P.lo[s] : (lab[s] == LOWER ? P.lo[s] : P.hi[s]);
+      vb_b[pos[s]] = P.hinge(s) ? P.lo(s) : (lab[s] == LOWER ? P.lo(s) : P.hi(s));
     }
   }
   wsync();
@@ -697,7 +747,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
 #pragma unroll
     for (int v = 0; v < NV; ++v) x[v] = x0[v];
 #pragma unroll
-    for (int s = 0; s < NR; ++s) y[s] = (P.hinge(s) && P.valid[s] && lab[s] == HLINEAR) ? -P.beta : 0.0;
+    for (int s = 0; s < NR; ++s) y[s] = (P.hinge(s) && P.valid(s) && lab[s] == HLINEAR) ? -P.beta : 0.0;
     return true;
   }
   const int myid = (l < m) ? ids[l] : 0;
@@ -711,12 +761,24 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     // S (upper triangle) into fac: lane a = row a, columns b >= a
     unsigned long long t_s = STAMP_T();
     sdiag = 0.0;
-    for (int b = 0; b < m; ++b) {
-      const int idb = rdli(myid, b);
-      if (l <= b && l < m) {
-        const double sv = s_entry(P, myid, idb);
-        if (b == l) sdiag = sv;
-        else P.fac[l * ld + b] = sv;
+    constexpr int SB = 4;
+    for (int b0 = 0; b0 < m; b0 += SB) {
+      Gather4 gg[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) gg[u] = s_gather(P, myid, rdli(myid, min(b0 + u, m - 1)));
+      double tv[SB][4];
+#pragma unroll
+      for (int u = 0; u < SB; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tv[u][k] = P.Pinv[gg[u].o[k]];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int b = b0 + u;
+        const double sv = gg[u].c[0] * tv[u][0] + gg[u].c[1] * tv[u][1] + gg[u].c[2] * tv[u][2] + gg[u].c[3] * tv[u][3];
+        if (b < m && l <= b && l < m) {
+          if (b == l) sdiag = sv;
+          else P.fac[l * ld + b] = sv;
+        }
       }
     }
     STAMP_ADD(ST_RED_S, t_s);
@@ -760,12 +822,41 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
   double xv[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) xv[v] = x0[v];
-  for (int a = 0; a < m; ++a) {
-    const int ida = rdli(myid, a);
-    const double la = rdl(lamv, a);
-    if (l < H) {
+  {
+    constexpr int XB = 4;
+    const int lc = (l < H) ? l : 0;
+    for (int a0 = 0; a0 < m; a0 += XB) {
+      int o[XB][NV][2];
+      double cf[XB][NV][2], la[XB];
 #pragma unroll
-      for (int v = 0; v < NV; ++v) xv[v] -= pcol(P, ida, v * H + l) * la;
+      for (int u = 0; u < XB; ++u) {
+        const int a = min(a0 + u, m - 1);
+        const RowT r = row_terms(P, rdli(myid, a));
+        la[u] = (a0 + u < m) ? rdl(lamv, a) : 0.0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int i = v * H + lc;
+          if (NV == 2 && r.hk >= 0) {        // (P^-1 G_k')_i, unscaled table times g_v
+            o[u][v][0] = o[u][v][1] = 4 * H * H + r.hk * P.n + i;
+            cf[u][v][0] = v ? P.g2 : P.g1;
+            cf[u][v][1] = 0.0;
+          } else {
+            o[u][v][0] = r.i0 * P.n + i; cf[u][v][0] = r.c0;
+            o[u][v][1] = r.i1 * P.n + i; cf[u][v][1] = r.c1;
+          }
+        }
+      }
+      double tv[XB][NV][2];
+#pragma unroll
+      for (int u = 0; u < XB; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+          for (int k = 0; k < 2; ++k) tv[u][v][k] = P.Pinv[o[u][v][k]];
+#pragma unroll
+      for (int u = 0; u < XB; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xv[v] -= (cf[u][v][0] * tv[u][v][0] + cf[u][v][1] * tv[u][v][1]) * la[u];
     }
   }
   STAMP_ADD(ST_RED_X, t_x);
@@ -776,7 +867,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
 #pragma unroll
   for (int s = 0; s < NR; ++s) {
     if (inW[s]) y[s] = vb_lam[pos[s]];
-    else if (P.hinge(s) && P.valid[s] && lab[s] == HLINEAR) y[s] = -P.beta;
+    else if (P.hinge(s) && P.valid(s) && lab[s] == HLINEAR) y[s] = -P.beta;
     else y[s] = 0.0;
   }
   wsync();
@@ -798,24 +889,24 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
   bool ok = true;
 #pragma unroll
   for (int s = 0; s < NR; ++s) {
-    if (!P.valid[s]) {
+    if (!P.valid(s)) {
       nlab[s] = 0;
       continue;
     }
-    const double tp = P.tol * (1.0 + fabs(P.lo[s]));
+    const double tp = P.tol * (1.0 + fabs(P.lo(s)));
     const double c = rrow(P, s) * P.E[s] * P.E[s];
     const double wv = ax[s] + y[s] / c;
     if (P.hinge(s)) {
-      const double h = P.lo[s];
+      const double h = P.lo(s);
       if (lab[s] == HZERO) ok &= ax[s] >= h - tp;
       else if (lab[s] == HLINEAR) ok &= ax[s] <= h + tp;
       else ok &= (y[s] <= ty) && (y[s] >= -P.beta - ty);
       nlab[s] = wv >= h ? HZERO : (wv <= h - P.beta / c ? HLINEAR : HKINK);
     } else {
-      if (lab[s] == FREE) ok &= (ax[s] >= P.lo[s] - tp) && (ax[s] <= P.hi[s] + tp);
+      if (lab[s] == FREE) ok &= (ax[s] >= P.lo(s) - tp) && (ax[s] <= P.hi(s) + tp);
       else if (lab[s] == LOWER) ok &= y[s] <= ty;
       else ok &= y[s] >= -ty;
-      nlab[s] = wv <= P.lo[s] ? LOWER : (wv >= P.hi[s] ? UPPER : FREE);
+      nlab[s] = wv <= P.lo(s) ? LOWER : (wv >= P.hi(s) ? UPPER : FREE);
     }
     ok &= isfinite(x[0]) && isfinite(y[s]);
   }
@@ -854,12 +945,12 @@ __device__ __forceinline__ double rho_ratio(const QP<NV>& P, const double* xs, c
   A_mul(P, xu, ax);
   P_mul(P, xu, px);
 #pragma unroll
-  for (int s = 0; s < NR; ++s) w[s] = P.valid[s] ? P.E[s] * ys[s] : 0.0;
+  for (int s = 0; s < NR; ++s) w[s] = P.valid(s) ? P.E[s] * ys[s] : 0.0;
   At_mul(P, w, aty);
   double rp = 0.0, na = 0.0, rd = 0.0, nd = 0.0;
 #pragma unroll
   for (int s = 0; s < NR; ++s) {
-    if (!P.valid[s]) continue;
+    if (!P.valid(s)) continue;
     const double a = P.E[s] * ax[s];
     rp = fmax(rp, fabs(a - zs[s]));
     na = fmax(na, fmax(fabs(a), fabs(zs[s])));
@@ -946,8 +1037,8 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
     for (int v = 0; v < NV; ++v) xs[v] = (P.D[v] != 0.0) ? x[v] / P.D[v] : 0.0;
 #pragma unroll
     for (int s = 0; s < NR; ++s) {
-      zs[s] = P.valid[s] ? P.E[s] * ax[s] : 0.0;
-      ys[s] = P.valid[s] ? y[s] / P.E[s] : 0.0;
+      zs[s] = P.valid(s) ? P.E[s] * ax[s] : 0.0;
+      ys[s] = P.valid(s) ? y[s] / P.E[s] : 0.0;
     }
   } else {
     st |= PIADMM_QP_INEXACT;
@@ -978,7 +1069,7 @@ __device__ __forceinline__ void ruiz(QP<NV>& P) {
     P.E[2 * v] = in ? 1.0 : 0.0;
     P.E[2 * v + 1] = (l < H - 1) ? 1.0 : 0.0;
   }
-  if constexpr (NV == 2) P.E[4] = P.valid[4] ? 1.0 : 0.0;
+  if constexpr (NV == 2) P.E[4] = P.valid(4) ? 1.0 : 0.0;
   const double ag[2] = {fabs(P.g1), fabs(P.g2)};
   for (int it = 0; it < RUIZ_ITERS; ++it) {
     double cn[NV], rn[NR];
@@ -1015,7 +1106,7 @@ __device__ __forceinline__ void ruiz(QP<NV>& P) {
       if (l < H - 1) P.E[2 * v + 1] *= 1.0 / sqrt(clamp_norm(rn[2 * v + 1]));
     }
     if constexpr (NV == 2) {
-      if (P.valid[4]) P.E[4] *= 1.0 / sqrt(clamp_norm(rn[4]));
+      if (P.valid(4)) P.E[4] *= 1.0 / sqrt(clamp_norm(rn[4]));
     }
   }
 }
@@ -1026,15 +1117,11 @@ struct WaveMem {
 };
 
 __device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, double rho0, QP<1>& P) {
-  const int l = lid();
   P.H = H;
   P.n = H;
-  P.lo[0] = -c.u_max;
-  P.hi[0] = c.u_max;
-  P.lo[1] = -c.du_max;
-  P.hi[1] = c.du_max;
-  P.valid[0] = l < H;
-  P.valid[1] = l < H - 1;
+  P.umax = c.u_max;
+  P.dumax = c.du_max;
+  P.h0 = 0.0;
   P.g1 = P.g2 = 0.0;
   P.Pcost2 = 2.0 * c.Pcost;
   P.beta = 0.0;
@@ -1042,8 +1129,6 @@ __device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, doubl
   P.sigma = c.admm_sigma;
   P.alpha = c.admm_alpha;
   P.tol = c.qp_tol;
-  P.PGt = nullptr;
-  P.GPG = nullptr;
 }
 
 // x-step QP of agent a (cost_function_primal, PI_ADMM_class.py:114-135, constraints :172-192):
@@ -1115,19 +1200,17 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
   P.g2 = 2.0 * (dbx * g2.ax + dby * g2.ay);
   const double Dsq = c.dis_thres * c.dis_thres;
   const double h_time = Dsq + dd - 2.0 * (dbx * (c2x - c1x) + dby * (c2y - c1y));
-  P.lo[4] = shdn(h_time, 1);                 // hinge lane k <-> time k+1
-  P.hi[4] = INFINITY;
-  P.valid[4] = (l >= 1) && in && (P.g1 != 0.0 || P.g2 != 0.0);
-  if (!P.valid[4]) P.lo[4] = 0.0;
+  P.h0 = shdn(h_time, 1);                    // hinge lane k <-> time k+1
+  if (!P.valid(4)) P.h0 = 0.0;
   P.coefP = c.rho;
   P.mm[0] = g1.mm;
   P.mm[1] = g2.mm;
 
   // ---- P_v^-1 blocks (HBM), Y = P_v^-1 T' (PGt, unscaled by g) and Z_v = T P_v^-1 T' (GPG):
-  // speed-only, so built once per scenario; g1, g2 scale them on the fly (s_entry, pcol)
+  // speed-only, so built once per scenario; g1, g2 scale them on the fly (s_gather, x recovery)
   if (!A.ecache[e]) {
     double* Yl = Ke_lds;             // H x n staging (the Ke region is rebuilt below)
-    double* Pi = A.Pinv_e + (size_t)e * n * n;
+    double* Pi = A.tab_e + (size_t)e * 8 * H * H;
     for (int v = 0; v < 2; ++v) {
       for (int i = 0; i < H; ++i)
         if (in) scr[i * LD + l] = P_entry(P, v, i, l);
@@ -1148,8 +1231,8 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
       }
       wsync();
     }
-    double* Zg = A.GPG + (size_t)e * 2 * H * H;
-    double* Pg = A.PGt + (size_t)e * H * n;
+    double* Pg = Pi + 4 * H * H;
+    double* Zg = Pi + 6 * H * H;
     const int b = in ? l : 0;
     for (int v = 0; v < 2; ++v) {
       double B = 0.0, Z = 0.0;
@@ -1271,19 +1354,15 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   double c1x = 0.0, c1y = 0.0, c2x = 0.0, c2y = 0.0;
   if (w == 0 && e >= 0) {
     unsigned long long t0 = STAMP_T();
-    const bool in = l < H;
     ge1 = make_geo(S.xt + 0, A.spd[a0], c);
     ge2 = make_geo(S.xt + 3, A.spd[a0 + 1], c);
     affine_c(ge1, c.dt, H, c1x, c1y);
     affine_c(ge2, c.dt, H, c2x, c2y);
     qe.H = H;
     qe.n = 2 * H;
-    qe.lo[0] = qe.lo[2] = -c.u_max;
-    qe.hi[0] = qe.hi[2] = c.u_max;
-    qe.lo[1] = qe.lo[3] = -c.du_max;
-    qe.hi[1] = qe.hi[3] = c.du_max;
-    qe.valid[0] = qe.valid[2] = in;
-    qe.valid[1] = qe.valid[3] = l < H - 1;
+    qe.umax = c.u_max;
+    qe.dumax = c.du_max;
+    qe.h0 = 0.0;
     qe.Pcost2 = 2.0 * c.Pcost;
     qe.beta = c.beta;
     qe.rho = A.rho_e[e];
@@ -1291,9 +1370,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     qe.alpha = c.admm_alpha;
     qe.tol = c.qp_tol;
     qe.K = Ke;
-    qe.Pinv = A.Pinv_e + (size_t)e * 4 * H * H;
-    qe.PGt = A.PGt + (size_t)e * 2 * H * H;
-    qe.GPG = A.GPG + (size_t)e * 2 * H * H;
+    qe.Pinv = A.tab_e + (size_t)e * 8 * H * H;
     qe.vb = wm.vb;
     qe.fac = scr;
     qe.fdiag = zdiag;

@@ -41,9 +41,9 @@ struct DevArgs {
   double* sc_x;             // N*4*HMAX   (D, Ebox, Erate, spare)
   double* ws_x;             // N*5*HMAX   warm ADMM state (xs, zs0, zs1, ys0, ys1)
   signed char* lab_x;       // N*2*HMAX
-  double* Pinv_e;           // E*(2H)*(2H)
-  double* PGt;              // E*H*(2H)   row k = P^-1 G_k'
-  double* GPG;              // E*2*H*H    Z_v = T P_v^-1 T'
+  double* tab_e;            // E * 8H^2 polish tables per edge, one block each:
+                            //   [0, 4H^2) P^-1 (2H x 2H, block-diagonal), [4H^2, 6H^2) PGt (H x 2H,
+                            //   row k = P_v^-1 T(k+1,.)'), [6H^2, 8H^2) GPG (Z_v = T P_v^-1 T')
   double* sc_e;             // E*8*HMAX   (D1, D2, Eb1, Er1, Eb2, Er2, Eh, h0)
   double* ws_e;             // E*12*HMAX  (xs0, xs1, zs0..4, ys0..4)
   signed char* lab_e;       // E*5*HMAX

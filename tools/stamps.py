@@ -25,3 +25,10 @@ tot = st[:, 9].mean()
 for i, n in enumerate(NAMES):
     v = st[:, i].mean()
     print(f"  {n:10s} mean cycles/comp/step {v/steps:14.0f}  ({100*v/tot:6.1f}% of kernel)  max {st[:, i].max()/steps:14.0f}")
+cc = s.component_counters()     # outer, x_qps, z_qps, admm_x, admm_z, pdas_x, pdas_z, inexact
+order = np.argsort(-st[:, 9])
+print("z_qps per comp per step histogram:", np.bincount(cc[:, 2] // steps))
+print("slowest components (cycles/step): kernel setup_z xstep zstep zqp zred admm | z_qps admm_z pdas_z (per step)")
+for k in order[:6]:
+    print(f"  comp {k:4d}: " + " ".join(f"{st[k, j]/steps:9.0f}" for j in (9, 1, 2, 6, 7, 8, 14)) +
+          f" | {cc[k, 2]/steps:5.2f} {cc[k, 4]/steps:7.1f} {cc[k, 6]/steps:6.1f}")
