@@ -38,7 +38,8 @@ __device__ unsigned long long* g_stamps;
 #endif
 enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL, ST_ZSTEP, ST_ZQP, ST_ZRED,
                  ST_KERNEL, ST_RED_GEMV, ST_RED_S, ST_RED_CHOL, ST_RED_X, ST_ADMM, ST_XQ, ST_TERM,
-                 ST_SZ_RUIZ, ST_SZ_KMAT, ST_SZ_GJ, ST_SZ_PRE };
+                 ST_SZ_RUIZ, ST_SZ_KMAT, ST_SZ_GJ, ST_SZ_PRE, ST_ZR_GEMV, ST_ZR_S, ST_ZR_CHOL, ST_ZR_X,
+                 ST_ZR_SOLVE, ST_XR_SOLVE, ST_ZKKT, ST_XKKT };
 
 // ============================================================ wave primitives
 __device__ __forceinline__ int lid() { return (int)__lane_id(); }
@@ -300,6 +301,7 @@ struct QP {
   const double* Pinv;     // n x n unscaled P^-1 (LDS for the x-step); for the pair the HBM
                           // table block DevArgs::tab_e: P^-1 | PGt (+4H^2) | GPG (+6H^2)
   double* vb;             // per-wave LDS vectors (512 doubles)
+  double* XT;             // x-step: per-wave LDS X' (H rows, stride XLD) and beta (row H)
   double* fac;            // LDS factor region: L (lower), S (upper), stride fld
   double* fdiag;          // LDS [2*64]: S_aa, 1/L_aa of the cached factor
   int* ib;                // per-wave LDS ints: [0,64) current W ids, [64,128) cached W ids
@@ -716,7 +718,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
   double x0[NV];
   unsigned long long t_rs = STAMP_T();
   gemv_sym<true>(P, P.Pinv, qt, x0);
-  STAMP_ADD(ST_RED_GEMV, t_rs);
+  STAMP_ADD(NV == 1 ? ST_RED_GEMV : ST_ZR_GEMV, t_rs);
 #pragma unroll
   for (int v = 0; v < NV; ++v) x0[v] = -x0[v];
   // working set, compacted in slot-major order
@@ -781,14 +783,14 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
         }
       }
     }
-    STAMP_ADD(ST_RED_S, t_s);
+    STAMP_ADD(NV == 1 ? ST_RED_S : ST_ZR_S, t_s);
     unsigned long long t_c = STAMP_T();
     const double dmax = wmax(l < m ? sdiag : 0.0);
     const double delta = 1e-14 * dmax;
     wsync();
     linv = 0.0;
     const bool fok = chol_factor(P.fac, ld, sdiag, delta, m, linv);
-    STAMP_ADD(ST_RED_CHOL, t_c);
+    STAMP_ADD(NV == 1 ? ST_RED_CHOL : ST_ZR_CHOL, t_c);
     if (!fok) {
       if (l == 0) P.fstate[0] = -1;
       wsync();
@@ -802,6 +804,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     if (l == 0) P.fstate[0] = m;
     wsync();
   }
+  unsigned long long t_sv = STAMP_T();
   double lamv = chol_solve(P.fac, ld, linv, rhs, m);
   // one step of iterative refinement against the unregularised S
   {
@@ -816,6 +819,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     const double r = (l < m) ? rhs - sl : 0.0;
     lamv += chol_solve(P.fac, ld, linv, r, m);
   }
+  STAMP_ADD(NV == 1 ? ST_XR_SOLVE : ST_ZR_SOLVE, t_sv);
   if (!isfinite(lamv)) return false;
   unsigned long long t_x = STAMP_T();
   // x = x0 - sum_a (P^-1 a_a) lam_a
@@ -859,7 +863,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
         for (int v = 0; v < NV; ++v) xv[v] -= (cf[u][v][0] * tv[u][v][0] + cf[u][v][1] * tv[u][v][1]) * la[u];
     }
   }
-  STAMP_ADD(ST_RED_X, t_x);
+  STAMP_ADD(NV == 1 ? ST_RED_X : ST_ZR_X, t_x);
   if (l < m) vb_lam[l] = lamv;
   wsync();
 #pragma unroll
@@ -870,6 +874,221 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     else if (P.hinge(s) && P.valid(s) && lab[s] == HLINEAR) y[s] = -P.beta;
     else y[s] = 0.0;
   }
+  wsync();
+  return true;
+}
+
+// x-step (NV = 1) polish in parametric form.  P and A are fixed for the whole MPC step and
+// only q changes between outer iterations, so for a working set W with bounds b
+//   lam = S^-1 (A_W x0 - b) = -X q - beta,   x = x0 - Y lam,   x0 = -P^-1 q,
+// with Y = P^-1 A_W', S = A_W Y, X = S^-1 Y', beta = S^-1 b.  X' (rows = variables) and
+// beta (row H) are rebuilt in LDS only when W or the bound side of one of its rows changes;
+// a hit costs one fused pass over P^-1 and X' plus the x recovery.
+__device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, const int* ids, const double* vb_b) {
+  const int l = lid(), H = P.H, ld = P.fld;
+  double* fac = P.fac;
+  double* XT = P.XT;
+  // S (upper triangle, lane a = row a) from the LDS P^-1
+  unsigned long long t_s = STAMP_T();
+  double sdiag = 0.0;
+  constexpr int SB = 4;
+  for (int b0 = 0; b0 < m; b0 += SB) {
+    Gather4 gg[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) gg[u] = s_gather(P, myid, ids[min(b0 + u, m - 1)]);
+    double tv[SB][4];
+#pragma unroll
+    for (int u = 0; u < SB; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tv[u][k] = P.Pinv[gg[u].o[k]];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int b = b0 + u;
+      const double sv = gg[u].c[0] * tv[u][0] + gg[u].c[1] * tv[u][1] + gg[u].c[2] * tv[u][2] + gg[u].c[3] * tv[u][3];
+      if (b < m && l <= b && l < m) {
+        if (b == l) sdiag = sv;
+        else fac[l * ld + b] = sv;
+      }
+    }
+  }
+  STAMP_ADD(ST_RED_S, t_s);
+  unsigned long long t_c = STAMP_T();
+  wsync();
+  double linv = 0.0;
+  // the same relative shift as the pair's factor: a transiently dependent W (PDAS label
+  // updates can propose one) still yields a usable step instead of an overflowing one
+  const double dmax = wmax(l < m ? sdiag : 0.0);
+  if (!chol_factor(fac, ld, sdiag, 1e-14 * dmax, m, linv)) return false;
+  if (l < m) P.fdiag[64 + l] = linv;
+  STAMP_ADD(ST_RED_CHOL, t_c);
+  unsigned long long t_x = STAMP_T();
+  // right-hand sides, one per lane: lane i < H -> row i of Y = P^-1 A_W', lane H -> b
+  const int li = (l <= H) ? l : H;
+  const bool own = l <= H;
+  double* xr = XT + li * XLD;
+  constexpr int XB = 4;
+  for (int a0 = 0; a0 < m; a0 += XB) {
+    int o[XB][2];
+    double cf[XB][2];
+#pragma unroll
+    for (int u = 0; u < XB; ++u) {
+      const RowT r = row_terms(P, ids[min(a0 + u, m - 1)]);
+      const int i = (l < H) ? l : 0;
+      o[u][0] = r.i0 * H + i; cf[u][0] = r.c0;
+      o[u][1] = r.i1 * H + i; cf[u][1] = r.c1;
+    }
+    double tv[XB][2];
+#pragma unroll
+    for (int u = 0; u < XB; ++u) {
+      tv[u][0] = P.Pinv[o[u][0]];
+      tv[u][1] = P.Pinv[o[u][1]];
+    }
+#pragma unroll
+    for (int u = 0; u < XB; ++u) {
+      const int a = a0 + u;
+      if (a < m) {
+        const double v = (l < H) ? cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1] : vb_b[a];
+        if (own) xr[a] = v;
+      }
+    }
+  }
+  wsync();
+  // L L' sol = rhs for every lane's right-hand side (L broadcast from fac, lane-own sol)
+  constexpr int TB = 8;
+  for (int a = 0; a < m; ++a) {
+    double acc = xr[a];
+    for (int b0 = 0; b0 < a; b0 += TB) {
+      double Lv[TB], sv[TB];
+#pragma unroll
+      for (int u = 0; u < TB; ++u) {
+        const int b = min(b0 + u, a - 1);
+        Lv[u] = (b0 + u < a) ? fac[a * ld + b] : 0.0;
+        sv[u] = xr[b];
+      }
+#pragma unroll
+      for (int u = 0; u < TB; ++u) acc -= Lv[u] * sv[u];
+    }
+    acc *= P.fdiag[64 + a];
+    if (own) xr[a] = acc;
+  }
+  for (int a = m - 1; a >= 0; --a) {
+    double acc = xr[a];
+    for (int b0 = a + 1; b0 < m; b0 += TB) {
+      double Lv[TB], sv[TB];
+#pragma unroll
+      for (int u = 0; u < TB; ++u) {
+        const int b = min(b0 + u, m - 1);
+        Lv[u] = (b0 + u < m) ? fac[b * ld + a] : 0.0;
+        sv[u] = xr[b];
+      }
+#pragma unroll
+      for (int u = 0; u < TB; ++u) acc -= Lv[u] * sv[u];
+    }
+    acc *= P.fdiag[64 + a];
+    if (own) xr[a] = acc;
+  }
+  wsync();
+  STAMP_ADD(ST_XR_SOLVE, t_x);
+  return true;
+}
+
+__device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed char* lab, double* x, double* y) {
+  const int l = lid(), H = P.H;
+  double* vb_q = P.vb;             // [0,64) q
+  double* vb_b = P.vb + 64;        // [64,128) rhs b of W rows
+  double* vb_lam = P.vb + 128;     // [128,192)
+  int* ids = P.ib;                 // current W
+  int* cids = P.ib + 64;           // W (with bound sides) of the cached X', beta
+  const double* XT = P.XT;
+  bool inW[2];
+  int pos[2];
+  int m = 0;
+  const unsigned long long ltmask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    inW[s] = P.valid(s) && lab[s] != FREE;
+    const unsigned long long bm = __ballot(inW[s]);
+    pos[s] = m + __popcll(bm & ltmask);
+    m += __popcll(bm);
+  }
+  if (m > P.mmax) return false;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if (inW[s]) {
+      ids[pos[s]] = s * H + l;
+      vb_b[pos[s]] = (lab[s] == LOWER) ? P.lo(s) : P.hi(s);
+    }
+  }
+  if (l < H) vb_q[l] = P.q[0];
+  wsync();
+  const int myid = (l < m) ? ids[l] : 0;
+  const int key = myid + ((l < m && vb_b[l] > 0.0) ? (1 << 20) : 0);
+  const bool cached = (P.fstate[0] == m) && wall(l >= m || cids[l] == key);
+  if (!cached) {
+    if (!param_build_x(P, m, myid, ids, vb_b)) {
+      if (l == 0) P.fstate[0] = -1;
+      wsync();
+      return false;
+    }
+    if (l < m) cids[l] = key;
+    if (l == 0) P.fstate[0] = m;
+    wsync();
+  }
+  unsigned long long t_rs = STAMP_T();
+  // fused pass: x0 = -P^-1 q (lane = variable), lam = -X q - beta (lane = W row)
+  double ap = 0.0, ax = 0.0;
+  {
+    const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
+    for (int j0 = 0; j0 < H; j0 += GEMV_U) {
+      double qv[GEMV_U], pv[GEMV_U], xv[GEMV_U];
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u) {
+        const int j = min(j0 + u, H - 1);
+        qv[u] = (j0 + u < H) ? vb_q[j] : 0.0;
+        pv[u] = P.Pinv[j * H + lc];
+        xv[u] = XT[j * XLD + la];
+      }
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u) {
+        ap += pv[u] * qv[u];
+        ax += xv[u] * qv[u];
+      }
+    }
+    if (l < m) vb_lam[l] = -ax - XT[H * XLD + l];
+  }
+  wsync();
+  STAMP_ADD(ST_RED_GEMV, t_rs);
+  unsigned long long t_x = STAMP_T();
+  // x = x0 - Y lam
+  double xv = -ap;
+  {
+    constexpr int XB = 4;
+    const int lc = (l < H) ? l : 0;
+    for (int a0 = 0; a0 < m; a0 += XB) {
+      int o[XB][2];
+      double cf[XB][2], la[XB];
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        const int a = min(a0 + u, m - 1);
+        const RowT r = row_terms(P, ids[a]);
+        la[u] = (a0 + u < m) ? vb_lam[a] : 0.0;
+        o[u][0] = r.i0 * H + lc; cf[u][0] = r.c0;
+        o[u][1] = r.i1 * H + lc; cf[u][1] = r.c1;
+      }
+      double tv[XB][2];
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        tv[u][0] = P.Pinv[o[u][0]];
+        tv[u][1] = P.Pinv[o[u][1]];
+      }
+#pragma unroll
+      for (int u = 0; u < XB; ++u) xv -= (cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1]) * la[u];
+    }
+  }
+  STAMP_ADD(ST_RED_X, t_x);
+  x[0] = (l < H) ? xv : 0.0;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) y[s] = inW[s] ? vb_lam[pos[s]] : 0.0;
   wsync();
   return true;
 }
@@ -920,10 +1139,15 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
   for (int it = 0; it < PDAS_STEPS; ++it) {
     ++nsolve;
     unsigned long long t_r = STAMP_T();
-    const bool rs_ok = reduced_solve(P, lab, x, y);
+    bool rs_ok;
+    if constexpr (NV == 1) rs_ok = reduced_solve_x(P, lab, x, y);
+    else rs_ok = reduced_solve(P, lab, x, y);
     STAMP_ADD(NV == 1 ? ST_XRED : ST_ZRED, t_r);
     if (!rs_ok) return false;
-    if (kkt_check(P, lab, x, y, nl)) return true;
+    unsigned long long t_k = STAMP_T();
+    const bool kok = kkt_check(P, lab, x, y, nl);
+    STAMP_ADD(NV == 1 ? ST_XKKT : ST_ZKKT, t_k);
+    if (kok) return true;
     bool same = true;
 #pragma unroll
     for (int s = 0; s < NR; ++s) same &= (nl[s] == lab[s]);
@@ -1006,7 +1230,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       if (f != 1.0) {
         P.rho = fmin(fmax(P.rho * f, 1e-6), 1e6);
         build_K(P, kscr, kld);
-        if (lid() == 0) P.fstate[0] = -1;   // the scratch may have held the cached factor
+        if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
         wsync();
       }
     }
@@ -1275,7 +1499,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   double* Ke = Px + 2 * H * H;                           // 4*H*H     pair K_s^-1
   double* scr = Ke + 4 * H * H;                          // 64 x LD   pair scratch (wave 0)
   double* xfac_all = scr + 64 * LD;                      // NW x HMAX x (HMAX+1)
-  double* vec_all = xfac_all + NW * HMAX * (HMAX + 1);   // NW x 512
+  double* xt_all = xfac_all + NW * HMAX * (HMAX + 1);    // NW x (HMAX+1) x XLD
+  double* vec_all = xt_all + NW * (HMAX + 1) * XLD;      // NW x 512
   double* fdiag_all = vec_all + NW * 512;                // NW x 256
   CompLds S;
   S.pos = fdiag_all + NW * 256;
@@ -1336,6 +1561,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     qx.Pinv = Px + w * H * H;
     qx.vb = wm.vb;
     qx.fac = xfac;
+    qx.XT = xt_all + w * (HMAX + 1) * XLD;
     qx.fdiag = xdiag;
     qx.ib = xids;
     qx.fstate = xfs;

@@ -8,6 +8,7 @@ constexpr int WAVE = 64;
 constexpr int NW = 2;        // waves per workgroup = agents per component (max)
 constexpr int HMAX = 32;     // horizon limit of this version: lane k <-> time index k
 constexpr int LD = 65;       // odd LDS stride of the per-wave matrix scratch
+constexpr int XLD = HMAX + 1;  // odd LDS stride of the x-step parametric table X'
 constexpr int RUIZ_ITERS = 10;
 constexpr int PDAS_STEPS = 4;
 
@@ -65,6 +66,7 @@ inline size_t lds_bytes(int H) {
   d += 4 * (size_t)H * H;          // pair K_s^-1 (2H x 2H)
   d += 64 * LD;                    // pair matrix scratch (wave 0)
   d += NW * HMAX * (HMAX + 1);     // per-wave x-step scratch / Cholesky factor
+  d += NW * (HMAX + 1) * XLD;      // per-wave x-step parametric table X' | beta
   d += NW * 512;                   // per-wave vector buffers
   d += NW * 256;                   // per-wave factor diagonals (x, z)
   size_t H1 = H + 1;
