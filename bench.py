@@ -56,6 +56,21 @@ def algorithmic_bytes(cnt: dict, H: int) -> float:
     return 8.0 * (cnt["x_qps"] * x_doubles + cnt["z_qps"] * z_doubles)
 
 
+def latest_traffic(workload: str):
+    """HBM bytes per launch from the newest committed PMC summary (profiles/traffic_<tag>.json,
+    tags sort by round: r01 < r01b < r01c ...) for this workload, else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                tj = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if tj.get("workload") == workload:
+            return tj.get("hbm_bytes_per_launch")
+    return None
+
+
 def cpu_baseline(n_tiles: int, budget_s: float) -> dict:
     """Time the NumPy oracle (the reference's loop structure, one QP at a time) on a bounded sample."""
     sys.path.insert(0, ROOT)
@@ -149,16 +164,7 @@ def main():
     bytes_launch = algorithmic_bytes(cnt, H) / K
     achieved = bytes_launch / avg_launch_s / 1e9
 
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_r01.json")
-    if os.path.exists(tpath):
-        try:
-            with open(tpath) as f:
-                tj = json.load(f)
-            if tj.get("workload") == f"tiled{N_TILES}_H{H}_matlab_pi_fixed{MAX_OUTER}":
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    traffic = latest_traffic(f"tiled{N_TILES}_H{H}_matlab_pi_fixed{MAX_OUTER}")
 
     line = {
         "metric": "PI-ADMM outer iterations/sec (and ms/MPC step) at N_agents×H; 1/2/4/8 GPU",
