@@ -213,13 +213,9 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.status, (size_t)N + E);
   rc |= dalloc(h, &A.Pinv_x, (size_t)N * H * H);
   rc |= dalloc(h, &A.sc_x, (size_t)N * 4 * pd::HMAX);
-  rc |= dalloc(h, &A.ws_x, (size_t)N * 5 * pd::HMAX);
   rc |= dalloc(h, &A.lab_x, (size_t)N * 2 * pd::HMAX);
   rc |= dalloc(h, &A.tab_e, E * 8 * H * H);
-  rc |= dalloc(h, &A.sc_e, E * 8 * pd::HMAX);
-  rc |= dalloc(h, &A.ws_e, E * 12 * pd::HMAX);
-  rc |= dalloc(h, &A.lab_e, E * 5 * pd::HMAX);
-  rc |= dalloc(h, &A.gcoef_e, E * 4);
+  rc |= dalloc(h, &A.warm_ok, (size_t)N);
   rc |= dalloc(h, &A.counters, C * 8);
   rc |= dalloc(h, &A.rho_x, (size_t)N);
   rc |= dalloc(h, &A.rho_e, E);
@@ -259,6 +255,8 @@ int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
   HIPCHK(h, hipSetDevice(h->cfg.device));
   HIPCHK(h, hipMemcpyAsync(h->a.xt, xt, (size_t)h->N * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  // a new state breaks the receding-horizon sequence: no label warm start for the next step
+  HIPCHK(h, hipMemsetAsync(h->a.warm_ok, 0, (size_t)h->N * sizeof(int), h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PIADMM_OK;
 }

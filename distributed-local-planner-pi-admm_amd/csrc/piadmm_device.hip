@@ -302,12 +302,15 @@ struct QP {
                           // table block DevArgs::tab_e: P^-1 | PGt (+4H^2) | GPG (+6H^2)
   double* vb;             // per-wave LDS vectors (512 doubles)
   double* XT;             // x-step: per-wave LDS X' (H rows, stride XLD) and beta (row H)
+  double* G;              // x-step: per-wave LDS G = P^-1 - Y X (H x H, stride H), g = Y beta (row H)
   double* fac;            // LDS factor region: L (lower), S (upper), stride fld
   double* fdiag;          // LDS [2*64]: S_aa, 1/L_aa of the cached factor
   int* ib;                // per-wave LDS ints: [0,64) current W ids, [64,128) cached W ids
   int* fstate;            // LDS int: m of the cached factor (-1: none)
   int fld;                // stride of fac
   int mmax;               // capacity of fac (rows)
+  bool kready;            // K holds K_s^-1 for the current rho (the pair builds it lazily:
+                          // a QP that the warm-label polish certifies never needs it)
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
   // Row s of vehicle v = s / 2: even = box (lanes < H), odd = rate (lanes < H-1), 4 = hinge
@@ -659,7 +662,12 @@ __device__ __forceinline__ double chol_solve(const double* L, int ld, double lin
 
 // Left-looking Cholesky of S + delta I.  S is stored in the upper triangle of fac
 // (row a, columns b >= a) with its diagonal in sdiag (lane a); L goes to the strict
-// lower triangle and the diagonal.  Returns false if a pivot is not positive.
+// lower triangle and the diagonal.  A row whose pivot collapses below DEP_TOL * S_kk is
+// linearly dependent on the earlier working-set rows (degenerate vertices of the box/rate
+// polytope, e.g. u_k = -umax, u_{k+3} = +umax and the three rates between them at +dumax):
+// it is dropped (zero column of L, linv = 0, so its multiplier solves to 0), as the
+// oracle's active-set solver does.  Returns false only on a non-finite pivot.
+constexpr double DEP_TOL = 1e-10;
 __device__ __forceinline__ bool chol_factor(double* fac, int ld, double sdiag, double delta, int m, double& linv) {
   const int l = lid();
   for (int k = 0; k < m; ++k) {
@@ -675,9 +683,10 @@ __device__ __forceinline__ bool chol_factor(double* fac, int ld, double sdiag, d
     const double sik = (l == k) ? sdiag + delta : ((l > k && l < m) ? fac[k * ld + l] : 0.0);
     const double d = sik - acc;
     const double piv = rdl(d, k);
-    if (!(piv > 0.0) || !isfinite(piv)) return false;
-    const double lkk = sqrt(piv);
-    const double inv = 1.0 / lkk;
+    if (!isfinite(piv)) return false;
+    const bool dep = !(piv > DEP_TOL * rdl(sdiag, k));
+    const double lkk = dep ? 1.0 : sqrt(piv);
+    const double inv = dep ? 0.0 : 1.0 / lkk;
     wsync();
     if (l == k) {
       fac[k * ld + k] = lkk;
@@ -989,6 +998,50 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   }
   wsync();
   STAMP_ADD(ST_XR_SOLVE, t_x);
+  // G = P^-1 - Y X and g = Y beta (lane j = column j): Y is re-gathered column by column
+  // into the factor scratch (the factor is not needed once X' is known), then every lane
+  // accumulates its column of Y X from LDS broadcasts of Y and its own row of X'.
+  {
+    const int lc = (l < H) ? l : 0;
+    for (int a0 = 0; a0 < m; a0 += XB) {
+      double tv[XB][2], cf[XB][2];
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        const RowT r = row_terms(P, ids[min(a0 + u, m - 1)]);
+        cf[u][0] = r.c0;
+        cf[u][1] = r.c1;
+        tv[u][0] = P.Pinv[r.i0 * H + lc];
+        tv[u][1] = P.Pinv[r.i1 * H + lc];
+      }
+#pragma unroll
+      for (int u = 0; u < XB; ++u)
+        if (a0 + u < m && l < H) fac[(a0 + u) * ld + l] = cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1];
+    }
+    wsync();
+    const double* xj = XT + lc * XLD;
+    constexpr int GB = 8;
+    for (int i0 = 0; i0 < H; i0 += GB) {
+      double acc[GB], pv[GB];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        acc[u] = 0.0;
+        pv[u] = P.Pinv[min(i0 + u, H - 1) * H + lc];
+      }
+      for (int a = 0; a < m; ++a) {
+        const double xja = xj[a];
+        const double* ya = fac + a * ld + i0;
+#pragma unroll
+        for (int u = 0; u < GB; ++u) acc[u] += ya[u] * xja;     // rows past H are never stored
+      }
+#pragma unroll
+      for (int u = 0; u < GB; ++u)
+        if (l < H && i0 + u < H) P.G[(i0 + u) * H + l] = pv[u] - acc[u];
+    }
+    double gacc = 0.0;
+    for (int a = 0; a < m; ++a) gacc += fac[a * ld + lc] * XT[H * XLD + a];
+    if (l < H) P.G[H * H + l] = gacc;
+    wsync();
+  }
   return true;
 }
 
@@ -1035,58 +1088,32 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
     wsync();
   }
   unsigned long long t_rs = STAMP_T();
-  // fused pass: x0 = -P^-1 q (lane = variable), lam = -X q - beta (lane = W row)
-  double ap = 0.0, ax = 0.0;
+  // one fused pass: x = -G q + g (lane = variable), lam = -X q - beta (lane = W row)
+  double ag = 0.0, ax = 0.0;
   {
     const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
+    const double* G = P.G;
     for (int j0 = 0; j0 < H; j0 += GEMV_U) {
-      double qv[GEMV_U], pv[GEMV_U], xv[GEMV_U];
+      double qv[GEMV_U], gv[GEMV_U], xv[GEMV_U];
 #pragma unroll
       for (int u = 0; u < GEMV_U; ++u) {
         const int j = min(j0 + u, H - 1);
         qv[u] = (j0 + u < H) ? vb_q[j] : 0.0;
-        pv[u] = P.Pinv[j * H + lc];
+        gv[u] = G[j * H + lc];
         xv[u] = XT[j * XLD + la];
       }
 #pragma unroll
       for (int u = 0; u < GEMV_U; ++u) {
-        ap += pv[u] * qv[u];
+        ag += gv[u] * qv[u];
         ax += xv[u] * qv[u];
       }
     }
     if (l < m) vb_lam[l] = -ax - XT[H * XLD + l];
+    ag = G[H * H + lc] - ag;
   }
   wsync();
   STAMP_ADD(ST_RED_GEMV, t_rs);
-  unsigned long long t_x = STAMP_T();
-  // x = x0 - Y lam
-  double xv = -ap;
-  {
-    constexpr int XB = 4;
-    const int lc = (l < H) ? l : 0;
-    for (int a0 = 0; a0 < m; a0 += XB) {
-      int o[XB][2];
-      double cf[XB][2], la[XB];
-#pragma unroll
-      for (int u = 0; u < XB; ++u) {
-        const int a = min(a0 + u, m - 1);
-        const RowT r = row_terms(P, ids[a]);
-        la[u] = (a0 + u < m) ? vb_lam[a] : 0.0;
-        o[u][0] = r.i0 * H + lc; cf[u][0] = r.c0;
-        o[u][1] = r.i1 * H + lc; cf[u][1] = r.c1;
-      }
-      double tv[XB][2];
-#pragma unroll
-      for (int u = 0; u < XB; ++u) {
-        tv[u][0] = P.Pinv[o[u][0]];
-        tv[u][1] = P.Pinv[o[u][1]];
-      }
-#pragma unroll
-      for (int u = 0; u < XB; ++u) xv -= (cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1]) * la[u];
-    }
-  }
-  STAMP_ADD(ST_RED_X, t_x);
-  x[0] = (l < H) ? xv : 0.0;
+  x[0] = (l < H) ? ag : 0.0;
 #pragma unroll
   for (int s = 0; s < 2; ++s) y[s] = inW[s] ? vb_lam[pos[s]] : 0.0;
   wsync();
@@ -1220,6 +1247,12 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
   signed char plab[NR];
 #pragma unroll
   for (int s = 0; s < NR; ++s) plab[s] = -1;
+  if (!ok && !P.kready) {
+    build_K(P, kscr, kld);
+    P.kready = true;
+    if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
+    wsync();
+  }
   for (int it = 1; !ok && it <= max_inner; ++it) {
     unsigned long long t_a = STAMP_T();
     admm_iter(P, xs, zs, ys);
@@ -1353,12 +1386,12 @@ __device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, doubl
   P.sigma = c.admm_sigma;
   P.alpha = c.admm_alpha;
   P.tol = c.qp_tol;
+  P.kready = true;      // setup_agent loads or builds K_s^-1
 }
 
 // x-step QP of agent a (cost_function_primal, PI_ADMM_class.py:114-135, constraints :172-192):
 // scaling, K_s^-1 (LDS) and P^-1 (LDS) for the whole MPC step.
-__device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, const Geo& g, double* xfac,
-                                            double* Px_lds) {
+__device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, const Geo& g, double* xfac) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, l = lid();
   const bool in = l < H;
@@ -1375,10 +1408,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
     P.E[0] = in ? sc[HMAX + li] : 0.0;
     P.E[1] = (l < H - 1) ? sc[2 * HMAX + li] : 0.0;
     for (int i = 0; i < H; ++i) {
-      if (in) {
-        P.K[i * H + l] = Kc[i * H + l];
-        Px_lds[i * H + l] = Pc[i * H + l];
-      }
+      if (in) P.K[i * H + l] = Kc[i * H + l];
     }
     wsync();
     return;
@@ -1391,9 +1421,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
   gj_invert(xfac, H, HMAX + 1);
   for (int i = 0; i < H; ++i) {
     if (in) {
-      const double v = xfac[i * (HMAX + 1) + l];
-      Px_lds[i * H + l] = v;
-      Pc[i * H + l] = v;
+      Pc[i * H + l] = xfac[i * (HMAX + 1) + l];
       Kc[i * H + l] = P.K[i * H + l];
     }
   }
@@ -1403,6 +1431,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
     sc[2 * HMAX + l] = P.E[1];
   }
   if (l == 0) A.xcache_rho[a] = P.rho;
+  __threadfence();      // P^-1 (read back through L2 by the polish) is visible to this wave
   wsync();
 }
 
@@ -1475,7 +1504,7 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
   unsigned long long t_r = STAMP_T();
   ruiz(P);
   STAMP_ADD(ST_SZ_RUIZ, t_r);
-  build_K(P, scr, LD);
+  P.kready = false;     // K_s^-1 is built by qp_solve when ADMM is first needed
 }
 // ============================================================ the MPC-step kernel
 struct CompLds {
@@ -1495,8 +1524,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
 
   // ---- LDS carve (lds_bytes() in piadmm_internal.h)
   double* Kx = lds;                                      // 2 x H*H   agent K_s^-1
-  double* Px = Kx + 2 * H * H;                           // 2 x H*H   agent P^-1
-  double* Ke = Px + 2 * H * H;                           // 4*H*H     pair K_s^-1
+  double* Gx = Kx + 2 * H * H;                           // 2 x (H*H+H) agent polish G | g
+  double* Ke = Gx + 2 * (H * H + H);                     // 4*H*H     pair K_s^-1
   double* scr = Ke + 4 * H * H;                          // 64 x LD   pair scratch (wave 0)
   double* xfac_all = scr + 64 * LD;                      // NW x HMAX x (HMAX+1)
   double* xt_all = xfac_all + NW * HMAX * (HMAX + 1);    // NW x (HMAX+1) x XLD
@@ -1558,7 +1587,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     affine_c(gx, c.dt, H, cx_own, cy_own);
     qp_common(c, H, A.rho_x[a], qx);
     qx.K = Kx + w * H * H;
-    qx.Pinv = Px + w * H * H;
+    qx.Pinv = A.Pinv_x + (size_t)a * H * H;    // L2-resident; read only when W changes
+    qx.G = Gx + w * (H * H + H);
     qx.vb = wm.vb;
     qx.fac = xfac;
     qx.XT = xt_all + w * (HMAX + 1) * XLD;
@@ -1568,7 +1598,21 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     qx.fld = HMAX + 1;
     qx.mmax = HMAX;
     nnb = A.nbr_cnt[a];
-    setup_agent(A, a, qx, gx, xfac, Px + w * H * H);
+    setup_agent(A, a, qx, gx, xfac);
+    // receding-horizon warm start: the previous step's final labels shifted by one time
+    // slot (lane k now holds time t+k = lane k+1 of step t-1); only a guess for the polish,
+    // the certified minimiser does not depend on it
+#ifndef PIADMM_NO_XWARM
+    if (A.warm_ok[a]) {
+#else
+    if (false) {
+#endif
+      const signed char* lb = A.lab_x + (size_t)a * 2 * HMAX;
+      const int src = min(l + 1, H - 1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) lab_x[s] = (l < H) ? lb[s * HMAX + src] : 0;
+      warm_x = true;
+    }
     STAMP_ADD(ST_SETUP_X, t0);
   }
   QP<2> qe;
@@ -1605,6 +1649,9 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     qe.fld = LD;
     qe.mmax = WAVE;
     setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke);
+    // (no receding-horizon label guess for the pair: tools/pair_exp.py found the polish from
+    // shifted labels failing on half of the bench's pair QPs, each failure costing PDAS_STEPS
+    // reduced solves before the ADMM fallback)
     STAMP_ADD(ST_SETUP_Z, t0);
   }
   __syncthreads();
@@ -1833,6 +1880,12 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     if (l == 0) {
       A.status[a] = status_x;
       A.rho_x[a] = qx.rho;
+      A.warm_ok[a] = 1;
+    }
+    if (l < HMAX) {
+      signed char* lb = A.lab_x + (size_t)a * 2 * HMAX;
+      lb[l] = lab_x[0];
+      lb[HMAX + l] = lab_x[1];
     }
     if (A.xcache_rho[a] != qx.rho) {       // adaptive rho rebuilt K_s^-1 in LDS: refresh the cache
       double* Kc = A.Kx_cache + (size_t)a * H * H;

@@ -40,15 +40,11 @@ struct DevArgs {
   // per-step solver workspace
   double* Pinv_x;           // N*H*H
   double* sc_x;             // N*4*HMAX   (D, Ebox, Erate, spare)
-  double* ws_x;             // N*5*HMAX   warm ADMM state (xs, zs0, zs1, ys0, ys1)
-  signed char* lab_x;       // N*2*HMAX
+  signed char* lab_x;       // N*2*HMAX   final x-step labels of the last step (next step's warm guess)
   double* tab_e;            // E * 8H^2 polish tables per edge, one block each:
                             //   [0, 4H^2) P^-1 (2H x 2H, block-diagonal), [4H^2, 6H^2) PGt (H x 2H,
                             //   row k = P_v^-1 T(k+1,.)'), [6H^2, 8H^2) GPG (Z_v = T P_v^-1 T')
-  double* sc_e;             // E*8*HMAX   (D1, D2, Eb1, Er1, Eb2, Er2, Eh, h0)
-  double* ws_e;             // E*12*HMAX  (xs0, xs1, zs0..4, ys0..4)
-  signed char* lab_e;       // E*5*HMAX
-  double* gcoef_e;          // E*4        (g1, g2, spare)
+  int* warm_ok;             // N          1: lab_x holds the labels of the previous MPC step
   unsigned long long* counters;  // C*8  accumulated work counters (see piadmm_get_counters)
   unsigned long long* stamps;    // C*32 phase cycle sums (diagnostic build -DPIADMM_STAMPS only)
   double* rho_x;            // N   ADMM penalty per agent QP (adapted, persists across steps)
@@ -62,7 +58,7 @@ struct DevArgs {
 inline size_t lds_bytes(int H) {
   size_t d = 0;
   d += 2 * (size_t)H * H;          // agent K_s^-1 (2 agents)
-  d += 2 * (size_t)H * H;          // agent P^-1 (2 agents)
+  d += 2 * ((size_t)H * H + H);    // agent polish G | g (2 agents)
   d += 4 * (size_t)H * H;          // pair K_s^-1 (2H x 2H)
   d += 64 * LD;                    // pair matrix scratch (wave 0)
   d += NW * HMAX * (HMAX + 1);     // per-wave x-step scratch / Cholesky factor

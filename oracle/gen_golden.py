@@ -116,10 +116,44 @@ def run_fixture(name):
                 preset=np.array(preset), cfg_kw=np.array(repr(kw)))
 
 
+# Bench tiles (scenario.tiled(128, 30, seed=0): tile k is seeded with k) whose MPC step t
+# reaches degenerate x-step QPs: a dependent working set (u_k = -umax, u_{k+3} = +umax and
+# the three rates between them at +dumax) with a zero multiplier.
+DEGENERATE = ((79, 15), (108, 15), (88, 18))
+DEG_OUTER = 8
+
+
+def gen_degenerate():
+    """Oracle state of the DEGENERATE tiles at step t (12-19 s of oracle time each)."""
+    H = 30
+    cfg_run = config.matlab_pi(H=H, fixed_iters=1, max_outer=100)
+    cfg_chk = config.matlab_pi(H=H, fixed_iters=1, max_outer=DEG_OUTER)
+    rec = {k: [] for k in ("tile", "t", "xt_t", "xt_next", "u", "spd", "ref", "xt0")}
+    for tile, t in DEGENERATE:
+        scn = scenario.tiled(1, H, n_steps=22, perturb=True, seed=tile)
+        orc = O.Oracle(cfg_run, scn)
+        for _ in range(t):
+            orc.mpc_step()
+        xt_t = orc.xt.copy()
+        chk = O.Oracle(cfg_chk, scn)
+        chk.xt, chk.t = xt_t.copy(), t
+        r = chk.mpc_step()
+        for k, v in (("tile", tile), ("t", t), ("xt_t", xt_t), ("xt_next", r.xt), ("u", r.u),
+                     ("spd", scn.spd), ("ref", scn.ref), ("xt0", scn.xt0)):
+            rec[k].append(v)
+        print("degenerate", tile, t)
+    np.savez_compressed(os.path.join(GOLD, "degenerate_xstep.npz"), outer=DEG_OUTER,
+                        **{k: np.asarray(v) for k, v in rec.items()})
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
+    if sys.argv[1:] == ["degenerate"]:
+        gen_degenerate()
+        return
     gen_qp_xstep()
     gen_qp_pair()
+    gen_degenerate()
     for name in RUNS:
         np.savez_compressed(os.path.join(GOLD, f"run_{name}.npz"), **run_fixture(name))
         print("wrote", name)

@@ -123,6 +123,26 @@ def test_bench_workload_sampled_tiles_match_oracle(Solver):
                 close(rg.u[sl], ro.u[sl])
 
 
+def test_degenerate_xstep_working_sets(Solver):
+    """Bench tiles whose x-step QPs have a linearly dependent optimal working set (two box
+    rows and the three rate rows between them, one zero multiplier): the polish drops the
+    dependent row and certifies the vertex (a singular Schur complement used to leave these
+    QPs uncertified after max_inner ADMM iterations).  Oracle state from oracle/gen_golden.py."""
+    d = np.load(os.path.join(GOLD, "degenerate_xstep.npz"), allow_pickle=False)
+    cfg = config.matlab_pi(H=30, fixed_iters=1, max_outer=int(d["outer"]))
+    for k in range(len(d["tile"])):
+        scn = scenario.Scenario(spd=d["spd"][k], xt0=d["xt0"][k], ref=d["ref"][k],
+                                edges=np.array([[0, 1]], np.int32), n_steps=22)
+        with Solver(cfg, scn) as s:
+            s.set_xt(d["xt_t"][k])
+            s.reset_counters()
+            r = s.mpc_step(t=int(d["t"][k]))
+            np.testing.assert_array_equal(r.status, 0)
+            assert s.counters()["inexact"] == 0
+            close(r.xt, d["xt_next"][k])
+            close(r.u, d["u"][k])
+
+
 def test_tiles_are_independent_at_1024_agents(Solver):
     """1024 agents x H30 (configs[3] size): identical tiles give bit-identical results,
     equal to the 2-vehicle run; every QP of the step is certified (status 0)."""
