@@ -10,11 +10,19 @@ never returns to the host inside it.
 
   python bench.py [--gpus N --steps K --warmup W]
 
+The job runs with the reference's global termination scope (term_global, quirk B9):
+all agents of all ranks form one ADMM job whose residual history (rk, sk summed over
+every pair) is the reference's.  With fixed iterations that is one fused launch per
+MPC step plus one RCCL all-reduce of the 2 x 100 residual partials over xGMI.
+
 N>1: launched by torch.distributed.run, one process per GPU; each rank owns its
 own 128 intersection tiles (256 agents), so per-GPU work is fixed ("weak").
-The components never straddle ranks, so the data path has no collective
-(multi-GPU); torch.distributed (gloo) is only the harness's barrier
-and max-over-ranks timer.
+Components never straddle ranks; the ranks join one RCCL communicator (the unique
+id travels over torch.distributed's gloo group, which is otherwise only the
+harness's barrier and max-over-ranks timer).
+
+--natural: natural termination instead (one launch + one RCCL all-reduce of the
+termination partials per outer iteration, host decision), reported as its own line.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 """
@@ -114,6 +122,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle timing (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--natural", action="store_true", help="natural (global) termination, not the headline")
     args = ap.parse_args()
 
     lib = _lib.load()                       # HIP runtime loaded before torch (same SONAME)
@@ -129,9 +138,17 @@ def main():
     from piadmm.solver import PI_ADMM_MI355X
     K, W = args.steps, args.warmup
     n_steps = max(K, W, 1)
-    cfg = config.matlab_pi(H=H, fixed_iters=1, max_outer=MAX_OUTER)
+    cfg = config.matlab_pi(H=H, fixed_iters=0 if args.natural else 1, max_outer=MAX_OUTER, term_global=1)
     scn = scenario.tiled(N_TILES, H, n_steps=n_steps, perturb=True, seed=1000 * rank)
     solver = PI_ADMM_MI355X(cfg, scn, device=local_rank)
+    if dist is not None:
+        from piadmm import dist as pdist
+
+        def bcast(b):
+            obj = [b]
+            dist.broadcast_object_list(obj, src=0)
+            return obj[0]
+        pdist.attach_rccl(solver, rank, world, bcast)
 
     # warmup: W steps from t=0, then reset the state so the timed steps repeat t=0..K-1
     if W > 0:
@@ -158,7 +175,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, ev_ms = float(tt[0]), float(tt[1])
 
-    outer_total = world * K * MAX_OUTER
+    outer_total = world * cnt["outer_iters"] / max(solver.C, 1)      # job iterations x ranks
     value = outer_total / wall
     avg_launch_s = (ev_ms / 1e3) / K
     bytes_launch = algorithmic_bytes(cnt, H) / K
@@ -181,9 +198,13 @@ def main():
         "data": "synthetic: 128 seeded tiles of the reference 2-vehicle intersection per GPU",
         "config": {
             "workload": f"256 agents x H{H} per GPU (128 tiles), matlab_pi preset (PI anti-windup), "
-                        f"{MAX_OUTER} outer iterations per MPC step, termination off",
-            "agents_per_gpu": 2 * N_TILES, "horizon": H, "outer_iters_per_step": MAX_OUTER,
-            "parallelism": f"components sharded over {world} GPU(s), no data-path collective",
+                        + (f"global natural termination (max {MAX_OUTER} outer iterations)" if args.natural else
+                           f"{MAX_OUTER} outer iterations per MPC step (fixed), global residual history"),
+            "agents_per_gpu": 2 * N_TILES, "horizon": H,
+            "outer_iters_per_step": outer_total / world / K,
+            "parallelism": f"components sharded over {world} GPU(s); " + (
+                "one RCCL all-reduce of the termination partials per outer iteration" if args.natural else
+                "one RCCL all-reduce of the residual history per MPC step") + (" (single rank: none)" if world == 1 else ""),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -4,6 +4,7 @@
 // Replaces the reference's per-call CasADi/OSQP instantiation
 // (casadi/main.py:96,146) and its Python loop state (casadi/main.py:52-72).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -24,6 +25,13 @@ struct piadmm_ctx {
   std::vector<void*> allocs;
   pd::DevArgs a{};
   std::string err;
+  // term_global: RCCL communicator (null = single rank), device partials, pinned host copy
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  double* d_part = nullptr;      // max_outer x 5 partials, or max_outer x 2 residual history
+  double* h_part = nullptr;      // pinned
+  std::vector<double> ghist;     // global (rk, sk) history of the last step
+  int giters = 0;
 };
 
 namespace {
@@ -59,6 +67,7 @@ int dalloc(piadmm_ctx* h, T** p, size_t n) {
 void free_all(piadmm_ctx* h) {
   for (void* p : h->allocs) (void)hipFree(p);
   h->allocs.clear();
+  h->d_part = nullptr;
   h->have_scn = false;
 }
 
@@ -72,6 +81,7 @@ int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
     return fail(h, PIADMM_E_ARG, "dt, L, rho, Pcost must be > 0; Pnorm, beta >= 0");
   if (c.max_inner <= 0 || c.polish_every <= 0) return fail(h, PIADMM_E_ARG, "max_inner, polish_every must be > 0");
   if (c.round_decimals > 12) return fail(h, PIADMM_E_ARG, "round_decimals must be <= 12");
+  if (c.tighten && !(c.tight_p > 0 && c.tight_p < 1)) return fail(h, PIADMM_E_ARG, "tight_p must be in (0, 1)");
   return 0;
 }
 
@@ -119,6 +129,7 @@ int32_t piadmm_create(const piadmm_config_t* cfg, piadmm_handle_t* out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&h->ev0);
   if (e == hipSuccess) e = hipEventCreate(&h->ev1);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_part, (size_t)std::max(cfg->max_outer, 1) * 5 * sizeof(double));
   if (e != hipSuccess) {
     g_err = std::string("HIP init: ") + hipGetErrorString(e);
     delete h;
@@ -133,6 +144,8 @@ int32_t piadmm_destroy(piadmm_handle_t h) {
   (void)hipSetDevice(h->cfg.device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_all(h);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->h_part) (void)hipHostFree(h->h_part);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -216,6 +229,17 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.lab_x, (size_t)N * 2 * pd::HMAX);
   rc |= dalloc(h, &A.tab_e, E * 8 * H * H);
   rc |= dalloc(h, &A.warm_ok, (size_t)N);
+  rc |= dalloc(h, &A.Sacc, E * 4 * H1);
+  rc |= dalloc(h, &A.Dacc, E * 4 * H1);
+  rc |= dalloc(h, &A.last, E * 4 * H1);
+  rc |= dalloc(h, &A.dischk, E);
+  rc |= dalloc(h, &A.deff, E);
+  rc |= dalloc(h, &A.qs_x, (size_t)N * 5 * pd::WAVE);
+  rc |= dalloc(h, &A.ql_x, (size_t)N * 2 * pd::WAVE);
+  rc |= dalloc(h, &A.qs_e, E * 12 * pd::WAVE);
+  rc |= dalloc(h, &A.ql_e, E * 5 * pd::WAVE);
+  rc |= dalloc(h, &A.cst, C * 4);
+  rc |= dalloc(h, &h->d_part, (size_t)h->cfg.max_outer * 5);
   rc |= dalloc(h, &A.counters, C * 8);
   rc |= dalloc(h, &A.rho_x, (size_t)N);
   rc |= dalloc(h, &A.rho_e, E);
@@ -261,6 +285,71 @@ int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
   return PIADMM_OK;
 }
 
+#define LAUNCH(h, expr)                                                                       \
+  do {                                                                                        \
+    if ((expr) != 0)                                                                          \
+      return fail((h), PIADMM_E_HIP, std::string("kernel launch: ") + hipGetErrorString(hipGetLastError())); \
+  } while (0)
+#define NCCLCHK(h, expr)                                                                      \
+  do {                                                                                        \
+    ncclResult_t _r = (expr);                                                                 \
+    if (_r != ncclSuccess) return fail((h), PIADMM_E_HIP, std::string(#expr ": ") + ncclGetErrorString(_r)); \
+  } while (0)
+
+// One MPC step.  Per-component termination (and any fixed-iteration step): one fused launch,
+// plus, under term_global, the component-summed residual history all-reduced once.  Global
+// termination with the stopping test on: one launch per outer iteration, the rank's partials
+// all-reduced over RCCL and read back, the stop decided on the host exactly as
+// casadi/main.py:115-118,174-178 (MATLAB :191-210) do over all agents, then a final launch
+// for outputs and propagation.
+static int32_t run_step(piadmm_handle_t h, int32_t t, bool sync_outputs) {
+  const piadmm_config_t& c = h->cfg;
+  hipStream_t s = h->stream;
+  const int M = c.max_outer;
+  if (!c.term_global) {
+    LAUNCH(h, pd::launch_mpc_step(h->a, t, 0, M, pd::F_FIRST | pd::F_LAST, s));
+    return PIADMM_OK;
+  }
+  if (c.fixed_iters) {
+    LAUNCH(h, pd::launch_mpc_step(h->a, t, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL, s));
+    LAUNCH(h, pd::launch_resid_history(h->a, h->d_part, s));
+    if (h->comm) NCCLCHK(h, ncclAllReduce(h->d_part, h->d_part, (size_t)2 * M, ncclDouble, ncclSum, h->comm, s));
+    h->giters = M;
+    if (sync_outputs) {
+      HIPCHK(h, hipMemcpyAsync(h->h_part, h->d_part, (size_t)2 * M * sizeof(double), hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      h->ghist.assign(h->h_part, h->h_part + 2 * M);
+    }
+    return PIADMM_OK;
+  }
+  LAUNCH(h, pd::launch_pair_deff(h->a, s));
+  h->ghist.assign((size_t)2 * M, NAN);
+  int flag = 0, n = 0, nanlast = 0;
+  for (int it = 0; it < M; ++it) {
+    LAUNCH(h, pd::launch_mpc_step(h->a, t, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
+    double* part = h->d_part + (size_t)5 * it;
+    LAUNCH(h, pd::launch_term_partials(h->a, it, part, s));
+    if (h->comm) NCCLCHK(h, ncclAllReduce(part, part, 5, ncclDouble, ncclSum, h->comm, s));
+    HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
+    const double n_seen = h->h_part[3], n_bad = h->h_part[4];
+    n = it + 1;
+    if (n_act == 0.0 && flag == 0) {      // no pair collides anywhere: stop (casadi/main.py:115-116)
+      nanlast = 1;
+      break;
+    }
+    flag = 1;
+    h->ghist[2 * it + 0] = rk;
+    h->ghist[2 * it + 1] = sk;
+    const bool dist_ok = n_seen > 0.0 && n_bad == 0.0;
+    if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok)) break;
+  }
+  h->giters = n;
+  LAUNCH(h, pd::launch_mpc_step(h->a, t, n, n, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
+  return PIADMM_OK;
+}
+
 static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
@@ -268,8 +357,7 @@ static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
     return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
   HIPCHK(h, hipSetDevice(h->cfg.device));
   for (int i = 0; i < n; ++i)
-    if (pd::launch_mpc_step(h->a, t0 + i, h->stream) != 0)
-      return fail(h, PIADMM_E_HIP, std::string("kernel launch: ") + hipGetErrorString(hipGetLastError()));
+    if (int rc = run_step(h, t0 + i, i == n - 1)) return rc;
   return PIADMM_OK;
 }
 
@@ -349,6 +437,40 @@ int32_t piadmm_get_component_counters(piadmm_handle_t h, uint64_t* out, int32_t 
   HIPCHK(h, hipSetDevice(h->cfg.device));
   HIPCHK(h, hipMemcpyAsync(out, h->a.counters, (size_t)h->C * 8 * 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PIADMM_OK;
+}
+
+int32_t piadmm_comm_unique_id(uint8_t* id_out) {
+  if (!id_out) return fail(nullptr, PIADMM_E_ARG, "null argument");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(nullptr, PIADMM_E_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return PIADMM_OK;
+}
+
+int32_t piadmm_comm_init(piadmm_handle_t h, const uint8_t* id_in, int32_t nranks, int32_t rank) {
+  if (!h || !id_in) return fail(h, PIADMM_E_ARG, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(h, PIADMM_E_ARG, "bad rank / nranks");
+  if (h->comm) return fail(h, PIADMM_E_STATE, "communicator already initialised");
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  ncclUniqueId id;
+  std::memcpy(id.internal, id_in, NCCL_UNIQUE_ID_BYTES);
+  NCCLCHK(h, ncclCommInitRank(&h->comm, nranks, id, rank));
+  h->nranks = nranks;
+  h->rank = rank;
+  return PIADMM_OK;
+}
+
+int32_t piadmm_global_resid(piadmm_handle_t h, double* resid_out, int32_t* iters_out) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!h->cfg.term_global) return fail(h, PIADMM_E_STATE, "term_global is off: residuals are per component");
+  const int M = h->cfg.max_outer;
+  if (resid_out) {
+    for (int i = 0; i < 2 * M; ++i) resid_out[i] = NAN;
+    for (int i = 0; i < 2 * h->giters && i < (int)h->ghist.size(); ++i) resid_out[i] = h->ghist[i];
+  }
+  if (iters_out) *iters_out = h->giters;
   return PIADMM_OK;
 }
 

@@ -1442,7 +1442,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
 // PGt = P^-1 G' (HBM), GPG = G P^-1 G' (HBM) and K_s^-1 (LDS).
 __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, const Geo& g1, const Geo& g2,
                                            double c1x, double c1y, double c2x, double c2y, const double* seeds,
-                                           double* scr, double* Ke_lds) {
+                                           double* scr, double* Ke_lds, double deff) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, n = 2 * H, l = lid();
   const bool in = l < H;
@@ -1451,7 +1451,7 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
   const double dd = dbx * dbx + dby * dby;
   P.g1 = -2.0 * (dbx * g1.ax + dby * g1.ay);
   P.g2 = 2.0 * (dbx * g2.ax + dby * g2.ay);
-  const double Dsq = c.dis_thres * c.dis_thres;
+  const double Dsq = deff * deff;
   const double h_time = Dsq + dd - 2.0 * (dbx * (c2x - c1x) + dby * (c2y - c1y));
   P.h0 = shdn(h_time, 1);                    // hinge lane k <-> time k+1
   if (!P.valid(4)) P.h0 = 0.0;
@@ -1511,7 +1511,25 @@ struct CompLds {
   double *pos, *xt, *seed, *u, *hat, *lam, *S, *D, *last, *sc;
 };
 
-__global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
+// Delay offset |delta| of compute_square_halfspaces_ca_prob (decentralized/util.py:81-96) for
+// an agent with heading th and speed s (oracle delay_offset).
+__device__ __forceinline__ double delay_norm(const piadmm_config_t& c, double th, double s) {
+#pragma clang fp contract(off)
+  const double cs = cos(th), sn = sin(th);
+  const double dxa = c.avg_delay * s * cs, dya = c.avg_delay * s * sn;
+  const double dxv = (c.var_delay * s * cs) * (c.var_delay * s * cs);
+  const double dyv = (c.var_delay * s * sn) * (c.var_delay * s * sn);
+  const double kap = sqrt(c.tight_p / (1.0 - c.tight_p));
+  return hypot(dxa + kap * dxv, dya + kap * dyv);
+}
+
+// One launch runs outer iterations [it0, it1) of MPC step t for every component (one
+// workgroup each).  The fused mode is one launch (0, max_outer, FIRST | LAST); the global
+// termination mode (term_global, reference quirk B9) runs one launch per outer iteration,
+// with the per-step state carried in HBM between launches (restore / save below) and the
+// stop decision taken by the host from all-reduced partials, then a LAST launch with no
+// iterations for the outputs and the propagation.
+__global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it0, int it1, int flags) {
   extern __shared__ double lds[];
   __shared__ int s_int[NW * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
   const piadmm_config_t& c = A.cfg;
@@ -1555,6 +1573,9 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     zfs[0] = -1;
   }
 
+  const bool first = (flags & F_FIRST) != 0;
+  const bool last_launch = (flags & F_LAST) != 0;
+  const bool global = (flags & F_GLOBAL) != 0;
   // ---- seeds (casadi/main.py:48-49) and zero per-step state (:52-63)
   if ((int)threadIdx.x < na) {
     const int a = a0 + threadIdx.x;
@@ -1565,10 +1586,38 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     S.seed[2 * threadIdx.x + 0] = around(x + c.dt * s * cos(th), c.round_decimals);
     S.seed[2 * threadIdx.x + 1] = around(y + c.dt * s * sin(th), c.round_decimals);
   }
-  for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) S.pos[i] = 0.0;
-  for (int i = threadIdx.x; i < 20 * H1; i += blockDim.x) S.hat[i] = 0.0;   // hat, lam, S, D, last
   for (int i = threadIdx.x; i < 32; i += blockDim.x) S.sc[i] = 0.0;
+  {
+    double* const edge_lds[5] = {S.hat, S.lam, S.S, S.D, S.last};
+    double* const edge_hbm[5] = {A.hat, A.lam, A.Sacc, A.Dacc, A.last};
+    if (first) {
+      for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) S.pos[i] = 0.0;
+      // casadi/main.py:52-63 resets hat, lam (and the PI accumulators) every MPC step; with
+      // warm_duals they continue from the previous step shifted by one slot (a12)
+      for (int k = 0; k < 5; ++k)
+        for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) {
+          double v = 0.0;
+          if (e >= 0 && c.warm_duals) {
+            const int r = i / H1, tt = i - r * H1;
+            v = edge_hbm[k][(size_t)e * 4 * H1 + r * H1 + min(tt + 1, H)];
+          }
+          edge_lds[k][i] = v;
+        }
+    } else {
+      // state of the previous launch of this step
+      for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
+        S.pos[i] = (i < na * 2 * H1) ? A.pos_old[(size_t)a0 * 2 * H1 + i] : 0.0;
+      for (int i = threadIdx.x; i < na * H; i += blockDim.x) S.u[i] = A.u[(size_t)a0 * H + i];
+      for (int k = 0; k < 5; ++k)
+        for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
+          edge_lds[k][i] = (e >= 0) ? edge_hbm[k][(size_t)e * 4 * H1 + i] : 0.0;
+    }
+  }
   __syncthreads();
+  // pair safety distance (a13 tightening from the step's start states, else dis_thres)
+  double deff = c.dis_thres;
+  if (e >= 0 && c.tighten && na == 2)
+    deff = c.dis_thres + delay_norm(c, S.xt[2], A.spd[a0]) + delay_norm(c, S.xt[5], A.spd[a0 + 1]);
   unsigned long long t_k = STAMP_T();
 
   // ---- per-step QP setup (registers of the owning wave stay live for the whole step)
@@ -1602,11 +1651,19 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     // receding-horizon warm start: the previous step's final labels shifted by one time
     // slot (lane k now holds time t+k = lane k+1 of step t-1); only a guess for the polish,
     // the certified minimiser does not depend on it
-#ifndef PIADMM_NO_XWARM
-    if (A.warm_ok[a]) {
-#else
-    if (false) {
-#endif
+    if (!first) {
+      const double* qs = A.qs_x + (size_t)a * 5 * WAVE;
+      const signed char* ql = A.ql_x + (size_t)a * 2 * WAVE;
+      xs_x[0] = qs[l];
+      zs_x[0] = qs[WAVE + l];
+      zs_x[1] = qs[2 * WAVE + l];
+      ys_x[0] = qs[3 * WAVE + l];
+      ys_x[1] = qs[4 * WAVE + l];
+      lab_x[0] = ql[l];
+      lab_x[1] = ql[WAVE + l];
+      warm_x = (A.cst[(size_t)ci * 4 + 2] >> w) & 1;
+      status_x = A.status[a];
+    } else if (A.warm_ok[a]) {
       const signed char* lb = A.lab_x + (size_t)a * 2 * HMAX;
       const int src = min(l + 1, H - 1);
 #pragma unroll
@@ -1648,7 +1705,21 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     qe.fstate = zfs;
     qe.fld = LD;
     qe.mmax = WAVE;
-    setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke);
+    setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke, deff);
+    if (!first) {
+      const double* qs = A.qs_e + (size_t)e * 12 * WAVE;
+      const signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
+      xs_e[0] = qs[l];
+      xs_e[1] = qs[WAVE + l];
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        zs_e[s] = qs[(2 + s) * WAVE + l];
+        ys_e[s] = qs[(7 + s) * WAVE + l];
+        lab_e[s] = ql[s * WAVE + l];
+      }
+      warm_e = (A.cst[(size_t)ci * 4 + 2] >> 2) & 1;
+      status_e = A.status[A.N + e];
+    }
     // (no receding-horizon label guess for the pair: tools/pair_exp.py found the polish from
     // shifted labels failing on half of the bench's pair QPs, each failure costing PDAS_STEPS
     // reduced solves before the ADMM fallback)
@@ -1657,13 +1728,16 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
   __syncthreads();
 
   const bool nonlin_pos = c.pos_model != 0;
-  const double thr = c.collide_sq_thres ? c.dis_thres * c.dis_thres : c.dis_thres;
-  int flag = 0, aliased = 0, iters = 0;
+  const double thr = c.collide_sq_thres ? deff * deff : deff;
+  int flag = first ? 0 : A.cst[(size_t)ci * 4 + 0];
+  int aliased = first ? 0 : A.cst[(size_t)ci * 4 + 1];
+  int iters = it0;
   int n_xqp = 0, n_zqp = 0, n_admm_x = 0, n_admm_z = 0, n_pdas_x = 0, n_pdas_z = 0, n_inexact = 0;
-  bool act = false;
-  double dis_chk = NAN;
+  bool act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
+  double dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
   double* resid = A.resid + (size_t)ci * c.max_outer * 2;
-  for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
+  if (first)
+    for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
   // reference positions of the own agent at time lanes (fixed for the step)
   double rx_own = 0.0, ry_own = 0.0;
   if (w < na && l <= H) {
@@ -1672,7 +1746,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     ry_own = rp[A.T + t + l];
   }
 
-  for (int it = 0; it < c.max_outer; ++it) {
+  for (int it = it0; it < it1; ++it) {
     iters = it + 1;
     // -------- x-step: every agent of the component (casadi/main.py:81-106)
     if (w < na) {
@@ -1722,7 +1796,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
       }
       act = wany(hit);
     }
-    if (!act && flag == 0 && !c.fixed_iters) break;   // no edge ever: stop (:115-116)
+    if (!act && flag == 0 && !c.fixed_iters && !global) break;   // no edge ever: stop (:115-116)
     flag = 1;
     // -------- z-step + dual update on the colliding pair (casadi/main.py:121-162)
     if (act && w == 0) {
@@ -1826,8 +1900,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
       resid[2 * it + 0] = rk;
       resid[2 * it + 1] = sk;
     }
-    if (!c.fixed_iters && rk <= c.eps_pri && sk <= c.eps_dual &&
-        (!c.term_dist_check || dis_chk > c.dis_thres))
+    if (!c.fixed_iters && !global && rk <= c.eps_pri && sk <= c.eps_dual &&
+        (!c.term_dist_check || dis_chk > deff))
       break;
     if (c.alias_dual_residual) {
       aliased = 1;
@@ -1849,7 +1923,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned long long* cn = A.counters + (size_t)ci * 8;
-      cn[0] += (unsigned long long)iters;
+      cn[0] += (unsigned long long)(iters - it0);
       for (int k = 0; k < 6; ++k) {
         unsigned long long sum = 0;
         for (int ww = 0; ww < NW; ++ww) sum += (unsigned long long)s_cnt[ww][k];
@@ -1860,50 +1934,160 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t) {
       cn[7] += inex;
     }
   }
-  // ---- outputs and propagation (casadi/main.py:185-192)
+  // ---- state of this launch (every launch) and outputs / propagation (LAST, casadi/main.py:185-192)
   if (threadIdx.x == 0) {
     A.iters[ci] = iters;
-    if (e >= 0) A.edge_active[e] = act ? 1 : 0;
+    if (e >= 0) {
+      A.edge_active[e] = act ? 1 : 0;
+      A.dischk[e] = dis_chk;
+    }
+    A.cst[(size_t)ci * 4 + 0] = flag;
+    A.cst[(size_t)ci * 4 + 1] = aliased;
+    if ((flags & F_NANLAST) && iters > 0) {      // global stop at the collision test of this iteration
+      resid[2 * (iters - 1) + 0] = NAN;
+      resid[2 * (iters - 1) + 1] = NAN;
+    }
+  }
+  {
+    __shared__ int s_warm;
+    if (threadIdx.x == 0) s_warm = 0;
+    __syncthreads();
+    if (l == 0 && w < na && warm_x) atomicOr(&s_warm, 1 << w);
+    if (l == 0 && w == 0 && e >= 0 && warm_e) atomicOr(&s_warm, 4);
+    __syncthreads();
+    if (threadIdx.x == 0) A.cst[(size_t)ci * 4 + 2] = s_warm;
   }
   if (w < na) {
     const int a = a0 + w;
     for (int i = l; i < 2 * H1; i += WAVE) A.pos_old[(size_t)a * 2 * H1 + i] = S.pos[w * 2 * H1 + i];
     const double u = (l < H) ? S.u[w * H + l] : 0.0;
     if (l < H) A.u[(size_t)a * H + l] = u;
-    double px, py, pth;
-    rollout(S.xt + 3 * w, A.spd[a], u, c, H, true, px, py, pth);
-    if (l == 1) {
-      A.xt[3 * a + 0] = px;
-      A.xt[3 * a + 1] = py;
-      A.xt[3 * a + 2] = pth;
-    }
     if (l == 0) {
       A.status[a] = status_x;
       A.rho_x[a] = qx.rho;
-      A.warm_ok[a] = 1;
-    }
-    if (l < HMAX) {
-      signed char* lb = A.lab_x + (size_t)a * 2 * HMAX;
-      lb[l] = lab_x[0];
-      lb[HMAX + l] = lab_x[1];
     }
     if (A.xcache_rho[a] != qx.rho) {       // adaptive rho rebuilt K_s^-1 in LDS: refresh the cache
       double* Kc = A.Kx_cache + (size_t)a * H * H;
       for (int i = l; i < H * H; i += WAVE) Kc[i] = qx.K[i];
       if (l == 0) A.xcache_rho[a] = qx.rho;
     }
-  }
-  if (w == 0 && e >= 0 && l == 0) A.rho_e[e] = qe.rho;
-  if (e >= 0) {
-    for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) {
-      A.hat[(size_t)e * 4 * H1 + i] = S.hat[i];
-      A.lam[(size_t)e * 4 * H1 + i] = S.lam[i];
+    if (!last_launch) {
+      double* qs = A.qs_x + (size_t)a * 5 * WAVE;
+      signed char* ql = A.ql_x + (size_t)a * 2 * WAVE;
+      qs[l] = xs_x[0];
+      qs[WAVE + l] = zs_x[0];
+      qs[2 * WAVE + l] = zs_x[1];
+      qs[3 * WAVE + l] = ys_x[0];
+      qs[4 * WAVE + l] = ys_x[1];
+      ql[l] = lab_x[0];
+      ql[WAVE + l] = lab_x[1];
+    } else {
+      double px, py, pth;
+      rollout(S.xt + 3 * w, A.spd[a], u, c, H, true, px, py, pth);
+      if (l == 1) {
+        A.xt[3 * a + 0] = px;
+        A.xt[3 * a + 1] = py;
+        A.xt[3 * a + 2] = pth;
+      }
+      if (l == 0) A.warm_ok[a] = 1;
+      if (l < HMAX) {
+        signed char* lb = A.lab_x + (size_t)a * 2 * HMAX;
+        lb[l] = lab_x[0];
+        lb[HMAX + l] = lab_x[1];
+      }
     }
+  }
+  if (w == 0 && e >= 0) {
+    if (l == 0) A.rho_e[e] = qe.rho;
+    if (!last_launch) {
+      double* qs = A.qs_e + (size_t)e * 12 * WAVE;
+      signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
+      qs[l] = xs_e[0];
+      qs[WAVE + l] = xs_e[1];
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        qs[(2 + s) * WAVE + l] = zs_e[s];
+        qs[(7 + s) * WAVE + l] = ys_e[s];
+        ql[s * WAVE + l] = lab_e[s];
+      }
+    }
+  }
+  if (e >= 0) {
+    double* const edge_lds[5] = {S.hat, S.lam, S.S, S.D, S.last};
+    double* const edge_hbm[5] = {A.hat, A.lam, A.Sacc, A.Dacc, A.last};
+    for (int k = 0; k < 5; ++k)
+      for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) edge_hbm[k][(size_t)e * 4 * H1 + i] = edge_lds[k][i];
     if (threadIdx.x == 0) A.status[A.N + e] = status_e;
   }
 }
 
-int launch_mpc_step(const DevArgs& a, int t, hipStream_t s) {
+// Global termination partials of outer iteration `it` (one workgroup): rk, sk summed over
+// components, active pairs, pairs with a distance check, pairs failing it.
+__global__ void __launch_bounds__(256) k_term_partials(DevArgs A, int it, double* out) {
+  __shared__ double red[5][256];
+  double v[5] = {0, 0, 0, 0, 0};
+  for (int ci = threadIdx.x; ci < A.C; ci += 256) {
+    const double* r = A.resid + ((size_t)ci * A.cfg.max_outer + it) * 2;
+    if (r[0] == r[0]) v[0] += r[0];
+    if (r[1] == r[1]) v[1] += r[1];
+  }
+  for (int e = threadIdx.x; e < A.E; e += 256) {
+    v[2] += A.edge_active[e] ? 1.0 : 0.0;
+    const double d = A.dischk[e];
+    if (d == d) {
+      v[3] += 1.0;
+      v[4] += (d > A.deff[e]) ? 0.0 : 1.0;
+    }
+  }
+  for (int k = 0; k < 5; ++k) red[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int k = 0; k < 5; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 5) out[threadIdx.x] = red[threadIdx.x][0];
+}
+
+// Residual history of a fixed-iteration step summed over components: out[it] = (rk, sk).
+__global__ void __launch_bounds__(256) k_resid_history(DevArgs A, double* out) {
+  const int it = blockIdx.x;
+  __shared__ double red[2][256];
+  double rk = 0.0, sk = 0.0;
+  for (int ci = threadIdx.x; ci < A.C; ci += 256) {
+    const double* r = A.resid + ((size_t)ci * A.cfg.max_outer + it) * 2;
+    if (r[0] == r[0]) rk += r[0];
+    if (r[1] == r[1]) sk += r[1];
+  }
+  red[0][threadIdx.x] = rk;
+  red[1][threadIdx.x] = sk;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[2 * it + 0] = red[0][0];
+    out[2 * it + 1] = red[1][0];
+  }
+}
+
+// Safety distance per pair for the partials (the kernel recomputes it per launch).
+__global__ void k_pair_deff(DevArgs A) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= A.E) return;
+  const piadmm_config_t& c = A.cfg;
+  const int v1 = A.edges[2 * e], v2 = A.edges[2 * e + 1];
+  double d = c.dis_thres;
+  if (c.tighten)
+    d = c.dis_thres + delay_norm(c, A.xt[3 * v1 + 2], A.spd[v1]) + delay_norm(c, A.xt[3 * v2 + 2], A.spd[v2]);
+  A.deff[e] = d;
+}
+
+int launch_mpc_step(const DevArgs& a, int t, int it0, int it1, int flags, hipStream_t s) {
   const size_t sh = lds_bytes(a.cfg.H);
   static bool attr = false;
 #ifdef PIADMM_STAMPS
@@ -1919,7 +2103,23 @@ int launch_mpc_step(const DevArgs& a, int t, hipStream_t s) {
       return -1;
     attr = true;
   }
-  hipLaunchKernelGGL(k_mpc_step, dim3(a.C), dim3(NW * WAVE), sh, s, a, t);
+  hipLaunchKernelGGL(k_mpc_step, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, it0, it1, flags);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_term_partials, dim3(1), dim3(256), 0, s, a, it, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_resid_history(const DevArgs& a, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_resid_history, dim3(a.cfg.max_outer), dim3(256), 0, s, a, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_pair_deff(const DevArgs& a, hipStream_t s) {
+  if (a.E == 0) return 0;
+  hipLaunchKernelGGL(k_pair_deff, dim3((a.E + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

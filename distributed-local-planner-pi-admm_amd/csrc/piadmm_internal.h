@@ -45,6 +45,18 @@ struct DevArgs {
                             //   [0, 4H^2) P^-1 (2H x 2H, block-diagonal), [4H^2, 6H^2) PGt (H x 2H,
                             //   row k = P_v^-1 T(k+1,.)'), [6H^2, 8H^2) GPG (Z_v = T P_v^-1 T')
   int* warm_ok;             // N          1: lab_x holds the labels of the previous MPC step
+  // per-step state carried between the launches of one step (term_global) and, for the
+  // PI accumulators, between steps (warm_duals)
+  double* Sacc;             // E*2*2*(H+1) PI integral S
+  double* Dacc;             // E*2*2*(H+1) back-calculation D
+  double* last;             // E*2*2*(H+1) last_iter_hat_pos (dual residual)
+  double* dischk;           // E   dis_vec(2) of the pair's last dual update (NaN: none yet)
+  double* deff;             // E   safety distance of the pair for the current step
+  double* qs_x;             // N*5*WAVE  ADMM state (xs, zs0, zs1, ys0, ys1) of the x-step QP
+  signed char* ql_x;        // N*2*WAVE  labels of the x-step QP
+  double* qs_e;             // E*12*WAVE ADMM state (xs0, xs1, zs0..4, ys0..4) of the pair QP
+  signed char* ql_e;        // E*5*WAVE  labels of the pair QP
+  int* cst;                 // C*4       flag, aliased, warm bits (x0, x1, pair), spare
   unsigned long long* counters;  // C*8  accumulated work counters (see piadmm_get_counters)
   unsigned long long* stamps;    // C*32 phase cycle sums (diagnostic build -DPIADMM_STAMPS only)
   double* rho_x;            // N   ADMM penalty per agent QP (adapted, persists across steps)
@@ -73,6 +85,15 @@ inline size_t lds_bytes(int H) {
   return d * sizeof(double);
 }
 
-int launch_mpc_step(const DevArgs& a, int t, hipStream_t s);
+// launch flags of k_mpc_step
+constexpr int F_FIRST = 1;    // first launch of the step: seeds, zero / warm per-step state
+constexpr int F_LAST = 2;     // last launch: outputs, propagation, cross-step warm labels
+constexpr int F_GLOBAL = 4;   // termination decided outside (term_global): no per-component stop
+constexpr int F_NANLAST = 8;  // the global loop stopped at the collision test of iteration it0-1
+
+int launch_mpc_step(const DevArgs& a, int t, int it0, int it1, int flags, hipStream_t s);
+int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s);
+int launch_resid_history(const DevArgs& a, double* out, hipStream_t s);
+int launch_pair_deff(const DevArgs& a, hipStream_t s);
 
 }  // namespace pd

@@ -31,6 +31,8 @@ class PiadmmConfigC(ctypes.Structure):
         ("fixed_iters", c_i32), ("max_inner", c_i32),
         ("admm_rho", c_dbl), ("admm_sigma", c_dbl), ("admm_alpha", c_dbl), ("qp_tol", c_dbl),
         ("polish_every", c_i32), ("device", c_i32),
+        ("term_global", c_i32), ("warm_duals", c_i32), ("tighten", c_i32), ("reserved0", c_i32),
+        ("tight_p", c_dbl), ("avg_delay", c_dbl), ("var_delay", c_dbl),
     ]
 
 
@@ -41,6 +43,8 @@ def to_c(cfg: PIADMMConfig, n_agents: int, device: int = 0) -> PiadmmConfigC:
             c.n_agents = int(n_agents)
         elif name == "device":
             c.device = int(device)
+        elif name == "reserved0":
+            c.reserved0 = 0
         else:
             setattr(c, name, getattr(cfg, name))
     return c
@@ -71,6 +75,9 @@ SYMBOLS = [
     ("piadmm_reset_counters", c_i32, [_H]),
     ("piadmm_get_component_counters", c_i32, [_H, _P(ctypes.c_uint64), c_i32]),
     ("piadmm_debug_stamps", c_i32, [_H, _P(ctypes.c_uint64), c_i32]),
+    ("piadmm_comm_unique_id", c_i32, [_P(ctypes.c_uint8)]),
+    ("piadmm_comm_init", c_i32, [_H, _P(ctypes.c_uint8), c_i32, c_i32]),
+    ("piadmm_global_resid", c_i32, [_H, _dp, _ip]),
 ]
 
 _lib = None

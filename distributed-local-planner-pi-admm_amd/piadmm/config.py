@@ -56,6 +56,15 @@ class PIADMMConfig:
     pos_model: int = POS_LINEAR   # B15: pos_old rollout model
     term_dist_check: int = 0    # MATLAB extra stop condition dis_vec(2) > dis_thres (:202)
     fixed_iters: int = 0        # 1: never terminate early (throughput runs)
+    # --- N-agent semantics and hot-path extensions (B9) ---
+    term_global: int = 0        # B9: 1 = flag / termination over ALL agents (reference, casadi/main.py:115-118,174);
+                                #     0 = per connected component (N-agent generalisation)
+    warm_duals: int = 0         # a12: 1 = receding-horizon shift of hat / lam / S / D between MPC steps
+                                #      (OBCA iterate_next_state, decentralized/optimizer.py:337-344)
+    tighten: int = 0            # a13: 1 = delay-tightened safety distance (decentralized/util.py:70-101)
+    tight_p: float = 0.95       # VehicleConfig.prob       (veh_config.py:27)
+    avg_delay: float = 0.05     # VehicleConfig.avg_delay  (veh_config.py:25)
+    var_delay: float = 0.025    # VehicleConfig.var_delay  (veh_config.py:26)
     # --- inner QP solver (build's own; not in the reference) ---
     admm_rho: float = 0.05      # ADMM penalty in the Ruiz-scaled space (tools/qp_sim.py sweep)
     admm_sigma: float = 1e-6
@@ -70,6 +79,10 @@ class PIADMMConfig:
     @property
     def thr_collide(self) -> float:
         return self.dis_thres ** 2 if self.collide_sq_thres else self.dis_thres
+
+    def collide_thr(self, d_eff: float) -> float:
+        """Collision-test threshold for safety distance d_eff (B2: Python compares d^2 with d_eff)."""
+        return d_eff * d_eff if self.collide_sq_thres else d_eff
 
 
 def casadi_default(**kw) -> PIADMMConfig:

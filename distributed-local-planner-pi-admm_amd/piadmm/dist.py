@@ -3,10 +3,17 @@
 The reference runs every agent in one Python loop (``casadi/main.py:81``,
 ``for i_veh in range(num_veh)``); nothing is distributed.  Here the agents of
 a scenario are split over ranks by connected component of the candidate-pair
-graph.  Because termination is per component and a component never
-straddles ranks, the outer ADMM loop of a rank needs nothing from any other
-rank: the data path has no collective.  Only the harness (bench.py) uses
-torch.distributed, for its barrier and max-over-ranks timing.
+graph; a component never straddles ranks.
+
+* per-component termination (default): the outer loop of a rank needs nothing
+  from any other rank -- no data-path collective.
+* ``term_global`` (the reference's global flag / termination, quirk B9): the
+  library all-reduces the termination partials over RCCL (xGMI) once per outer
+  iteration -- or the residual history once per MPC step when ``fixed_iters`` --
+  through the communicator :func:`attach_rccl` sets up.
+
+The harness (bench.py) uses torch.distributed (gloo) only for its barrier,
+max-over-ranks timing and to ship the RCCL unique id.
 """
 from __future__ import annotations
 
@@ -48,3 +55,14 @@ def shard(scn: Scenario, rank: int, world: int) -> Scenario:
         raise ValueError("a candidate pair straddles two ranks")
     return Scenario(spd=scn.spd[a0:a1].copy(), xt0=scn.xt0[a0:a1].copy(), ref=scn.ref[a0:a1].copy(),
                     edges=(scn.edges[sel] - a0).astype(np.int32), n_steps=scn.n_steps)
+
+
+def attach_rccl(solver, rank: int, world: int, broadcast_bytes):
+    """Create the RCCL communicator of a sharded job on ``solver`` (a PI_ADMM_MI355X).
+
+    ``broadcast_bytes(b: bytes | None) -> bytes`` ships rank 0's 128-byte unique id to every
+    rank over any out-of-band channel (bench.py uses torch.distributed's gloo group)."""
+    from .solver import comm_unique_id
+    uid = comm_unique_id() if rank == 0 else None
+    uid = broadcast_bytes(uid)
+    solver.comm_init(uid, world, rank)

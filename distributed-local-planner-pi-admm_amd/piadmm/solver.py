@@ -29,6 +29,8 @@ class StepResult:
     resid: np.ndarray      # (C, max_outer, 2) (rk, sk) per executed iteration, NaN after
     iters: np.ndarray      # (C,) outer iterations executed (iter_his, :186)
     status: np.ndarray     # (N+E,) PIADMM_QP_* flags per agent then per pair
+    global_resid: np.ndarray | None = None   # term_global: (max_outer, 2) summed over all ranks
+    global_iters: int | None = None          # term_global: outer iterations of the whole job
 
 
 class PI_ADMM_MI355X:
@@ -84,7 +86,25 @@ class PI_ADMM_MI355X:
         self.iter_his.append(iters)
         self.x_vec.append(xt[:, :2].T.copy())
         self.u_vec.append(u[:, 0].copy())
-        return StepResult(xt=xt, u=u, resid=resid, iters=iters, status=status)
+        res = StepResult(xt=xt, u=u, resid=resid, iters=iters, status=status)
+        if self.cfg.term_global:
+            res.global_resid, res.global_iters = self.global_resid()
+        return res
+
+    def global_resid(self):
+        """(max_outer, 2) residual history summed over every pair of every rank, and the
+        job's outer-iteration count (term_global; casadi/main.py:164-178 over all agents)."""
+        out = np.empty((self.cfg.max_outer, 2))
+        n = ctypes.c_int32()
+        self._check(self.lib.piadmm_global_resid(self._h, _lib.dptr(out), ctypes.byref(n)))
+        return out, int(n.value)
+
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int):
+        """Join the RCCL communicator of a sharded term_global job (piadmm_comm_init)."""
+        if len(unique_id) != 128:
+            raise ValueError("an RCCL unique id has 128 bytes")
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._check(self.lib.piadmm_comm_init(self._h, buf, int(nranks), int(rank)))
 
     def run(self, n_steps: int | None = None) -> list[StepResult]:
         n = self.scn.n_steps if n_steps is None else n_steps
@@ -156,3 +176,10 @@ class PI_ADMM_MI355X:
 
 def device_count() -> int:
     return int(_lib.load().piadmm_device_count())
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 creates it and ships it to the other ranks)."""
+    buf = (ctypes.c_uint8 * 128)()
+    _lib.check(_lib.load().piadmm_comm_unique_id(buf))
+    return bytes(buf)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PIADMM_ABI_VERSION 1
+#define PIADMM_ABI_VERSION 2
 
 enum {
   PIADMM_OK = 0,
@@ -74,6 +74,16 @@ typedef struct piadmm_config {
   double admm_rho, admm_sigma, admm_alpha, qp_tol;
   int32_t polish_every;      /* PDAS polish attempt period (ADMM iterations) */
   int32_t device;            /* HIP device ordinal */
+  /* ABI 2: N-agent semantics and the hot path's remaining rows */
+  int32_t term_global;       /* 1: flag / termination over ALL agents of all ranks (casadi/main.py:
+                                115-118,174; one RCCL all-reduce per outer iteration when sharded);
+                                0: per connected component */
+  int32_t warm_duals;        /* 1: hat, lam, S, D shifted one slot into the next MPC step
+                                (iterate_next_state, Distributed_planner/decentralized/optimizer.py:337-344) */
+  int32_t tighten;           /* 1: delay-tightened safety distance d_eff = dis_thres + |delta_i| + |delta_j|
+                                (compute_square_halfspaces_ca_prob, decentralized/util.py:70-101) */
+  int32_t reserved0;
+  double tight_p, avg_delay, var_delay;   /* VehicleConfig prob / avg_delay / var_delay (veh_config.py:25-27) */
 } piadmm_config_t;
 
 typedef struct piadmm_ctx* piadmm_handle_t;
@@ -136,6 +146,21 @@ int32_t piadmm_get_counters(piadmm_handle_t h, uint64_t* out8);
 int32_t piadmm_reset_counters(piadmm_handle_t h);
 /* The same counters per component (C x 8 uint64, n >= 8*C). */
 int32_t piadmm_get_component_counters(piadmm_handle_t h, uint64_t* out, int32_t n);
+
+/* Multi-GPU (term_global): one process per GPU, one handle each, joined by an RCCL
+ * communicator over xGMI.  Rank 0 calls piadmm_comm_unique_id and ships the 128 bytes to
+ * the other ranks (any out-of-band channel); every rank then calls piadmm_comm_init.
+ * mpc_step then all-reduces the termination partials (rk, sk, active pairs, distance
+ * checks) once per outer iteration, or, with fixed_iters, the residual history once per
+ * MPC step.  Components never straddle ranks.  Without a communicator the handle is a
+ * single-rank job. */
+int32_t piadmm_comm_unique_id(uint8_t* id_out /* 128 bytes */);
+int32_t piadmm_comm_init(piadmm_handle_t h, const uint8_t* id /* 128 bytes */, int32_t nranks, int32_t rank);
+
+/* Global residual history of the last step (term_global): max_outer x 2 (rk, sk summed over
+ * every active pair of every rank, NaN after the last executed iteration) and the number of
+ * executed outer iterations (equal on every rank). */
+int32_t piadmm_global_resid(piadmm_handle_t h, double* resid_out, int32_t* iters_out);
 
 /* Diagnostic builds (-DPIADMM_STAMPS, libpiadmm_stamps.so) only: per-component
  * cycle sums of the kernel phases (C x 32 uint64); PIADMM_E_STATE otherwise. */

@@ -23,7 +23,7 @@ def test_library_is_built_for_gfx950():
     lib = _lib.load()
     info = lib.piadmm_build_info().decode()
     assert "gfx950" in info
-    assert lib.piadmm_abi_version() == 1
+    assert lib.piadmm_abi_version() == 2
 
 
 def test_exports_every_declared_symbol():
@@ -38,11 +38,11 @@ def test_exports_every_declared_symbol():
 
 def test_config_struct_layout():
     lib = _lib.load()
-    assert lib.piadmm_config_size() == ctypes.sizeof(_lib.PiadmmConfigC) == 216
+    assert lib.piadmm_config_size() == ctypes.sizeof(_lib.PiadmmConfigC) == 256
     c = _lib.to_c(config.matlab_pi(H=30), n_agents=256, device=3)
     assert (c.n_agents, c.H, c.device, c.dual_mode, c.windup) == (256, 30, 3, 1, 1)
     # every dataclass field the struct carries is mirrored
-    fields = {f for f, _ in _lib.PiadmmConfigC._fields_} - {"n_agents", "device"}
+    fields = {f for f, _ in _lib.PiadmmConfigC._fields_} - {"n_agents", "device", "reserved0"}
     assert fields <= set(config.PIADMMConfig.__dataclass_fields__)
 
 

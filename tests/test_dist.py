@@ -4,6 +4,9 @@ Each rank owns whole components (piadmm.dist.shard), runs its shard through the
 oracle (the CPU stand-in for one GPU) and the shards are gathered; the result
 must equal one process running all agents, because no component straddles ranks.
 The same harness (barrier + max-over-ranks timing) is what bench.py uses.
+
+With term_global the ranks exchange their termination partials once per outer
+iteration -- the protocol libpiadmm runs over RCCL -- here as a gloo all-reduce.
 """
 import os
 import socket
@@ -64,3 +67,60 @@ def test_two_rank_shards_match_single_process(tmp_path):
     for _ in range(3):
         orc.run(10)
     np.testing.assert_array_equal(np.load(out), orc.xt)
+
+
+def _global_worker(rank, world, port, out):
+    import sys
+    from conftest import PKG, ROOT
+    sys.path[:0] = [ROOT, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import piadmm_oracle as O
+    from piadmm import config, dist, scenario
+    scn = scenario.tiled(5, 15, n_steps=30, seed=3)
+    sub = dist.shard(scn, rank, world)
+    orc = O.Oracle(config.casadi_default(H=15, term_global=1), sub)
+    calls = [0]
+
+    def allreduce(part):
+        calls[0] += 1
+        t = torch.tensor(part, dtype=torch.float64)
+        tdist.all_reduce(t)                      # libpiadmm: ncclAllReduce(sum) of 5 doubles
+        return t.numpy()
+    its, ghist = [], []
+    for _ in range(12):
+        r = orc.mpc_step(reduce=allreduce)
+        its.append(r.iters.tolist())
+        ghist.append(np.array(r.global_resid).reshape(-1, 2))
+    a0, _ = dist.shard_bounds(scn, rank, world)
+    gathered = [None] * world
+    tdist.all_gather_object(gathered, {"a0": a0, "xt": orc.xt, "its": its, "ghist": ghist, "calls": calls[0]})
+    if rank == 0:
+        xt = np.zeros((scn.n_agents, 3))
+        for g in gathered:
+            xt[g["a0"]:g["a0"] + g["xt"].shape[0]] = g["xt"]
+        np.savez(out, xt=xt, its0=np.array(gathered[0]["its"][-1]), its1=np.array(gathered[1]["its"][-1]),
+                 g0=np.concatenate(gathered[0]["ghist"]), g1=np.concatenate(gathered[1]["ghist"]),
+                 calls=np.array([g["calls"] for g in gathered]))
+    tdist.destroy_process_group()
+
+
+def test_two_rank_global_termination_matches_single_process(tmp_path):
+    """Sharded term_global (one all-reduce of the partials per outer iteration) equals the
+    unsharded job: same states, same job-wide iteration count and residual history."""
+    out = str(tmp_path / "g.npz")
+    mp.spawn(_global_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    from oracle import piadmm_oracle as O
+    from piadmm import config, scenario
+    scn = scenario.tiled(5, 15, n_steps=30, seed=3)
+    orc = O.Oracle(config.casadi_default(H=15, term_global=1), scn)
+    ghist = []
+    for _ in range(12):
+        r = orc.mpc_step()
+        ghist.append(np.array(r.global_resid).reshape(-1, 2))
+    d = np.load(out)
+    np.testing.assert_array_equal(d["xt"], orc.xt)
+    assert set(d["its0"].tolist()) == set(d["its1"].tolist()) == {int(r.iters[0])}
+    np.testing.assert_allclose(d["g0"], np.concatenate(ghist), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(d["g1"], d["g0"], rtol=0, atol=0)
+    assert d["calls"][0] == d["calls"][1] > 0

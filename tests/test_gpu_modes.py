@@ -1,0 +1,90 @@
+"""GPU parity of the ABI-2 modes through the C-ABI: global termination (stepped launches,
+host decision from all-reduced partials), receding-horizon dual warm start (a12), delay
+tightening (a13), and the RCCL communicator on a single rank.  Tolerances as in
+test_gpu_parity.py (held 1e-8, contract 1e-5)."""
+import numpy as np
+import pytest
+
+from oracle import piadmm_oracle as O
+from piadmm import config, scenario
+
+pytestmark = pytest.mark.gpu
+RTOL = ATOL = 1e-8
+
+
+@pytest.fixture(scope="module")
+def Solver():
+    from piadmm.solver import PI_ADMM_MI355X, device_count
+    if device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests need an MI355X")
+    return PI_ADMM_MI355X
+
+
+def close(a, b):
+    np.testing.assert_allclose(a, b, rtol=RTOL, atol=ATOL)
+
+
+def compare(Solver, cfg, scn, n_steps, setup=None):
+    orc = O.Oracle(cfg, scn)
+    with Solver(cfg, scn) as s:
+        if setup:
+            setup(s)
+        for _ in range(n_steps):
+            ro, rg = orc.mpc_step(), s.mpc_step()
+            np.testing.assert_array_equal(rg.status, 0)
+            np.testing.assert_array_equal(rg.iters, ro.iters)
+            close(rg.xt, ro.xt)
+            close(rg.u, ro.u)
+            for c in range(s.C):
+                n = len(ro.resid[c])
+                if n:
+                    close(rg.resid[c, :n], np.array(ro.resid[c]))
+                assert np.all(np.isnan(rg.resid[c, n:]))
+            if cfg.term_global:
+                n = len(ro.global_resid)
+                assert rg.global_iters == int(ro.iters[0])
+                if n:
+                    close(rg.global_resid[:n], np.array(ro.global_resid))
+                assert np.all(np.isnan(rg.global_resid[n:]))
+
+
+@pytest.mark.parametrize("preset", ["casadi_default", "matlab_pi"])
+def test_global_termination_matches_oracle(Solver, preset):
+    compare(Solver, config.PRESETS[preset](H=15, term_global=1), scenario.tiled(3, 15, n_steps=30, seed=3), 14)
+
+
+def test_global_termination_fixed_iterations(Solver):
+    compare(Solver, config.matlab_pi(H=12, fixed_iters=1, max_outer=6, term_global=1),
+            scenario.tiled(2, 12, n_steps=10, seed=1), 4)
+
+
+def test_global_termination_without_any_collision(Solver):
+    """No pair ever collides: the job stops at the first collision test (resid NaN)."""
+    compare(Solver, config.matlab_pi(H=10, term_global=1), scenario.tiled(3, 10, n_steps=12, seed=3), 3)
+
+
+@pytest.mark.parametrize("preset", ["casadi_default", "matlab_pi"])
+def test_warm_duals_match_oracle(Solver, preset):
+    compare(Solver, config.PRESETS[preset](H=15, warm_duals=1), scenario.tiled(2, 15, n_steps=30, seed=5), 20)
+
+
+def test_tightening_matches_oracle(Solver):
+    compare(Solver, config.matlab_pi(H=15, tighten=1, avg_delay=0.2, var_delay=0.1),
+            scenario.tiled(2, 15, n_steps=30, seed=6), 20)
+
+
+def test_all_modes_together_at_bench_horizon(Solver):
+    cfg = config.matlab_pi(H=30, term_global=1, warm_duals=1, tighten=1)
+    compare(Solver, cfg, scenario.tiled(2, 30, n_steps=10, seed=8), 6)
+
+
+def test_rccl_single_rank_communicator(Solver):
+    """The RCCL path (ncclCommInitRank + one all-reduce per outer iteration) on one rank
+    gives the same job as no communicator."""
+    from piadmm.solver import comm_unique_id
+    uid = comm_unique_id()
+    assert len(uid) == 128
+    compare(Solver, config.casadi_default(H=15, term_global=1), scenario.tiled(3, 15, n_steps=30, seed=3), 6,
+            setup=lambda s: s.comm_init(uid, 1, 0))
+    compare(Solver, config.matlab_pi(H=12, fixed_iters=1, max_outer=6, term_global=1),
+            scenario.tiled(2, 12, n_steps=10, seed=1), 3, setup=lambda s: s.comm_init(comm_unique_id(), 1, 0))
