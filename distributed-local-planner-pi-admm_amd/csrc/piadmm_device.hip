@@ -794,8 +794,9 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     }
     STAMP_ADD(NV == 1 ? ST_RED_S : ST_ZR_S, t_s);
     unsigned long long t_c = STAMP_T();
-    const double dmax = wmax(l < m ? sdiag : 0.0);
-    const double delta = 1e-14 * dmax;
+    // no diagonal shift: a dependent working-set row is dropped by its collapsed pivot
+    // (chol_factor); a shift would hide the collapse of rows with a small S_kk
+    const double delta = 0.0;
     wsync();
     linv = 0.0;
     const bool fok = chol_factor(P.fac, ld, sdiag, delta, m, linv);
@@ -924,10 +925,8 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   unsigned long long t_c = STAMP_T();
   wsync();
   double linv = 0.0;
-  // the same relative shift as the pair's factor: a transiently dependent W (PDAS label
-  // updates can propose one) still yields a usable step instead of an overflowing one
-  const double dmax = wmax(l < m ? sdiag : 0.0);
-  if (!chol_factor(fac, ld, sdiag, 1e-14 * dmax, m, linv)) return false;
+  // unshifted: a dependent working-set row (degenerate vertex) is dropped by chol_factor
+  if (!chol_factor(fac, ld, sdiag, 0.0, m, linv)) return false;
   if (l < m) P.fdiag[64 + l] = linv;
   STAMP_ADD(ST_RED_CHOL, t_c);
   unsigned long long t_x = STAMP_T();
@@ -1140,19 +1139,39 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
       continue;
     }
     const double tp = P.tol * (1.0 + fabs(P.lo(s)));
-    const double c = rrow(P, s) * P.E[s] * P.E[s];
-    const double wv = ax[s] + y[s] / c;
+    // Label update: a violated row changes state by one step only -- an active row whose
+    // multiplier has the wrong sign is released (never flipped to the opposite bound), a
+    // free row becomes active only when its bound is violated beyond the tolerance.  At a
+    // degenerate vertex (dependent rows, zero multipliers) this releases the row that
+    // received the wrong-signed multiplier instead of cycling between the two bounds.
     if (P.hinge(s)) {
       const double h = P.lo(s);
-      if (lab[s] == HZERO) ok &= ax[s] >= h - tp;
-      else if (lab[s] == HLINEAR) ok &= ax[s] <= h + tp;
-      else ok &= (y[s] <= ty) && (y[s] >= -P.beta - ty);
-      nlab[s] = wv >= h ? HZERO : (wv <= h - P.beta / c ? HLINEAR : HKINK);
+      if (lab[s] == HZERO) {
+        const bool v = ax[s] < h - tp;
+        ok &= !v;
+        nlab[s] = v ? HKINK : HZERO;
+      } else if (lab[s] == HLINEAR) {
+        const bool v = ax[s] > h + tp;
+        ok &= !v;
+        nlab[s] = v ? HKINK : HLINEAR;
+      } else {
+        // a kink row must sit at h: the reduced solve drops a dependent row, which is only
+        // right when the dropped equation is implied by the others (consistent labels)
+        ok &= (y[s] <= ty) && (y[s] >= -P.beta - ty) && fabs(ax[s] - h) <= tp;
+        nlab[s] = (y[s] > ty) ? HZERO : ((y[s] < -P.beta - ty) ? HLINEAR : HKINK);
+      }
     } else {
-      if (lab[s] == FREE) ok &= (ax[s] >= P.lo(s) - tp) && (ax[s] <= P.hi(s) + tp);
-      else if (lab[s] == LOWER) ok &= y[s] <= ty;
-      else ok &= y[s] >= -ty;
-      nlab[s] = wv <= P.lo(s) ? LOWER : (wv >= P.hi(s) ? UPPER : FREE);
+      if (lab[s] == FREE) {
+        const bool vl = ax[s] < P.lo(s) - tp, vu = ax[s] > P.hi(s) + tp;
+        ok &= !vl && !vu;
+        nlab[s] = vl ? LOWER : (vu ? UPPER : FREE);
+      } else if (lab[s] == LOWER) {
+        ok &= (y[s] <= ty) && fabs(ax[s] - P.lo(s)) <= tp;   // equality too (dropped rows)
+        nlab[s] = (y[s] > ty) ? FREE : LOWER;
+      } else {
+        ok &= (y[s] >= -ty) && fabs(ax[s] - P.hi(s)) <= tp;
+        nlab[s] = (y[s] < -ty) ? FREE : UPPER;
+      }
     }
     ok &= isfinite(x[0]) && isfinite(y[s]);
   }
@@ -1258,7 +1277,10 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
     admm_iter(P, xs, zs, ys);
     STAMP_ADD(ST_ADMM, t_a);
     ++n_admm;
-    if (it % ADAPT_EVERY == 0) {
+    // adaptive rho for the x-step only: on the pair QPs with long runs of hinge kinks the
+    // OSQP rule stalls ADMM (tools/pair_policy.py: 3 of 15 hard pair QPs uncertified after
+    // 4000 iterations with it, all 15 certified within 530 without it)
+    if (NV == 1 && it % ADAPT_EVERY == 0) {
       const double f = rho_ratio(P, xs, zs, ys);
       if (f != 1.0) {
         P.rho = fmin(fmax(P.rho * f, 1e-6), 1e6);

@@ -117,9 +117,11 @@ def run_fixture(name):
 
 
 # Bench tiles (scenario.tiled(128, 30, seed=0): tile k is seeded with k) whose MPC step t
-# reaches degenerate x-step QPs: a dependent working set (u_k = -umax, u_{k+3} = +umax and
-# the three rates between them at +dumax) with a zero multiplier.
-DEGENERATE = ((79, 15), (108, 15), (88, 18))
+# holds hard QPs: degenerate x-step vertices -- a dependent working set (u_k = -umax,
+# u_{k+3} = +umax and the three rates between them) with a zero multiplier, at t = 15, 18
+# (dependent row last in working-set order) and t = 31 (dependent row first) -- and pair QPs
+# with the safety hinge at its kink over the whole horizon (t = 27, 31).
+DEGENERATE = ((79, 15), (108, 15), (88, 18), (13, 31), (37, 27), (15, 31))
 DEG_OUTER = 8
 
 
@@ -130,7 +132,7 @@ def gen_degenerate():
     cfg_chk = config.matlab_pi(H=H, fixed_iters=1, max_outer=DEG_OUTER)
     rec = {k: [] for k in ("tile", "t", "xt_t", "xt_next", "u", "spd", "ref", "xt0")}
     for tile, t in DEGENERATE:
-        scn = scenario.tiled(1, H, n_steps=22, perturb=True, seed=tile)
+        scn = scenario.tiled(1, H, n_steps=40, perturb=True, seed=tile)
         orc = O.Oracle(cfg_run, scn)
         for _ in range(t):
             orc.mpc_step()

@@ -124,15 +124,16 @@ def test_bench_workload_sampled_tiles_match_oracle(Solver):
 
 
 def test_degenerate_xstep_working_sets(Solver):
-    """Bench tiles whose x-step QPs have a linearly dependent optimal working set (two box
-    rows and the three rate rows between them, one zero multiplier): the polish drops the
-    dependent row and certifies the vertex (a singular Schur complement used to leave these
-    QPs uncertified after max_inner ADMM iterations).  Oracle state from oracle/gen_golden.py."""
+    """Bench tiles with hard QPs (oracle/gen_golden.py DEGENERATE): x-step QPs whose optimal
+    working set is linearly dependent (two box rows and the three rate rows between them,
+    one zero multiplier) -- the polish drops the dependent row and the one-step label update
+    releases a wrong-signed row instead of flipping it -- and pair QPs with the hinge at its
+    kink over the whole horizon (ADMM without the adaptive penalty).  All certified."""
     d = np.load(os.path.join(GOLD, "degenerate_xstep.npz"), allow_pickle=False)
     cfg = config.matlab_pi(H=30, fixed_iters=1, max_outer=int(d["outer"]))
     for k in range(len(d["tile"])):
         scn = scenario.Scenario(spd=d["spd"][k], xt0=d["xt0"][k], ref=d["ref"][k],
-                                edges=np.array([[0, 1]], np.int32), n_steps=22)
+                                edges=np.array([[0, 1]], np.int32), n_steps=40)
         with Solver(cfg, scn) as s:
             s.set_xt(d["xt_t"][k])
             s.reset_counters()

@@ -147,8 +147,9 @@ def scale_problem(gq, mode):
         for _ in range(15):
             cn = np.maximum(np.abs(P).max(axis=0), np.abs(A).max(axis=0))
             rn = np.abs(A).max(axis=1)
-            dd = 1.0 / np.sqrt(np.maximum(cn, 1e-8))
-            ee = 1.0 / np.sqrt(np.maximum(rn, 1e-8))
+            # the kernel's clamp_norm: a (near-)zero row or column keeps scale 1
+            dd = 1.0 / np.sqrt(np.where(cn > 1e-6, np.minimum(cn, 1e6), 1.0))
+            ee = 1.0 / np.sqrt(np.where(rn > 1e-6, np.minimum(rn, 1e6), 1.0))
             P = dd[:, None] * P * dd[None, :]
             A = ee[:, None] * A * dd[None, :]
             D *= dd
