@@ -73,7 +73,7 @@ void free_all(piadmm_ctx* h) {
 
 int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
   if (c.n_agents <= 0) return fail(h, PIADMM_E_ARG, "n_agents must be > 0");
-  if (c.H < 3 || c.H > pd::HMAX) return fail(h, PIADMM_E_ARG, "H must be in [3, 32] in this version");
+  if (c.H < 3 || c.H > pd::HBIG) return fail(h, PIADMM_E_ARG, "H must be in [3, 63] in this version");
   if (c.max_outer <= 0) return fail(h, PIADMM_E_ARG, "max_outer must be > 0");
   if (c.dual_mode != PIADMM_DUAL_PLAIN && c.dual_mode != PIADMM_DUAL_PI)
     return fail(h, PIADMM_E_ARG, "dual_mode must be 0 (plain) or 1 (PI)");
@@ -93,8 +93,8 @@ int32_t piadmm_abi_version(void) { return PIADMM_ABI_VERSION; }
 
 const char* piadmm_build_info(void) {
   static char buf[160];
-  std::snprintf(buf, sizeof(buf), "libpiadmm abi=%d arch=gfx950 hip=%d.%d waves/wg=%d hmax=%d", PIADMM_ABI_VERSION,
-                HIP_VERSION_MAJOR, HIP_VERSION_MINOR, pd::NW, pd::HMAX);
+  std::snprintf(buf, sizeof(buf), "libpiadmm abi=%d arch=gfx950 hip=%d.%d waves/wg=%d hmax=%d (lds layout <= %d)",
+                PIADMM_ABI_VERSION, HIP_VERSION_MAJOR, HIP_VERSION_MINOR, pd::NW, pd::HBIG, pd::HMAX);
   return buf;
 }
 
@@ -225,8 +225,12 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.resid, C * h->cfg.max_outer * 2);
   rc |= dalloc(h, &A.status, (size_t)N + E);
   rc |= dalloc(h, &A.Pinv_x, (size_t)N * H * H);
-  rc |= dalloc(h, &A.sc_x, (size_t)N * 4 * pd::HMAX);
-  rc |= dalloc(h, &A.lab_x, (size_t)N * 2 * pd::HMAX);
+  rc |= dalloc(h, &A.sc_x, (size_t)N * 4 * pd::HCAP);
+  rc |= dalloc(h, &A.lab_x, (size_t)N * 2 * pd::HCAP);
+  const bool big = H > pd::HMAX;
+  rc |= dalloc(h, &A.Gx_g, big ? (size_t)N * (H * H + H) : 1);
+  rc |= dalloc(h, &A.XT_g, big ? (size_t)N * H1 * pd::XLDG : 1);
+  rc |= dalloc(h, &A.Ke_g, big ? E * 4 * H * H : 1);
   rc |= dalloc(h, &A.tab_e, E * 8 * H * H);
   rc |= dalloc(h, &A.warm_ok, (size_t)N);
   rc |= dalloc(h, &A.Sacc, E * 4 * H1);

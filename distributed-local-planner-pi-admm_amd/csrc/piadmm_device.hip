@@ -52,6 +52,13 @@ __device__ __forceinline__ void wsync() {
   asm volatile("" ::: "memory");
 }
 
+// Global-memory hand-off between lanes of one wave (big mode): wait for the stores, then
+// the wave barrier; all waves of the workgroup share the CU's vector L1.
+__device__ __forceinline__ void gsync() {
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+}
+
 // Broadcast lane k's value (k wave-uniform) through SGPRs.
 __device__ __forceinline__ double rdl(double v, int k) {
   unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -100,37 +107,46 @@ __device__ __forceinline__ double wmin(double v) {
 __device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
 __device__ __forceinline__ bool wall(bool p) { return __ballot(!p) == 0ull; }
 
-// Inclusive prefix / suffix sums over lanes 0..31 (H <= 32: every scanned vector lives there;
-// lanes 32..63 of the result are unspecified).  Four DPP row shifts inside each 16-lane row,
-// then one readlane to carry across the two rows.
+// DPP move restricted to the 16-lane rows in ROWS (other rows read 0).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dppd_rows(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b & 0xffffffffull), CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, ROWS, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// Inclusive prefix / suffix sums over the 64 lanes (time lanes 0..H, H <= 63).  Four DPP
+// row shifts inside each 16-lane row; the prefix carries across rows with the GFX9
+// row_bcast:15 / row_bcast:31 DPP broadcasts, the suffix with three readlanes.
 __device__ __forceinline__ double scan_incl(double v) {
   v += dppd<0x111>(v);   // row_shr:1
   v += dppd<0x112>(v);   // row_shr:2
   v += dppd<0x114>(v);   // row_shr:4
   v += dppd<0x118>(v);   // row_shr:8
-  const double c = rdl(v, 15);
-  const int l = lid();
-  return (l >= 16 && l < 32) ? v + c : v;
+  v += dppd_rows<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3
+  v += dppd_rows<0x143, 0xc>(v);   // row_bcast:31 -> rows 2, 3
+  return v;
 }
 __device__ __forceinline__ double scan_incl_rev(double v) {
   v += dppd<0x101>(v);   // row_shl:1
   v += dppd<0x102>(v);   // row_shl:2
   v += dppd<0x104>(v);   // row_shl:4
   v += dppd<0x108>(v);   // row_shl:8
-  const double c = rdl(v, 16);
-  return (lid() < 16) ? v + c : v;
+  const double r1 = rdl(v, 16), r2 = rdl(v, 32), r3 = rdl(v, 48);
+  const int l = lid();
+  const double c = (l < 16) ? r1 + (r2 + r3) : ((l < 32) ? r2 + r3 : ((l < 48) ? r3 : 0.0));
+  return v + c;
 }
 // T(t, j) = (t-1-j)+ is the rollout's double integrator (casadi/PI_ADMM_class.py:59-69:
 // theta accumulates u, x/y accumulate theta).  "hinge lane" k holds time t = k+1.
 // T_apply : var lanes u_j        -> hinge lanes (T u)_{k+1} = sum_{j<=k-1} (k-j) u_j
 // Tt_apply: hinge lanes w_k      -> var lanes   sum_{k>=j+1} (k-j) w_k
 __device__ __forceinline__ double T_apply(double u) {
-  const double r = scan_incl(scan_incl(u));
-  return shup(lid() < 32 ? r : 0.0, 1);
+  return shup(scan_incl(scan_incl(u)), 1);
 }
 __device__ __forceinline__ double Tt_apply(double w) {
-  const double r = scan_incl_rev(scan_incl_rev(w));
-  return shdn(lid() < 32 ? r : 0.0, 1);
+  return shdn(scan_incl_rev(scan_incl_rev(w)), 1);
 }
 
 // ============================================================ reference arithmetic
@@ -273,6 +289,47 @@ __device__ __forceinline__ void gj_invert(double* m, int n, int ld) {
   }
 }
 
+// Gauss-Jordan inverse of an SPD n x n matrix (64 < n <= 128), lane l owning columns l and
+// l + 64 (the pair's K beyond H = 32, in HBM in big mode: each pivot ends with a fence).
+// Same read-before-write ordering as gj_invert.
+__device__ __forceinline__ void gj_invert2(double* m, int n, int ld, bool global_mem) {
+  const int l = lid();
+  const int c1 = l + WAVE;
+  const bool own1 = c1 < n;
+  const int lc1 = own1 ? c1 : n - 1;
+  constexpr int U = 4;
+  for (int p = 0; p < n; ++p) {
+    const double ip = 1.0 / m[p * ld + p];
+    const double r0 = (l == p) ? ip : m[p * ld + l] * ip;
+    const double r1 = (c1 == p) ? ip : m[p * ld + lc1] * ip;
+    int i = 0;
+    for (; i + U <= n; i += U) {
+      double a[U], v0[U], v1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        a[u] = m[(i + u) * ld + p];
+        v0[u] = m[(i + u) * ld + l];
+        v1[u] = m[(i + u) * ld + lc1];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        m[(i + u) * ld + l] = (l == p) ? -a[u] * ip : v0[u] - a[u] * r0;
+        if (own1) m[(i + u) * ld + c1] = (c1 == p) ? -a[u] * ip : v1[u] - a[u] * r1;
+      }
+    }
+    for (; i < n; ++i) {
+      const double a = m[i * ld + p];
+      const double v0 = m[i * ld + l], v1 = m[i * ld + lc1];
+      m[i * ld + l] = (l == p) ? -a * ip : v0 - a * r0;
+      if (own1) m[i * ld + c1] = (c1 == p) ? -a * ip : v1 - a * r1;
+    }
+    m[p * ld + l] = r0;
+    if (own1) m[p * ld + c1] = r1;
+    if (global_mem) gsync();
+    else wsync();
+  }
+}
+
 __device__ __forceinline__ double clamp_norm(double v) {
   if (!(v > 1e-6)) return 1.0;
   return v > 1e6 ? 1e6 : v;
@@ -301,7 +358,9 @@ struct QP {
   const double* Pinv;     // n x n unscaled P^-1 (LDS for the x-step); for the pair the HBM
                           // table block DevArgs::tab_e: P^-1 | PGt (+4H^2) | GPG (+6H^2)
   double* vb;             // per-wave LDS vectors (512 doubles)
-  double* XT;             // x-step: per-wave LDS X' (H rows, stride XLD) and beta (row H)
+  double* XT;             // x-step: per-wave X' (H rows, stride xld) and beta (row H)
+  int xld;                // stride of XT (XLD in LDS mode, XLDG in big mode)
+  bool gmem;              // big mode: K / G / XT live in HBM (cross-lane reads need a fence)
   double* G;              // x-step: per-wave LDS G = P^-1 - Y X (H x H, stride H), g = Y beta (row H)
   double* fac;            // LDS factor region: L (lower), S (upper), stride fld
   double* fdiag;          // LDS [2*64]: S_aa, 1/L_aa of the cached factor
@@ -368,15 +427,22 @@ __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
   unsigned long long t_km = STAMP_T();
   const int l = lid();
   const int H = P.H, n = P.n;
-  const int vc = (NV == 2 && l >= H) ? 1 : 0;
-  const int jc = l - vc * H;
-  const bool incol = l < n;
-  const int src = (jc >= 0 && jc < H) ? jc : 0;
-  double Dsh[NV];
+  // lane l owns columns l and, for the pair beyond H = 32 (n > 64), l + 64
+  const int ncol = (n > WAVE) ? 2 : 1;
+  int vc[2], jc[2];
+  double Dc[2], gc[2];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) Dsh[v] = __shfl(P.D[v], src);
-  const double Dc = (NV == 2 && vc == 1) ? Dsh[NV - 1] : Dsh[0];
-  const double gc = (vc == 0) ? P.g1 : P.g2;
+  for (int cc = 0; cc < 2; ++cc) {
+    const int col = l + WAVE * cc;
+    vc[cc] = (NV == 2 && col >= H) ? 1 : 0;
+    jc[cc] = col - vc[cc] * H;
+    const int src = (jc[cc] >= 0 && jc[cc] < H) ? jc[cc] : 0;
+    double Dsh[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) Dsh[v] = __shfl(P.D[v], src);
+    Dc[cc] = (NV == 2 && vc[cc] == 1) ? Dsh[NV - 1] : Dsh[0];
+    gc[cc] = (vc[cc] == 0) ? P.g1 : P.g2;
+  }
   // hinge block of A_s'A_s: sum_{k > max(i,j)} e2_k (k-i)(k-j) = S2 - (i+j) S1 + i j S0 with
   // suffix sums S0..S2 of e2_k k^0..2 taken at lane max(i,j)+1 (one bpermute each per row)
   double hS0 = 0.0, hS1 = 0.0, hS2 = 0.0;
@@ -402,35 +468,42 @@ __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
       Err = rdl(P.E[1], ir);
       Errm = (ir >= 1) ? rdl(P.E[1], ir - 1) : 0.0;
     }
-    double hs = 0.0;
-    if constexpr (NV == 2) {
-      const double gr = (vr == 0) ? P.g1 : P.g2;
-      const int M = max(ir, jc) + 1;
-      const int ms = (M < H) ? M : 0;
-      const double s0 = __shfl(hS0, ms), s1 = __shfl(hS1, ms), s2 = __shfl(hS2, ms);
-      if (M < H) hs = s2 - (double)(ir + jc) * s1 + (double)ir * (double)jc * s0;
-      hs *= gr * gc * HINGE_RHO;
-    }
-    if (incol) {
-      double ata = hs, v = 0.0;
-      if (vr == vc) {
-        v = Dr * P_entry(P, vr, ir, jc) * Dc;
-        if (ir == jc) ata += Ebr * Ebr + Err * Err + Errm * Errm;
-        else if (jc == ir + 1) ata += -Err * Err;
-        else if (jc == ir - 1) ata += -Errm * Errm;
+    for (int cc = 0; cc < ncol; ++cc) {
+      const int col = l + WAVE * cc;
+      double hs = 0.0;
+      if constexpr (NV == 2) {
+        const double gr = (vr == 0) ? P.g1 : P.g2;
+        const int M = max(ir, jc[cc]) + 1;
+        const int ms = (M < H) ? M : 0;
+        const double s0 = __shfl(hS0, ms), s1 = __shfl(hS1, ms), s2 = __shfl(hS2, ms);
+        if (M < H) hs = s2 - (double)(ir + jc[cc]) * s1 + (double)ir * (double)jc[cc] * s0;
+        hs *= gr * gc[cc] * HINGE_RHO;
       }
-      v += P.rho * Dr * Dc * ata + (r == l ? P.sigma : 0.0);
-      m[r * ld + l] = v;
+      if (col < n) {
+        double ata = hs, v = 0.0;
+        if (vr == vc[cc]) {
+          v = Dr * P_entry(P, vr, ir, jc[cc]) * Dc[cc];
+          if (ir == jc[cc]) ata += Ebr * Ebr + Err * Err + Errm * Errm;
+          else if (jc[cc] == ir + 1) ata += -Err * Err;
+          else if (jc[cc] == ir - 1) ata += -Errm * Errm;
+        }
+        v += P.rho * Dr * Dc[cc] * ata + (r == col ? P.sigma : 0.0);
+        m[r * ld + col] = v;
+      }
     }
   }
   wsync();
   if (NV == 2) STAMP_ADD(ST_SZ_KMAT, t_km);
   unsigned long long t_gj = STAMP_T();
-  gj_invert(m, n, ld);
+  if (P.gmem && m == P.K) gsync();
+  if (ncol == 2) gj_invert2(m, n, ld, P.gmem && m == P.K);
+  else gj_invert(m, n, ld);
   if (NV == 2) STAMP_ADD(ST_SZ_GJ, t_gj);
-  for (int r = 0; r < n; ++r)
-    if (incol) P.K[r * n + l] = m[r * ld + l];
-  wsync();
+  if (m != P.K)
+    for (int r = 0; r < n; ++r)
+      if (l < n) P.K[r * n + l] = m[r * ld + l];
+  if (P.gmem) gsync();
+  else wsync();
 }
 template <int NV>
 __device__ __forceinline__ void A_mul(const QP<NV>& P, const double* x, double* ax) {
@@ -933,7 +1006,7 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   // right-hand sides, one per lane: lane i < H -> row i of Y = P^-1 A_W', lane H -> b
   const int li = (l <= H) ? l : H;
   const bool own = l <= H;
-  double* xr = XT + li * XLD;
+  double* xr = XT + li * P.xld;
   constexpr int XB = 4;
   for (int a0 = 0; a0 < m; a0 += XB) {
     int o[XB][2];
@@ -995,7 +1068,8 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
     acc *= P.fdiag[64 + a];
     if (own) xr[a] = acc;
   }
-  wsync();
+  if (P.gmem) gsync();
+  else wsync();
   STAMP_ADD(ST_XR_SOLVE, t_x);
   // G = P^-1 - Y X and g = Y beta (lane j = column j): Y is re-gathered column by column
   // into the factor scratch (the factor is not needed once X' is known), then every lane
@@ -1017,7 +1091,7 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
         if (a0 + u < m && l < H) fac[(a0 + u) * ld + l] = cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1];
     }
     wsync();
-    const double* xj = XT + lc * XLD;
+    const double* xj = XT + lc * P.xld;
     constexpr int GB = 8;
     for (int i0 = 0; i0 < H; i0 += GB) {
       double acc[GB], pv[GB];
@@ -1037,9 +1111,10 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
         if (l < H && i0 + u < H) P.G[(i0 + u) * H + l] = pv[u] - acc[u];
     }
     double gacc = 0.0;
-    for (int a = 0; a < m; ++a) gacc += fac[a * ld + lc] * XT[H * XLD + a];
+    for (int a = 0; a < m; ++a) gacc += fac[a * ld + lc] * XT[H * P.xld + a];
     if (l < H) P.G[H * H + l] = gacc;
-    wsync();
+    if (P.gmem) gsync();
+    else wsync();
   }
   return true;
 }
@@ -1099,7 +1174,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
         const int j = min(j0 + u, H - 1);
         qv[u] = (j0 + u < H) ? vb_q[j] : 0.0;
         gv[u] = G[j * H + lc];
-        xv[u] = XT[j * XLD + la];
+        xv[u] = XT[j * P.xld + la];
       }
 #pragma unroll
       for (int u = 0; u < GEMV_U; ++u) {
@@ -1107,7 +1182,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
         ax += xv[u] * qv[u];
       }
     }
-    if (l < m) vb_lam[l] = -ax - XT[H * XLD + l];
+    if (l < m) vb_lam[l] = -ax - XT[H * P.xld + l];
     ag = G[H * H + lc] - ag;
   }
   wsync();
@@ -1421,36 +1496,36 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
   P.mm[0] = g.mm;
   double* Kc = A.Kx_cache + (size_t)a * H * H;
   double* Pc = A.Pinv_x + (size_t)a * H * H;
-  double* sc = A.sc_x + (size_t)a * 4 * HMAX;
-  const int li = l < HMAX ? l : 0;
+  double* sc = A.sc_x + (size_t)a * 4 * HCAP;
+  const int li = l < HCAP ? l : 0;
   // P depends on the agent's speed only (make_geo): K_s^-1, P^-1 and the scaling are
   // cached in HBM per scenario and rebuilt only when the ADMM penalty differs.
   if (A.xcache_rho[a] == P.rho) {
     P.D[0] = in ? sc[li] : 0.0;
-    P.E[0] = in ? sc[HMAX + li] : 0.0;
-    P.E[1] = (l < H - 1) ? sc[2 * HMAX + li] : 0.0;
-    for (int i = 0; i < H; ++i) {
-      if (in) P.K[i * H + l] = Kc[i * H + l];
-    }
+    P.E[0] = in ? sc[HCAP + li] : 0.0;
+    P.E[1] = (l < H - 1) ? sc[2 * HCAP + li] : 0.0;
+    if (P.K != Kc)
+      for (int i = 0; i < H; ++i)
+        if (in) P.K[i * H + l] = Kc[i * H + l];
     wsync();
     return;
   }
   ruiz(P);
-  build_K(P, xfac, HMAX + 1);
+  build_K(P, xfac, P.fld);
   for (int i = 0; i < H; ++i)
-    if (in) xfac[i * (HMAX + 1) + l] = P_entry(P, 0, i, l);
+    if (in) xfac[i * P.fld + l] = P_entry(P, 0, i, l);
   wsync();
-  gj_invert(xfac, H, HMAX + 1);
+  gj_invert(xfac, H, P.fld);
   for (int i = 0; i < H; ++i) {
     if (in) {
-      Pc[i * H + l] = xfac[i * (HMAX + 1) + l];
-      Kc[i * H + l] = P.K[i * H + l];
+      Pc[i * H + l] = xfac[i * P.fld + l];
+      if (P.K != Kc) Kc[i * H + l] = P.K[i * H + l];
     }
   }
-  if (l < HMAX) {
-    sc[0 * HMAX + l] = P.D[0];
-    sc[1 * HMAX + l] = P.E[0];
-    sc[2 * HMAX + l] = P.E[1];
+  if (l < HCAP) {
+    sc[0 * HCAP + l] = P.D[0];
+    sc[1 * HCAP + l] = P.E[0];
+    sc[2 * HCAP + l] = P.E[1];
   }
   if (l == 0) A.xcache_rho[a] = P.rho;
   __threadfence();      // P^-1 (read back through L2 by the polish) is visible to this wave
@@ -1504,7 +1579,8 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
         if (in) acc1 += scr[l * LD + k];
         Y += acc1;
       }
-      wsync();
+      if (P.gmem) gsync();      // big mode: the staging is in HBM
+      else wsync();
     }
     double* Pg = Pi + 4 * H * H;
     double* Zg = Pi + 6 * H * H;
@@ -1518,9 +1594,9 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
       }
     }
     for (int k = 0; k < H; ++k)
-      if (l < n) Pg[k * n + l] = Yl[k * n + l];
+      for (int col = l; col < n; col += WAVE) Pg[k * n + col] = Yl[k * n + col];
     if (l == 0) A.ecache[e] = 1;
-    wsync();
+    gsync();                    // the tables are read back through L2 by the polish
   }
   STAMP_ADD(ST_SZ_PRE, t_pre);
   unsigned long long t_r = STAMP_T();
@@ -1563,13 +1639,22 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
   const int e = A.comp_edge[ci];
 
   // ---- LDS carve (lds_bytes() in piadmm_internal.h)
-  double* Kx = lds;                                      // 2 x H*H   agent K_s^-1
-  double* Gx = Kx + 2 * H * H;                           // 2 x (H*H+H) agent polish G | g
-  double* Ke = Gx + 2 * (H * H + H);                     // 4*H*H     pair K_s^-1
-  double* scr = Ke + 4 * H * H;                          // 64 x LD   pair scratch (wave 0)
-  double* xfac_all = scr + 64 * LD;                      // NW x HMAX x (HMAX+1)
-  double* xt_all = xfac_all + NW * HMAX * (HMAX + 1);    // NW x (HMAX+1) x XLD
-  double* vec_all = xt_all + NW * (HMAX + 1) * XLD;      // NW x 512
+  const bool big = H > HMAX;
+  double *Kx = nullptr, *Gx = nullptr, *Ke, *scr, *xfac_all, *xt_all = nullptr, *vec_all;
+  if (!big) {
+    Kx = lds;                                            // 2 x H*H   agent K_s^-1
+    Gx = Kx + 2 * H * H;                                 // 2 x (H*H+H) agent polish G | g
+    Ke = Gx + 2 * (H * H + H);                           // 4*H*H     pair K_s^-1
+    scr = Ke + 4 * H * H;                                // 64 x LD   pair scratch (wave 0)
+    xfac_all = scr + 64 * LD;                            // NW x HMAX x (HMAX+1)
+    xt_all = xfac_all + NW * HMAX * (HMAX + 1);          // NW x (HMAX+1) x XLD
+    vec_all = xt_all + NW * (HMAX + 1) * XLD;            // NW x 512
+  } else {
+    Ke = (e >= 0) ? A.Ke_g + (size_t)e * 4 * H * H : nullptr;   // HBM / L2
+    scr = lds;                                           // 64 x LD   pair scratch (wave 0)
+    xfac_all = scr + 64 * LD;                            // NW x 64 x LD
+    vec_all = xfac_all + NW * 64 * LD;                   // NW x 512
+  }
   double* fdiag_all = vec_all + NW * 512;                // NW x 256
   CompLds S;
   S.pos = fdiag_all + NW * 256;
@@ -1583,7 +1668,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
   S.last = S.D + 4 * H1;
   S.sc = S.last + 4 * H1;
   WaveMem wm{vec_all + w * 512, s_int + w * 272};
-  double* xfac = xfac_all + w * HMAX * (HMAX + 1);
+  double* xfac = big ? xfac_all + w * 64 * LD : xfac_all + w * HMAX * (HMAX + 1);
   double* xdiag = fdiag_all + w * 256;
   double* zdiag = xdiag + 128;
   int* xids = wm.ib;
@@ -1657,17 +1742,19 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
     gx = make_geo(S.xt + 3 * w, A.spd[a], c);
     affine_c(gx, c.dt, H, cx_own, cy_own);
     qp_common(c, H, A.rho_x[a], qx);
-    qx.K = Kx + w * H * H;
+    qx.K = big ? A.Kx_cache + (size_t)a * H * H : Kx + w * H * H;
     qx.Pinv = A.Pinv_x + (size_t)a * H * H;    // L2-resident; read only when W changes
-    qx.G = Gx + w * (H * H + H);
+    qx.G = big ? A.Gx_g + (size_t)a * (H * H + H) : Gx + w * (H * H + H);
     qx.vb = wm.vb;
     qx.fac = xfac;
-    qx.XT = xt_all + w * (HMAX + 1) * XLD;
+    qx.XT = big ? A.XT_g + (size_t)a * H1 * XLDG : xt_all + w * (HMAX + 1) * XLD;
+    qx.xld = big ? XLDG : XLD;
+    qx.gmem = big;
     qx.fdiag = xdiag;
     qx.ib = xids;
     qx.fstate = xfs;
-    qx.fld = HMAX + 1;
-    qx.mmax = HMAX;
+    qx.fld = big ? LD : HMAX + 1;
+    qx.mmax = big ? 64 : HMAX;
     nnb = A.nbr_cnt[a];
     setup_agent(A, a, qx, gx, xfac);
     // receding-horizon warm start: the previous step's final labels shifted by one time
@@ -1686,10 +1773,10 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
       warm_x = (A.cst[(size_t)ci * 4 + 2] >> w) & 1;
       status_x = A.status[a];
     } else if (A.warm_ok[a]) {
-      const signed char* lb = A.lab_x + (size_t)a * 2 * HMAX;
+      const signed char* lb = A.lab_x + (size_t)a * 2 * HCAP;
       const int src = min(l + 1, H - 1);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) lab_x[s] = (l < H) ? lb[s * HMAX + src] : 0;
+      for (int s = 0; s < 2; ++s) lab_x[s] = (l < H) ? lb[s * HCAP + src] : 0;
       warm_x = true;
     }
     STAMP_ADD(ST_SETUP_X, t0);
@@ -1727,6 +1814,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
     qe.fstate = zfs;
     qe.fld = LD;
     qe.mmax = WAVE;
+    qe.gmem = big;
+    qe.xld = 0;
     setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke, deff);
     if (!first) {
       const double* qs = A.qs_e + (size_t)e * 12 * WAVE;
@@ -1788,7 +1877,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int stx = qp_solve(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
-                               HMAX + 1, ustar, n_admm_x, n_pdas_x);
+                               qx.fld, ustar, n_admm_x, n_pdas_x);
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
       ++n_xqp;
@@ -1836,7 +1925,10 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
       qe.q[1] = (l < H) ? -c.rho * q2 : 0.0;
       double uh[2];
       unsigned long long t_zq = STAMP_T();
-      const int ste = qp_solve(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every, scr, LD, uh,
+      // K_s^-1 of the pair is built in the LDS scratch and copied (2H <= 64), or in place
+      // (big mode, two columns per lane, in HBM)
+      const int ste = qp_solve(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
+                               big ? Ke : scr, big ? 2 * H : LD, uh,
                                n_admm_z, n_pdas_z);
       STAMP_ADD(ST_ZQP, t_zq);
       status_e |= ste;
@@ -2012,10 +2104,10 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
         A.xt[3 * a + 2] = pth;
       }
       if (l == 0) A.warm_ok[a] = 1;
-      if (l < HMAX) {
-        signed char* lb = A.lab_x + (size_t)a * 2 * HMAX;
+      if (l < HCAP) {
+        signed char* lb = A.lab_x + (size_t)a * 2 * HCAP;
         lb[l] = lab_x[0];
-        lb[HMAX + l] = lab_x[1];
+        lb[HCAP + l] = lab_x[1];
       }
     }
   }

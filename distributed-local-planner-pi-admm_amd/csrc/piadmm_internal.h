@@ -6,9 +6,12 @@ namespace pd {
 
 constexpr int WAVE = 64;
 constexpr int NW = 2;        // waves per workgroup = agents per component (max)
-constexpr int HMAX = 32;     // horizon limit of this version: lane k <-> time index k
+constexpr int HCAP = 64;     // storage stride of per-lane state: lane k <-> time index k, H <= 63
+constexpr int HMAX = 32;     // largest H of the all-in-LDS layout ("LDS mode")
+constexpr int HBIG = 63;     // largest H supported (matrices in HBM / L2 beyond HMAX: "big mode")
 constexpr int LD = 65;       // odd LDS stride of the per-wave matrix scratch
-constexpr int XLD = HMAX + 1;  // odd LDS stride of the x-step parametric table X'
+constexpr int XLD = HMAX + 1;  // odd LDS stride of the x-step parametric table X' (LDS mode)
+constexpr int XLDG = 65;       // stride of X' in HBM (big mode: up to 64 working-set rows)
 constexpr int RUIZ_ITERS = 10;
 constexpr int PDAS_STEPS = 4;
 
@@ -39,8 +42,12 @@ struct DevArgs {
   int* status;              // N+E
   // per-step solver workspace
   double* Pinv_x;           // N*H*H
-  double* sc_x;             // N*4*HMAX   (D, Ebox, Erate, spare)
-  signed char* lab_x;       // N*2*HMAX   final x-step labels of the last step (next step's warm guess)
+  double* sc_x;             // N*4*HCAP   (D, Ebox, Erate, spare)
+  signed char* lab_x;       // N*2*HCAP   final x-step labels of the last step (next step's warm guess)
+  // big mode (H > HMAX): the matrices the LDS layout keeps per workgroup live in HBM / L2
+  double* Gx_g;             // N*(H*H+H)   x-step polish G | g
+  double* XT_g;             // N*(H+1)*XLDG  x-step X' | beta
+  double* Ke_g;             // E*4*H*H     pair K_s^-1
   double* tab_e;            // E * 8H^2 polish tables per edge, one block each:
                             //   [0, 4H^2) P^-1 (2H x 2H, block-diagonal), [4H^2, 6H^2) PGt (H x 2H,
                             //   row k = P_v^-1 T(k+1,.)'), [6H^2, 8H^2) GPG (Z_v = T P_v^-1 T')
@@ -67,14 +74,21 @@ struct DevArgs {
 };
 
 // LDS bytes needed by one workgroup for horizon H (must match the carve in k_mpc_step).
+// LDS mode (H <= HMAX): every matrix of the component in LDS.  Big mode: agent K_s^-1, G and
+// X' and the pair K_s^-1 in HBM / L2; LDS keeps the factor scratches and the vectors.
 inline size_t lds_bytes(int H) {
   size_t d = 0;
-  d += 2 * (size_t)H * H;          // agent K_s^-1 (2 agents)
-  d += 2 * ((size_t)H * H + H);    // agent polish G | g (2 agents)
-  d += 4 * (size_t)H * H;          // pair K_s^-1 (2H x 2H)
-  d += 64 * LD;                    // pair matrix scratch (wave 0)
-  d += NW * HMAX * (HMAX + 1);     // per-wave x-step scratch / Cholesky factor
-  d += NW * (HMAX + 1) * XLD;      // per-wave x-step parametric table X' | beta
+  if (H <= HMAX) {
+    d += 2 * (size_t)H * H;          // agent K_s^-1 (2 agents)
+    d += 2 * ((size_t)H * H + H);    // agent polish G | g (2 agents)
+    d += 4 * (size_t)H * H;          // pair K_s^-1 (2H x 2H)
+    d += 64 * LD;                    // pair matrix scratch (wave 0)
+    d += NW * HMAX * (HMAX + 1);     // per-wave x-step scratch / Cholesky factor
+    d += NW * (HMAX + 1) * XLD;      // per-wave x-step parametric table X' | beta
+  } else {
+    d += 64 * LD;                    // pair matrix scratch (wave 0)
+    d += NW * 64 * LD;               // per-wave x-step scratch / Cholesky factor (m <= 64)
+  }
   d += NW * 512;                   // per-wave vector buffers
   d += NW * 256;                   // per-wave factor diagonals (x, z)
   size_t H1 = H + 1;

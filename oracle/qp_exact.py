@@ -82,6 +82,7 @@ def solve(P, q, A, l, u, x0, tol=1e-12, max_iter=2000, W0=None):
             W.append((i, s))
 
     at_eqp_min = False
+    degenerate = False      # the last step had length 0: use Bland's rule to avoid cycling
     for _ in range(max_iter):
         rows = [r for r, _ in W]
         k = len(rows)
@@ -100,9 +101,14 @@ def solve(P, q, A, l, u, x0, tol=1e-12, max_iter=2000, W0=None):
         if at_eqp_min or np.max(np.abs(p), initial=0.0) <= 1e-13 * (1.0 + np.max(np.abs(x))):
             # stationary on the working set: check multiplier signs
             worst, wj = -1e-12 * (1.0 + np.max(np.abs(lam), initial=0.0)), -1
+            thr = worst
             for j, (r, s) in enumerate(W):
                 v = lam[j] * s
-                if v < worst:
+                if degenerate:
+                    # Bland: the wrong-signed row of lowest index
+                    if v < thr and (wj < 0 or r < W[wj][0]):
+                        wj = j
+                elif v < worst:
                     worst, wj = v, j
             if wj < 0:
                 # optimal working set: re-solve it directly for full accuracy
@@ -132,6 +138,7 @@ def solve(P, q, A, l, u, x0, tol=1e-12, max_iter=2000, W0=None):
         x = x + alpha * p
         if block is not None:
             W.append(block)
+        degenerate = block is not None and alpha <= 0.0
         at_eqp_min = block is None    # full step: x minimises the EQP of W
     raise QPError("active-set iteration limit")
 
