@@ -422,17 +422,18 @@ __device__ __forceinline__ double P_entry(const QP<NV>& P, int v, int i, int j) 
   return e;
 }
 
-template <int NV>
+// TWO: the pair beyond H = 32 (n > 64), lane l owning columns l and l + 64 (big mode only,
+// a separate instantiation so the LDS-mode kernel carries none of it).
+template <int NV, bool TWO>
 __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
   unsigned long long t_km = STAMP_T();
   const int l = lid();
   const int H = P.H, n = P.n;
-  // lane l owns columns l and, for the pair beyond H = 32 (n > 64), l + 64
-  const int ncol = (n > WAVE) ? 2 : 1;
-  int vc[2], jc[2];
-  double Dc[2], gc[2];
+  constexpr int ncol = TWO ? 2 : 1;
+  int vc[ncol], jc[ncol];
+  double Dc[ncol], gc[ncol];
 #pragma unroll
-  for (int cc = 0; cc < 2; ++cc) {
+  for (int cc = 0; cc < ncol; ++cc) {
     const int col = l + WAVE * cc;
     vc[cc] = (NV == 2 && col >= H) ? 1 : 0;
     jc[cc] = col - vc[cc] * H;
@@ -496,7 +497,7 @@ __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
   if (NV == 2) STAMP_ADD(ST_SZ_KMAT, t_km);
   unsigned long long t_gj = STAMP_T();
   if (P.gmem && m == P.K) gsync();
-  if (ncol == 2) gj_invert2(m, n, ld, P.gmem && m == P.K);
+  if constexpr (TWO) gj_invert2(m, n, ld, P.gmem && m == P.K);
   else gj_invert(m, n, ld);
   if (NV == 2) STAMP_ADD(ST_SZ_GJ, t_gj);
   if (m != P.K)
@@ -1323,7 +1324,7 @@ __device__ __forceinline__ double rho_ratio(const QP<NV>& P, const double* xs, c
 #define PIADMM_ADAPT_EVERY 25
 #endif
 constexpr int ADAPT_EVERY = PIADMM_ADAPT_EVERY;
-template <int NV>
+template <int NV, bool TWO>
 __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
                                         bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
                                         double* x_out, int& n_admm, int& n_pdas) {
@@ -1342,7 +1343,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
 #pragma unroll
   for (int s = 0; s < NR; ++s) plab[s] = -1;
   if (!ok && !P.kready) {
-    build_K(P, kscr, kld);
+    build_K<NV, TWO>(P, kscr, kld);
     P.kready = true;
     if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
     wsync();
@@ -1359,7 +1360,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       const double f = rho_ratio(P, xs, zs, ys);
       if (f != 1.0) {
         P.rho = fmin(fmax(P.rho * f, 1e-6), 1e6);
-        build_K(P, kscr, kld);
+        build_K<NV, TWO>(P, kscr, kld);
         if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
         wsync();
       }
@@ -1511,7 +1512,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
     return;
   }
   ruiz(P);
-  build_K(P, xfac, P.fld);
+  build_K<1, false>(P, xfac, P.fld);
   for (int i = 0; i < H; ++i)
     if (in) xfac[i * P.fld + l] = P_entry(P, 0, i, l);
   wsync();
@@ -1627,6 +1628,7 @@ __device__ __forceinline__ double delay_norm(const piadmm_config_t& c, double th
 // with the per-step state carried in HBM between launches (restore / save below) and the
 // stop decision taken by the host from all-reduced partials, then a LAST launch with no
 // iterations for the outputs and the propagation.
+template <bool BIG>
 __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it0, int it1, int flags) {
   extern __shared__ double lds[];
   __shared__ int s_int[NW * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
@@ -1639,7 +1641,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
   const int e = A.comp_edge[ci];
 
   // ---- LDS carve (lds_bytes() in piadmm_internal.h)
-  const bool big = H > HMAX;
+  constexpr bool big = BIG;      // H > HMAX (launch_mpc_step picks the instantiation)
   double *Kx = nullptr, *Gx = nullptr, *Ke, *scr, *xfac_all, *xt_all = nullptr, *vec_all;
   if (!big) {
     Kx = lds;                                            // 2 x H*H   agent K_s^-1
@@ -1876,7 +1878,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
-      const int stx = qp_solve(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n_admm_x, n_pdas_x);
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
@@ -1927,7 +1929,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
       unsigned long long t_zq = STAMP_T();
       // K_s^-1 of the pair is built in the LDS scratch and copied (2H <= 64), or in place
       // (big mode, two columns per lane, in HBM)
-      const int ste = qp_solve(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
+      const int ste = qp_solve<2, BIG>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
                                big ? Ke : scr, big ? 2 * H : LD, uh,
                                n_admm_z, n_pdas_z);
       STAMP_ADD(ST_ZQP, t_zq);
@@ -2203,7 +2205,8 @@ __global__ void k_pair_deff(DevArgs A) {
 
 int launch_mpc_step(const DevArgs& a, int t, int it0, int it1, int flags, hipStream_t s) {
   const size_t sh = lds_bytes(a.cfg.H);
-  static bool attr = false;
+  const bool big = a.cfg.H > HMAX;
+  static size_t attr[2] = {0, 0};     // dynamic LDS limit set so far per instantiation
 #ifdef PIADMM_STAMPS
   static unsigned long long* last = nullptr;
   if (a.stamps != last) {
@@ -2211,13 +2214,15 @@ int launch_mpc_step(const DevArgs& a, int t, int it0, int it1, int flags, hipStr
     last = a.stamps;
   }
 #endif
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)k_mpc_step, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sh) != hipSuccess)
-      return -1;
-    attr = true;
+  const void* fn = big ? (const void*)k_mpc_step<true> : (const void*)k_mpc_step<false>;
+  if (sh > attr[big]) {
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return -1;
+    attr[big] = sh;
   }
-  hipLaunchKernelGGL(k_mpc_step, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, it0, it1, flags);
+  if (big)
+    hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, it0, it1, flags);
+  else
+    hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, it0, it1, flags);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
