@@ -61,7 +61,12 @@ def algorithmic_bytes(cnt: dict, H: int) -> float:
     H1 = H + 1
     x_doubles = 3 + 1 + 2 * H1 + (2 * H1 + 2 * H1) + H + 2 * H1
     z_doubles = 4 * H1 + 4 * H1 + 6 + 4 + 4 * H1 + 12 * H1
-    return 8.0 * (cnt["x_qps"] * x_doubles + cnt["z_qps"] * z_doubles)
+    b = 8.0 * (cnt["x_qps"] * x_doubles + cnt["z_qps"] * z_doubles)
+    if H > 32:
+        # big mode: the polish tables G (H^2+H) and X' (<= H1 x H) of each x-step QP
+        # and the pair's K_s^-1 (4H^2) per pair ADMM iteration stream from L2 / HBM
+        b += 8.0 * (cnt["x_qps"] * (H * H + H + H1 * H) + cnt["admm_z"] * 4 * H * H)
+    return b
 
 
 def latest_traffic(workload: str):
@@ -79,7 +84,7 @@ def latest_traffic(workload: str):
     return None
 
 
-def cpu_baseline(n_tiles: int, budget_s: float) -> dict:
+def cpu_baseline(n_tiles: int, budget_s: float, H: int = H, tighten: int = 0) -> dict:
     """Time the NumPy oracle (the reference's loop structure, one QP at a time) on a bounded sample."""
     sys.path.insert(0, ROOT)
     from oracle import piadmm_oracle as O
@@ -87,7 +92,7 @@ def cpu_baseline(n_tiles: int, budget_s: float) -> dict:
         from threadpoolctl import threadpool_limits
     except ImportError:      # pragma: no cover
         threadpool_limits = None
-    cfg = config.matlab_pi(H=H, fixed_iters=1, max_outer=MAX_OUTER)
+    cfg = config.matlab_pi(H=H, fixed_iters=1, max_outer=MAX_OUTER, tighten=tighten)
     scn = scenario.tiled(N_TILES, H, n_steps=4)
     done_tiles = 0
     t_used = 0.0
@@ -123,7 +128,11 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle timing (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--natural", action="store_true", help="natural (global) termination, not the headline")
+    ap.add_argument("--config5", action="store_true",
+                    help="BASELINE configs[4]: H=50 with delay tightening (not the headline)")
     args = ap.parse_args()
+    H = 50 if args.config5 else globals()["H"]
+    tighten = 1 if args.config5 else 0
 
     lib = _lib.load()                       # HIP runtime loaded before torch (same SONAME)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,7 +147,8 @@ def main():
     from piadmm.solver import PI_ADMM_MI355X
     K, W = args.steps, args.warmup
     n_steps = max(K, W, 1)
-    cfg = config.matlab_pi(H=H, fixed_iters=0 if args.natural else 1, max_outer=MAX_OUTER, term_global=1)
+    cfg = config.matlab_pi(H=H, fixed_iters=0 if args.natural else 1, max_outer=MAX_OUTER, term_global=1,
+                           tighten=tighten)
     scn = scenario.tiled(N_TILES, H, n_steps=n_steps, perturb=True, seed=1000 * rank)
     solver = PI_ADMM_MI355X(cfg, scn, device=local_rank)
     if dist is not None:
@@ -198,6 +208,7 @@ def main():
         "data": "synthetic: 128 seeded tiles of the reference 2-vehicle intersection per GPU",
         "config": {
             "workload": f"256 agents x H{H} per GPU (128 tiles), matlab_pi preset (PI anti-windup), "
+                        + ("delay tightening p=0.95 (configs[4]), " if tighten else "")
                         + (f"global natural termination (max {MAX_OUTER} outer iterations)" if args.natural else
                            f"{MAX_OUTER} outer iterations per MPC step (fixed), global residual history"),
             "agents_per_gpu": 2 * N_TILES, "horizon": H,
@@ -224,7 +235,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(N_TILES, args.cpu_budget)
+        line["cpu_baseline"] = cpu_baseline(N_TILES, args.cpu_budget, H, tighten)
         line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
     solver.close()
     if rank == 0:
