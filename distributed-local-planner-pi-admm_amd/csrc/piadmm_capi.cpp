@@ -266,7 +266,11 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
     HIPCHK(h, hipMemcpyAsync(A.rho_x, r0.data(), (size_t)N * sizeof(double), hipMemcpyHostToDevice, h->stream));
     // (pair QPs keep this penalty: no adaptation, and on the GPU smaller fixed penalties cost
     // more ADMM iterations on the bench's pair QPs -- 0.5x: +0%, 0.2x: +39%, 0.1x: +114% time)
-    if (E) HIPCHK(h, hipMemcpyAsync(A.rho_e, r0.data(), E * sizeof(double), hipMemcpyHostToDevice, h->stream));
+#ifndef PIADMM_PAIR_RHO_SCALE
+#define PIADMM_PAIR_RHO_SCALE 1.0
+#endif
+    std::vector<double> r1((size_t)std::max<size_t>(E, 1), h->cfg.admm_rho * PIADMM_PAIR_RHO_SCALE);
+    if (E) HIPCHK(h, hipMemcpyAsync(A.rho_e, r1.data(), E * sizeof(double), hipMemcpyHostToDevice, h->stream));
   }
   HIPCHK(h, hipMemsetAsync(A.xcache_rho, 0xff, (size_t)N * sizeof(double), h->stream));   // NaN: no cache
   HIPCHK(h, hipStreamSynchronize(h->stream));

@@ -1,0 +1,67 @@
+"""Run records (piadmm.io): the reference driver's outputs as files.  CPU: recorder, npz/json
+round trip, the reference's progress line and figure.  GPU: the CLI end to end."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import piadmm_oracle as O
+from piadmm import config, io, scenario
+
+
+def _oracle_record(n=6):
+    cfg = config.casadi_default(H=10)
+    orc = O.Oracle(cfg, scenario.intersection(10))
+    rec = io.RunRecorder(meta={"preset": "casadi_default", "H": 10})
+    for _ in range(n):
+        r = orc.mpc_step()
+        resid = np.full((orc.n_comp, cfg.max_outer, 2), np.nan)
+        for c, rr in enumerate(r.resid):
+            if rr:
+                resid[c, :len(rr)] = rr
+        rec.add(r.xt, r.u, r.iters, resid, r.lam)
+    return rec.record(), cfg
+
+
+def test_record_round_trip(tmp_path):
+    run, _ = _oracle_record()
+    npz, js = io.save_run(str(tmp_path / "run"), run)
+    assert os.path.exists(npz) and os.path.exists(js)
+    back = io.load_run(str(tmp_path / "run"))
+    for f in ("x_vec", "theta_vec", "u_vec", "iter_his", "dual_max", "dual_min"):
+        np.testing.assert_array_equal(getattr(back, f), getattr(run, f))
+    np.testing.assert_array_equal(np.isnan(back.resid), np.isnan(run.resid))
+    assert back.meta == {"preset": "casadi_default", "H": 10}
+    assert run.x_vec.shape == (6, 2, 2) and run.u_vec.shape == (6, 2)
+
+
+def test_step_line_is_the_reference_format():
+    """casadi/main.py:193-196."""
+    xt = np.array([[1.5, 0.0, 0.0], [0.0, 2.5, -1.0]])
+    line = io.step_line(3, np.array([7]), 0.25, -0.5, 2.0, xt)
+    want = ("t_step: {}, iter: {}, max dual: {}, min dual: {}, rho: {}, veh_x: {}, veh_y: {}"
+            .format(4, 7, 0.25, -0.5, 2.0, xt[:, 0], xt[:, 1]))
+    assert line == want
+
+
+def test_plot_writes_the_trajectory_scatter(tmp_path):
+    pytest.importorskip("matplotlib")
+    run, _ = _oracle_record(4)
+    p = io.plot_run(run, str(tmp_path / "traj.png"))
+    assert os.path.getsize(p) > 1000
+
+
+@pytest.mark.gpu
+def test_cli_run_matches_oracle(tmp_path):
+    from piadmm import run as cli
+    from piadmm.solver import device_count
+    if device_count() < 1:
+        pytest.fail("no HIP device visible")
+    out = str(tmp_path / "cli")
+    assert cli.main(["--preset", "casadi_default", "--H", "10", "--steps", "6", "--out", out,
+                     "--plot", out + ".png", "--quiet"]) == 0
+    got = io.load_run(out)
+    want, _ = _oracle_record(6)
+    np.testing.assert_allclose(got.x_vec, want.x_vec, rtol=1e-8, atol=1e-8)
+    np.testing.assert_array_equal(got.iter_his, want.iter_his)
+    assert os.path.getsize(out + ".png") > 1000
