@@ -82,6 +82,10 @@ int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
   if (c.max_inner <= 0 || c.polish_every <= 0) return fail(h, PIADMM_E_ARG, "max_inner, polish_every must be > 0");
   if (c.round_decimals > 12) return fail(h, PIADMM_E_ARG, "round_decimals must be <= 12");
   if (c.tighten && !(c.tight_p > 0 && c.tight_p < 1)) return fail(h, PIADMM_E_ARG, "tight_p must be in (0, 1)");
+  if (c.precision != 0 && c.precision != 1) return fail(h, PIADMM_E_ARG, "precision must be 0 (fp64) or 1 (fp32 ADMM matrices)");
+  if (pd::lds_bytes(c.H, c.precision) + pd::STATIC_LDS > pd::MAX_LDS)
+    return fail(h, PIADMM_E_ARG, "the workgroup's LDS exceeds 160 KB (precision 1 keeps the pair's fp32 "
+                                  "K_s^-1 in LDS: H <= 55 in big mode)");
   return 0;
 }
 

@@ -355,6 +355,8 @@ struct QP {
   double Pcost2;          // 2 Pcost
   double beta, rho, sigma, alpha, tol;
   double* K;              // LDS  n x n  scaled (P_s + sigma I + rho A_s'A_s)^-1
+  float* Kf;              // precision 1: the same matrix in fp32 (what the ADMM iteration reads)
+  bool kf32;              // ADMM reads Kf (the polish and its certificate stay fp64)
   const double* Pinv;     // n x n unscaled P^-1 (LDS for the x-step); for the pair the HBM
                           // table block DevArgs::tab_e: P^-1 | PGt (+4H^2) | GPG (+6H^2)
   double* vb;             // per-wave LDS vectors (512 doubles)
@@ -425,7 +427,7 @@ __device__ __forceinline__ double P_entry(const QP<NV>& P, int v, int i, int j) 
 // TWO: the pair beyond H = 32 (n > 64), lane l owning columns l and l + 64 (big mode only,
 // a separate instantiation so the LDS-mode kernel carries none of it).
 template <int NV, bool TWO>
-__device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
+__device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld, double* kcache = nullptr) {
   unsigned long long t_km = STAMP_T();
   const int l = lid();
   const int H = P.H, n = P.n;
@@ -500,10 +502,17 @@ __device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld) {
   if constexpr (TWO) gj_invert2(m, n, ld, P.gmem && m == P.K);
   else gj_invert(m, n, ld);
   if (NV == 2) STAMP_ADD(ST_SZ_GJ, t_gj);
-  if (m != P.K)
-    for (int r = 0; r < n; ++r)
-      if (l < n) P.K[r * n + l] = m[r * ld + l];
-  if (P.gmem) gsync();
+  // copies: the fp64 matrix (unless built in place), its fp32 image (precision 1) and the
+  // per-scenario HBM cache (x-step); lane = column, up to two columns per lane
+  for (int col = l; col < n; col += WAVE) {
+    for (int r = 0; r < n; ++r) {
+      const double v = m[r * ld + col];
+      if (P.kf32) P.Kf[r * n + col] = (float)v;
+      else if (m != P.K) P.K[r * n + col] = v;
+      if (kcache) kcache[r * n + col] = v;
+    }
+  }
+  if (P.gmem || kcache) gsync();
   else wsync();
 }
 template <int NV>
@@ -630,7 +639,8 @@ __device__ __forceinline__ void admm_iter(const QP<NV>& P, double* xs, double* z
   At_mul(P, w, t);
 #pragma unroll
   for (int v = 0; v < NV; ++v) rhs[v] = P.sigma * xs[v] - P.D[v] * P.q[v] + P.D[v] * t[v];
-  gemv_sym<false>(P, P.K, rhs, xt);
+  if (P.kf32) gemv_sym<false>(P, P.Kf, rhs, xt);     // fp32 storage, fp64 accumulation
+  else gemv_sym<false>(P, P.K, rhs, xt);
 #pragma unroll
   for (int v = 0; v < NV; ++v) xu[v] = P.D[v] * xt[v];
   A_mul(P, xu, a);
@@ -1505,14 +1515,18 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
     P.D[0] = in ? sc[li] : 0.0;
     P.E[0] = in ? sc[HCAP + li] : 0.0;
     P.E[1] = (l < H - 1) ? sc[2 * HCAP + li] : 0.0;
-    if (P.K != Kc)
+    if (P.kf32) {
+      for (int i = 0; i < H; ++i)
+        if (in) P.Kf[i * H + l] = (float)Kc[i * H + l];
+    } else if (P.K != Kc) {
       for (int i = 0; i < H; ++i)
         if (in) P.K[i * H + l] = Kc[i * H + l];
+    }
     wsync();
     return;
   }
   ruiz(P);
-  build_K<1, false>(P, xfac, P.fld);
+  build_K<1, false>(P, xfac, P.fld, Kc);
   for (int i = 0; i < H; ++i)
     if (in) xfac[i * P.fld + l] = P_entry(P, 0, i, l);
   wsync();
@@ -1520,7 +1534,6 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
   for (int i = 0; i < H; ++i) {
     if (in) {
       Pc[i * H + l] = xfac[i * P.fld + l];
-      if (P.K != Kc) Kc[i * H + l] = P.K[i * H + l];
     }
   }
   if (l < HCAP) {
@@ -1642,20 +1655,26 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
 
   // ---- LDS carve (lds_bytes() in piadmm_internal.h)
   constexpr bool big = BIG;      // H > HMAX (launch_mpc_step picks the instantiation)
-  double *Kx = nullptr, *Gx = nullptr, *Ke, *scr, *xfac_all, *xt_all = nullptr, *vec_all;
+  const bool f32 = c.precision == 1;   // ADMM matrices in fp32 (lds_bytes: half the space)
+  double *Kx = nullptr, *Gx = nullptr, *Ke = nullptr, *scr, *xfac_all, *xt_all = nullptr, *vec_all;
+  float* Kef = nullptr;
+  float* Kxf = nullptr;
   if (!big) {
-    Kx = lds;                                            // 2 x H*H   agent K_s^-1
-    Gx = Kx + 2 * H * H;                                 // 2 x (H*H+H) agent polish G | g
-    Ke = Gx + 2 * (H * H + H);                           // 4*H*H     pair K_s^-1
-    scr = Ke + 4 * H * H;                                // 64 x LD   pair scratch (wave 0)
+    double* p = lds;
+    if (f32) { Kxf = (float*)p; p += H * H; }            // 2 x H*H fp32 agent K_s^-1
+    else { Kx = p; p += 2 * H * H; }                     // 2 x H*H   agent K_s^-1
+    Gx = p; p += 2 * (H * H + H);                        // 2 x (H*H+H) agent polish G | g
+    if (f32) { Kef = (float*)p; p += 2 * H * H; }        // 4*H*H fp32 pair K_s^-1
+    else { Ke = p; p += 4 * H * H; }                     // 4*H*H     pair K_s^-1
+    scr = p;                                             // 64 x LD   pair scratch (wave 0)
     xfac_all = scr + 64 * LD;                            // NW x HMAX x (HMAX+1)
     xt_all = xfac_all + NW * HMAX * (HMAX + 1);          // NW x (HMAX+1) x XLD
     vec_all = xt_all + NW * (HMAX + 1) * XLD;            // NW x 512
   } else {
-    Ke = (e >= 0) ? A.Ke_g + (size_t)e * 4 * H * H : nullptr;   // HBM / L2
+    Ke = (e >= 0) ? A.Ke_g + (size_t)e * 4 * H * H : nullptr;   // HBM / L2 (built in place)
     scr = lds;                                           // 64 x LD   pair scratch (wave 0)
-    xfac_all = scr + 64 * LD;                            // NW x 64 x LD
-    vec_all = xfac_all + NW * 64 * LD;                   // NW x 512
+    xfac_all = scr + 64 * LD;                            // NW x xrows(H) x (xrows+1)
+    vec_all = xfac_all + NW * xrows(H) * (xrows(H) + 1); // NW x 512
   }
   double* fdiag_all = vec_all + NW * 512;                // NW x 256
   CompLds S;
@@ -1669,8 +1688,9 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
   S.D = S.S + 4 * H1;
   S.last = S.D + 4 * H1;
   S.sc = S.last + 4 * H1;
+  if (big && f32) Kef = (float*)(S.sc + 32);             // big mode: fp32 image of the pair K_s^-1
   WaveMem wm{vec_all + w * 512, s_int + w * 272};
-  double* xfac = big ? xfac_all + w * 64 * LD : xfac_all + w * HMAX * (HMAX + 1);
+  double* xfac = big ? xfac_all + w * xrows(H) * (xrows(H) + 1) : xfac_all + w * HMAX * (HMAX + 1);
   double* xdiag = fdiag_all + w * 256;
   double* zdiag = xdiag + 128;
   int* xids = wm.ib;
@@ -1744,7 +1764,9 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
     gx = make_geo(S.xt + 3 * w, A.spd[a], c);
     affine_c(gx, c.dt, H, cx_own, cy_own);
     qp_common(c, H, A.rho_x[a], qx);
-    qx.K = big ? A.Kx_cache + (size_t)a * H * H : Kx + w * H * H;
+    qx.K = big ? A.Kx_cache + (size_t)a * H * H : (Kx ? Kx + w * H * H : nullptr);
+    qx.Kf = (!big && f32) ? Kxf + w * H * H : nullptr;
+    qx.kf32 = !big && f32;                        // big mode: the x-step K stays fp64 in HBM
     qx.Pinv = A.Pinv_x + (size_t)a * H * H;    // L2-resident; read only when W changes
     qx.G = big ? A.Gx_g + (size_t)a * (H * H + H) : Gx + w * (H * H + H);
     qx.vb = wm.vb;
@@ -1755,8 +1777,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
     qx.fdiag = xdiag;
     qx.ib = xids;
     qx.fstate = xfs;
-    qx.fld = big ? LD : HMAX + 1;
-    qx.mmax = big ? 64 : HMAX;
+    qx.fld = big ? xrows(H) + 1 : HMAX + 1;
+    qx.mmax = big ? xrows(H) : HMAX;
     nnb = A.nbr_cnt[a];
     setup_agent(A, a, qx, gx, xfac);
     // receding-horizon warm start: the previous step's final labels shifted by one time
@@ -1808,6 +1830,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
     qe.alpha = c.admm_alpha;
     qe.tol = c.qp_tol;
     qe.K = Ke;
+    qe.Kf = Kef;
+    qe.kf32 = f32;
     qe.Pinv = A.tab_e + (size_t)e * 8 * H * H;
     qe.vb = wm.vb;
     qe.fac = scr;
@@ -1818,7 +1842,9 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
     qe.mmax = WAVE;
     qe.gmem = big;
     qe.xld = 0;
-    setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke, deff);
+    // Ke doubles as the H x 2H staging of the per-scenario pair tables; with fp32 images in
+    // LDS mode the fp32 region (2H^2 doubles of space) takes that role
+    setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke ? Ke : (double*)Kef, deff);
     if (!first) {
       const double* qs = A.qs_e + (size_t)e * 12 * WAVE;
       const signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
@@ -2084,7 +2110,11 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
     }
     if (A.xcache_rho[a] != qx.rho) {       // adaptive rho rebuilt K_s^-1 in LDS: refresh the cache
       double* Kc = A.Kx_cache + (size_t)a * H * H;
-      for (int i = l; i < H * H; i += WAVE) Kc[i] = qx.K[i];
+      if (qx.kf32) {
+        for (int i = l; i < H * H; i += WAVE) Kc[i] = (double)qx.Kf[i];   // the fp32 image
+      } else if (qx.K != Kc) {
+        for (int i = l; i < H * H; i += WAVE) Kc[i] = qx.K[i];
+      }
       if (l == 0) A.xcache_rho[a] = qx.rho;
     }
     if (!last_launch) {
@@ -2204,7 +2234,7 @@ __global__ void k_pair_deff(DevArgs A) {
 }
 
 int launch_mpc_step(const DevArgs& a, int t, int it0, int it1, int flags, hipStream_t s) {
-  const size_t sh = lds_bytes(a.cfg.H);
+  const size_t sh = lds_bytes(a.cfg.H, a.cfg.precision);
   const bool big = a.cfg.H > HMAX;
   static size_t attr[2] = {0, 0};     // dynamic LDS limit set so far per instantiation
 #ifdef PIADMM_STAMPS

@@ -73,21 +73,29 @@ struct DevArgs {
   int* ecache;              // E   1 when the pair's speed-only tables are built
 };
 
+// Big mode: rows of the per-wave x-step factor scratch (working sets of up to H + 2 rows:
+// a degenerate vertex can hold one or two dependent rows beyond the H variables).
+constexpr int xrows(int H) { return H + 2 < 64 ? H + 2 : 64; }
+// LDS the kernel declares statically (s_int, s_cnt, s_warm) on top of lds_bytes().
+constexpr size_t STATIC_LDS = NW * 272 * 4 + NW * 8 * 4 + 16;
+constexpr size_t MAX_LDS = 160 * 1024;
+
 // LDS bytes needed by one workgroup for horizon H (must match the carve in k_mpc_step).
 // LDS mode (H <= HMAX): every matrix of the component in LDS.  Big mode: agent K_s^-1, G and
 // X' and the pair K_s^-1 in HBM / L2; LDS keeps the factor scratches and the vectors.
-inline size_t lds_bytes(int H) {
+inline size_t lds_bytes(int H, int precision = 0) {
   size_t d = 0;
+  const bool f32 = precision == 1;
   if (H <= HMAX) {
-    d += 2 * (size_t)H * H;          // agent K_s^-1 (2 agents)
+    d += (f32 ? 1 : 2) * (size_t)H * H;   // agent K_s^-1 (2 agents; fp32: half)
     d += 2 * ((size_t)H * H + H);    // agent polish G | g (2 agents)
-    d += 4 * (size_t)H * H;          // pair K_s^-1 (2H x 2H)
+    d += (f32 ? 2 : 4) * (size_t)H * H;   // pair K_s^-1 (2H x 2H)
     d += 64 * LD;                    // pair matrix scratch (wave 0)
     d += NW * HMAX * (HMAX + 1);     // per-wave x-step scratch / Cholesky factor
     d += NW * (HMAX + 1) * XLD;      // per-wave x-step parametric table X' | beta
   } else {
     d += 64 * LD;                    // pair matrix scratch (wave 0)
-    d += NW * 64 * LD;               // per-wave x-step scratch / Cholesky factor (m <= 64)
+    d += NW * (size_t)xrows(H) * (xrows(H) + 1);   // per-wave x-step scratch / Cholesky factor
   }
   d += NW * 512;                   // per-wave vector buffers
   d += NW * 256;                   // per-wave factor diagonals (x, z)
@@ -96,6 +104,7 @@ inline size_t lds_bytes(int H) {
   d += 2 * 3 + 2 * 2 + 2 * H;      // xt, seeds, u
   d += 5 * 2 * 2 * H1;             // hat, lam, S, D, last_hat
   d += 32;                         // scalars
+  if (H > HMAX && f32) d += 2 * (size_t)H * H + 2;   // big mode: fp32 image of the pair K_s^-1
   return d * sizeof(double);
 }
 

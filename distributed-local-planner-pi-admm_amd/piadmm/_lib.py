@@ -31,7 +31,7 @@ class PiadmmConfigC(ctypes.Structure):
         ("fixed_iters", c_i32), ("max_inner", c_i32),
         ("admm_rho", c_dbl), ("admm_sigma", c_dbl), ("admm_alpha", c_dbl), ("qp_tol", c_dbl),
         ("polish_every", c_i32), ("device", c_i32),
-        ("term_global", c_i32), ("warm_duals", c_i32), ("tighten", c_i32), ("reserved0", c_i32),
+        ("term_global", c_i32), ("warm_duals", c_i32), ("tighten", c_i32), ("precision", c_i32),
         ("tight_p", c_dbl), ("avg_delay", c_dbl), ("var_delay", c_dbl),
     ]
 
@@ -43,8 +43,6 @@ def to_c(cfg: PIADMMConfig, n_agents: int, device: int = 0) -> PiadmmConfigC:
             c.n_agents = int(n_agents)
         elif name == "device":
             c.device = int(device)
-        elif name == "reserved0":
-            c.reserved0 = 0
         else:
             setattr(c, name, getattr(cfg, name))
     return c

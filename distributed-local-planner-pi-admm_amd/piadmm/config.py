@@ -65,6 +65,8 @@ class PIADMMConfig:
     tight_p: float = 0.95       # VehicleConfig.prob       (veh_config.py:27)
     avg_delay: float = 0.05     # VehicleConfig.avg_delay  (veh_config.py:25)
     var_delay: float = 0.025    # VehicleConfig.var_delay  (veh_config.py:26)
+    precision: int = 0          # 1: ADMM matrices K_s^-1 in fp32 (mixed precision; the polish and its
+                                #    certificate stay fp64, so answers do not change) -- configs[4] study
     # --- inner QP solver (build's own; not in the reference) ---
     admm_rho: float = 0.05      # ADMM penalty in the Ruiz-scaled space (tools/qp_sim.py sweep)
     admm_sigma: float = 1e-6

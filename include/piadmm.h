@@ -82,7 +82,8 @@ typedef struct piadmm_config {
                                 (iterate_next_state, Distributed_planner/decentralized/optimizer.py:337-344) */
   int32_t tighten;           /* 1: delay-tightened safety distance d_eff = dis_thres + |delta_i| + |delta_j|
                                 (compute_square_halfspaces_ca_prob, decentralized/util.py:70-101) */
-  int32_t reserved0;
+  int32_t precision;         /* 0: fp64; 1: ADMM iteration matrices K_s^-1 stored fp32 (half the LDS),
+                                polish and certificate fp64 -- answers unchanged (configs[4] study) */
   double tight_p, avg_delay, var_delay;   /* VehicleConfig prob / avg_delay / var_delay (veh_config.py:25-27) */
 } piadmm_config_t;
 

@@ -42,7 +42,7 @@ def test_config_struct_layout():
     c = _lib.to_c(config.matlab_pi(H=30), n_agents=256, device=3)
     assert (c.n_agents, c.H, c.device, c.dual_mode, c.windup) == (256, 30, 3, 1, 1)
     # every dataclass field the struct carries is mirrored
-    fields = {f for f, _ in _lib.PiadmmConfigC._fields_} - {"n_agents", "device", "reserved0"}
+    fields = {f for f, _ in _lib.PiadmmConfigC._fields_} - {"n_agents", "device"}
     assert fields <= set(config.PIADMMConfig.__dataclass_fields__)
 
 

@@ -88,3 +88,11 @@ def test_rccl_single_rank_communicator(Solver):
             setup=lambda s: s.comm_init(uid, 1, 0))
     compare(Solver, config.matlab_pi(H=12, fixed_iters=1, max_outer=6, term_global=1),
             scenario.tiled(2, 12, n_steps=10, seed=1), 3, setup=lambda s: s.comm_init(comm_unique_id(), 1, 0))
+
+
+@pytest.mark.parametrize("H,n", [(10, 12), (30, 6), (50, 3)])
+def test_fp32_admm_matrices_keep_answers(Solver, H, n):
+    """precision 1 (configs[4] study): the ADMM iterations read fp32 K_s^-1 images, the polish
+    and its KKT certificate stay fp64 -- every QP certified, answers equal the oracle's."""
+    compare(Solver, config.matlab_pi(H=H, precision=1, tighten=int(H == 50)),
+            scenario.tiled(2, H, n_steps=12, seed=H + 1), n)
