@@ -187,8 +187,13 @@ def main():
 
     outer_total = world * cnt["outer_iters"] / max(solver.C, 1)      # job iterations x ranks
     value = outer_total / wall
-    avg_launch_s = (ev_ms / 1e3) / K
-    bytes_launch = algorithmic_bytes(cnt, H) / K
+    # k_mpc_step launches in the timed region: one persistent launch per steps_per_launch()
+    # MPC steps (fixed iterations), or one per outer iteration plus one per step (natural
+    # global termination, where each launch's share of the device time is taken as equal)
+    spl = solver.steps_per_launch()
+    n_launch = -(-K // spl) if not args.natural else int(cnt["outer_iters"] / max(solver.C, 1)) + K
+    avg_launch_s = (ev_ms / 1e3) / n_launch
+    bytes_launch = algorithmic_bytes(cnt, H) / n_launch
     achieved = bytes_launch / avg_launch_s / 1e9
 
     traffic = latest_traffic(f"tiled{N_TILES}_H{H}_matlab_pi_fixed{MAX_OUTER}")
@@ -221,6 +226,7 @@ def main():
             "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
             "kernel": "pd::k_mpc_step", "avg_launch_ms": avg_launch_s * 1e3,
+            "steps_per_launch": spl if not args.natural else None, "launches": n_launch,
             "algorithmic_bytes_per_launch": bytes_launch,
             "note": "latency-bound: one dependent ADMM/PDAS chain per wave; see DESIGN.md",
         },

@@ -32,6 +32,7 @@ struct piadmm_ctx {
   double* h_part = nullptr;      // pinned
   std::vector<double> ghist;     // global (rk, sk) history of the last step
   int giters = 0;
+  int step_cap = 1;              // MPC steps per persistent launch (resid slots)
 };
 
 namespace {
@@ -226,7 +227,13 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.lam, E * 4 * H1);
   rc |= dalloc(h, &A.edge_active, E);
   rc |= dalloc(h, &A.iters, C);
-  rc |= dalloc(h, &A.resid, C * h->cfg.max_outer * 2);
+  // one residual-history slot per step of a persistent multi-step launch (<= 32 steps,
+  // <= 64 MB of history per launch)
+  {
+    const size_t per_step = (size_t)C * std::max(h->cfg.max_outer, 1) * 2 * sizeof(double);
+    h->step_cap = (int)std::max<size_t>(1, std::min<size_t>(32, ((size_t)64 << 20) / per_step));
+  }
+  rc |= dalloc(h, &A.resid, (size_t)h->step_cap * C * h->cfg.max_outer * 2);
   rc |= dalloc(h, &A.status, (size_t)N + E);
   rc |= dalloc(h, &A.Pinv_x, (size_t)N * H * H);
   rc |= dalloc(h, &A.sc_x, (size_t)N * 4 * pd::HCAP);
@@ -247,7 +254,7 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.qs_e, E * 12 * pd::WAVE);
   rc |= dalloc(h, &A.ql_e, E * 5 * pd::WAVE);
   rc |= dalloc(h, &A.cst, C * 4);
-  rc |= dalloc(h, &h->d_part, (size_t)h->cfg.max_outer * 5);
+  rc |= dalloc(h, &h->d_part, (size_t)h->cfg.max_outer * std::max(5, 2 * h->step_cap));
   rc |= dalloc(h, &A.counters, C * 8);
   rc |= dalloc(h, &A.rho_x, (size_t)N);
   rc |= dalloc(h, &A.rho_e, E);
@@ -310,57 +317,64 @@ int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
     if (_r != ncclSuccess) return fail((h), PIADMM_E_HIP, std::string(#expr ": ") + ncclGetErrorString(_r)); \
   } while (0)
 
-// One MPC step.  Per-component termination (and any fixed-iteration step): one fused launch,
-// plus, under term_global, the component-summed residual history all-reduced once.  Global
-// termination with the stopping test on: one launch per outer iteration, the rank's partials
-// all-reduced over RCCL and read back, the stop decided on the host exactly as
+// MPC steps t .. t+n-1 (n <= step_cap).  Per-component termination, or fixed iterations
+// under term_global: ONE persistent launch for all n steps (each workgroup runs its
+// component's steps back to back), plus, under term_global, the component-summed residual
+// history of every step, all-reduced once (n x 2 x max_outer doubles).  Global termination
+// with the stopping test on (one step per call): one launch per outer iteration, the rank's
+// partials all-reduced over RCCL and read back, the stop decided on the host exactly as
 // casadi/main.py:115-118,174-178 (MATLAB :191-210) do over all agents, then a final launch
 // for outputs and propagation.
-static int32_t run_step(piadmm_handle_t h, int32_t t, bool sync_outputs) {
+static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outputs) {
   const piadmm_config_t& c = h->cfg;
   hipStream_t s = h->stream;
   const int M = c.max_outer;
   if (!c.term_global) {
-    LAUNCH(h, pd::launch_mpc_step(h->a, t, 0, M, pd::F_FIRST | pd::F_LAST, s));
+    LAUNCH(h, pd::launch_mpc_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST, s));
     return PIADMM_OK;
   }
   if (c.fixed_iters) {
-    LAUNCH(h, pd::launch_mpc_step(h->a, t, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL, s));
-    LAUNCH(h, pd::launch_resid_history(h->a, h->d_part, s));
-    if (h->comm) NCCLCHK(h, ncclAllReduce(h->d_part, h->d_part, (size_t)2 * M, ncclDouble, ncclSum, h->comm, s));
+    LAUNCH(h, pd::launch_mpc_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL, s));
+    LAUNCH(h, pd::launch_resid_history(h->a, n, h->d_part, s));
+    if (h->comm)
+      NCCLCHK(h, ncclAllReduce(h->d_part, h->d_part, (size_t)n * 2 * M, ncclDouble, ncclSum, h->comm, s));
     h->giters = M;
     if (sync_outputs) {
-      HIPCHK(h, hipMemcpyAsync(h->h_part, h->d_part, (size_t)2 * M * sizeof(double), hipMemcpyDeviceToHost, s));
+      const double* last = h->d_part + (size_t)(n - 1) * 2 * M;
+      HIPCHK(h, hipMemcpyAsync(h->h_part, last, (size_t)2 * M * sizeof(double), hipMemcpyDeviceToHost, s));
       HIPCHK(h, hipStreamSynchronize(s));
       h->ghist.assign(h->h_part, h->h_part + 2 * M);
     }
     return PIADMM_OK;
   }
-  LAUNCH(h, pd::launch_pair_deff(h->a, s));
-  h->ghist.assign((size_t)2 * M, NAN);
-  int flag = 0, n = 0, nanlast = 0;
-  for (int it = 0; it < M; ++it) {
-    LAUNCH(h, pd::launch_mpc_step(h->a, t, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
-    double* part = h->d_part + (size_t)5 * it;
-    LAUNCH(h, pd::launch_term_partials(h->a, it, part, s));
-    if (h->comm) NCCLCHK(h, ncclAllReduce(part, part, 5, ncclDouble, ncclSum, h->comm, s));
-    HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipStreamSynchronize(s));
-    const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
-    const double n_seen = h->h_part[3], n_bad = h->h_part[4];
-    n = it + 1;
-    if (n_act == 0.0 && flag == 0) {      // no pair collides anywhere: stop (casadi/main.py:115-116)
-      nanlast = 1;
-      break;
+  for (int k = 0; k < n; ++k) {
+    const int tk = t + k;
+    LAUNCH(h, pd::launch_pair_deff(h->a, s));
+    h->ghist.assign((size_t)2 * M, NAN);
+    int flag = 0, nit = 0, nanlast = 0;
+    for (int it = 0; it < M; ++it) {
+      LAUNCH(h, pd::launch_mpc_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
+      double* part = h->d_part + (size_t)5 * it;
+      LAUNCH(h, pd::launch_term_partials(h->a, it, part, s));
+      if (h->comm) NCCLCHK(h, ncclAllReduce(part, part, 5, ncclDouble, ncclSum, h->comm, s));
+      HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
+      const double n_seen = h->h_part[3], n_bad = h->h_part[4];
+      nit = it + 1;
+      if (n_act == 0.0 && flag == 0) {      // no pair collides anywhere: stop (casadi/main.py:115-116)
+        nanlast = 1;
+        break;
+      }
+      flag = 1;
+      h->ghist[2 * it + 0] = rk;
+      h->ghist[2 * it + 1] = sk;
+      const bool dist_ok = n_seen > 0.0 && n_bad == 0.0;
+      if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok)) break;
     }
-    flag = 1;
-    h->ghist[2 * it + 0] = rk;
-    h->ghist[2 * it + 1] = sk;
-    const bool dist_ok = n_seen > 0.0 && n_bad == 0.0;
-    if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok)) break;
+    h->giters = nit;
+    LAUNCH(h, pd::launch_mpc_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
   }
-  h->giters = n;
-  LAUNCH(h, pd::launch_mpc_step(h->a, t, n, n, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
   return PIADMM_OK;
 }
 
@@ -370,8 +384,11 @@ static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
   if (n < 0 || t0 < 0 || t0 + (n > 0 ? n - 1 : 0) + h->cfg.H + 1 > h->T)
     return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
   HIPCHK(h, hipSetDevice(h->cfg.device));
-  for (int i = 0; i < n; ++i)
-    if (int rc = run_step(h, t0 + i, i == n - 1)) return rc;
+  for (int i = 0; i < n;) {
+    const int k = std::min(h->step_cap, n - i);
+    if (int rc = run_steps(h, t0 + i, k, i + k == n)) return rc;
+    i += k;
+  }
   return PIADMM_OK;
 }
 
@@ -430,6 +447,11 @@ int32_t piadmm_time_steps(piadmm_handle_t h, int32_t t0, int32_t n_steps, float*
 }
 
 int32_t piadmm_n_components(piadmm_handle_t h) { return h && h->have_scn ? h->C : 0; }
+
+int32_t piadmm_steps_per_launch(piadmm_handle_t h) {
+  if (!h || !h->have_scn) return 0;
+  return (h->cfg.term_global && !h->cfg.fixed_iters) ? 1 : h->step_cap;
+}
 
 int32_t piadmm_get_counters(piadmm_handle_t h, uint64_t* out) {
   if (!h || !out) return fail(h, PIADMM_E_ARG, "null argument");

@@ -1642,7 +1642,7 @@ __device__ __forceinline__ double delay_norm(const piadmm_config_t& c, double th
 // stop decision taken by the host from all-reduced partials, then a LAST launch with no
 // iterations for the outputs and the propagation.
 template <bool BIG>
-__global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it0, int it1, int flags) {
+__device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot) {
   extern __shared__ double lds[];
   __shared__ int s_int[NW * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
   const piadmm_config_t& c = A.cfg;
@@ -1874,7 +1874,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
   int n_xqp = 0, n_zqp = 0, n_admm_x = 0, n_admm_z = 0, n_pdas_x = 0, n_pdas_z = 0, n_inexact = 0;
   bool act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
   double dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
-  double* resid = A.resid + (size_t)ci * c.max_outer * 2;
+  double* resid = A.resid + ((size_t)slot * A.C + ci) * c.max_outer * 2;   // slot: step of the launch
   if (first)
     for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
   // reference positions of the own agent at time lanes (fixed for the step)
@@ -2167,6 +2167,21 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t, int it
   }
 }
 
+// Persistent multi-step launch (the reference's `for num_step` loop,
+// casadi/main.py:43-201, on the device): each workgroup runs MPC steps t0 .. t0+nsteps-1 of
+// its component back to back.  Components are independent whenever no step needs a
+// job-wide decision (per-component termination, or fixed iterations), so a component never
+// waits for the slowest one of each step: the launch takes max_c sum_t instead of
+// sum_t max_c.  The step-to-step state (xt, labels, caches) goes through HBM inside one
+// workgroup (same CU: the barrier's workgroup-scope fences order it).
+template <bool BIG>
+__global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
+  for (int k = 0; k < nsteps; ++k) {
+    mpc_step_body<BIG>(A, t0 + k, it0, it1, flags, k);
+    __syncthreads();
+  }
+}
+
 // Global termination partials of outer iteration `it` (one workgroup): rk, sk summed over
 // components, active pairs, pairs with a distance check, pairs failing it.
 __global__ void __launch_bounds__(256) k_term_partials(DevArgs A, int it, double* out) {
@@ -2198,10 +2213,12 @@ __global__ void __launch_bounds__(256) k_term_partials(DevArgs A, int it, double
 // Residual history of a fixed-iteration step summed over components: out[it] = (rk, sk).
 __global__ void __launch_bounds__(256) k_resid_history(DevArgs A, double* out) {
   const int it = blockIdx.x;
+  const int slot = blockIdx.y;                 // step of the multi-step launch
+  out += (size_t)slot * 2 * A.cfg.max_outer;
   __shared__ double red[2][256];
   double rk = 0.0, sk = 0.0;
   for (int ci = threadIdx.x; ci < A.C; ci += 256) {
-    const double* r = A.resid + ((size_t)ci * A.cfg.max_outer + it) * 2;
+    const double* r = A.resid + (((size_t)slot * A.C + ci) * A.cfg.max_outer + it) * 2;
     if (r[0] == r[0]) rk += r[0];
     if (r[1] == r[1]) sk += r[1];
   }
@@ -2233,7 +2250,7 @@ __global__ void k_pair_deff(DevArgs A) {
   A.deff[e] = d;
 }
 
-int launch_mpc_step(const DevArgs& a, int t, int it0, int it1, int flags, hipStream_t s) {
+int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s) {
   const size_t sh = lds_bytes(a.cfg.H, a.cfg.precision);
   const bool big = a.cfg.H > HMAX;
   static size_t attr[2] = {0, 0};     // dynamic LDS limit set so far per instantiation
@@ -2250,9 +2267,9 @@ int launch_mpc_step(const DevArgs& a, int t, int it0, int it1, int flags, hipStr
     attr[big] = sh;
   }
   if (big)
-    hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, it0, it1, flags);
+    hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
   else
-    hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, it0, it1, flags);
+    hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2261,8 +2278,8 @@ int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_resid_history(const DevArgs& a, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_resid_history, dim3(a.cfg.max_outer), dim3(256), 0, s, a, out);
+int launch_resid_history(const DevArgs& a, int nsteps, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_resid_history, dim3(a.cfg.max_outer, nsteps), dim3(256), 0, s, a, out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

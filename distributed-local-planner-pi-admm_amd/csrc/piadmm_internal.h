@@ -38,7 +38,7 @@ struct DevArgs {
   double* lam;              // E*2*2*(H+1)
   unsigned char* edge_active;  // E
   int* iters;               // C
-  double* resid;            // C*max_outer*2
+  double* resid;            // step_cap*C*max_outer*2 (slot k: step k of a multi-step launch)
   int* status;              // N+E
   // per-step solver workspace
   double* Pinv_x;           // N*H*H
@@ -114,9 +114,9 @@ constexpr int F_LAST = 2;     // last launch: outputs, propagation, cross-step w
 constexpr int F_GLOBAL = 4;   // termination decided outside (term_global): no per-component stop
 constexpr int F_NANLAST = 8;  // the global loop stopped at the collision test of iteration it0-1
 
-int launch_mpc_step(const DevArgs& a, int t, int it0, int it1, int flags, hipStream_t s);
+int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s);
-int launch_resid_history(const DevArgs& a, double* out, hipStream_t s);
+int launch_resid_history(const DevArgs& a, int nsteps, double* out, hipStream_t s);
 int launch_pair_deff(const DevArgs& a, hipStream_t s);
 
 }  // namespace pd

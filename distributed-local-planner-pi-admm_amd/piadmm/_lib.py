@@ -69,6 +69,7 @@ SYMBOLS = [
     ("piadmm_time_steps", c_i32, [_H, c_i32, c_i32, _P(ctypes.c_float)]),
     ("piadmm_get_state", c_i32, [_H, _dp, _dp, _dp, _dp, _dp, _P(ctypes.c_uint8), _ip]),
     ("piadmm_n_components", c_i32, [_H]),
+    ("piadmm_steps_per_launch", c_i32, [_H]),
     ("piadmm_get_counters", c_i32, [_H, _P(ctypes.c_uint64)]),
     ("piadmm_reset_counters", c_i32, [_H]),
     ("piadmm_get_component_counters", c_i32, [_H, _P(ctypes.c_uint64), c_i32]),

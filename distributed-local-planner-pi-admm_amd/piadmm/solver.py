@@ -117,6 +117,10 @@ class PI_ADMM_MI355X:
     def sync(self):
         self._check(self.lib.piadmm_sync(self._h))
 
+    def steps_per_launch(self) -> int:
+        """MPC steps the library runs per persistent kernel launch."""
+        return int(self.lib.piadmm_steps_per_launch(self._h))
+
     def time_steps(self, t0: int, n_steps: int) -> float:
         """hipEvent time (ms) of n_steps MPC steps on the handle's stream."""
         ms = ctypes.c_float()

@@ -123,7 +123,10 @@ int32_t piadmm_mpc_step(piadmm_handle_t h, int32_t t, double* xt_out, double* u_
                         double* resid_out, int32_t* iters_out, int32_t* status_out);
 
 /* Enqueue n_steps consecutive MPC steps starting at t0 on the handle's stream
- * without host copies or synchronisation (device-resident MPC loop). */
+ * without host copies or synchronisation (device-resident MPC loop: the reference's
+ * `for num_step` loop, casadi/main.py:43-201).  Unless global termination with the
+ * stopping test is on, up to piadmm_steps_per_launch() steps run in ONE persistent
+ * launch, each component stepping through them on its own. */
 int32_t piadmm_mpc_steps_async(piadmm_handle_t h, int32_t t0, int32_t n_steps);
 int32_t piadmm_sync(piadmm_handle_t h);
 
@@ -137,6 +140,8 @@ int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_o
                          double* hat, double* lam, uint8_t* edge_active, int32_t* iters);
 
 int32_t piadmm_n_components(piadmm_handle_t h);
+/* MPC steps per persistent launch (after set_scenario; 1 under global natural termination). */
+int32_t piadmm_steps_per_launch(piadmm_handle_t h);
 
 /* Work counters accumulated over all steps since the last reset, summed over
  * components: [0] outer iterations executed (per component), [1] x-step QPs,

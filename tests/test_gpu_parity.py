@@ -208,6 +208,31 @@ def test_async_steps_equal_blocking_steps(Solver):
         assert cnt["x_qps"] >= 6 * 16 and cnt["inexact"] == 0
 
 
+@pytest.mark.parametrize("H,fixed", [(30, 1), (40, 1), (12, 0)])
+def test_persistent_launch_equals_single_steps(Solver, H, fixed):
+    """Persistent multi-step launches (the bench's mode: fixed iterations under the global
+    scope, chunks of steps_per_launch() steps) give bit-identical states, controls and the
+    global residual history of the last step as one launch per MPC step."""
+    n = 9
+    cfg = config.matlab_pi(H=H, fixed_iters=fixed, max_outer=40, term_global=fixed)
+    scn = scenario.tiled(16, H, n_steps=n + 1, perturb=True, seed=3)
+    with Solver(cfg, scn) as s1, Solver(cfg, scn) as s2:
+        assert s2.steps_per_launch() >= (n if fixed or not cfg.term_global else 1)
+        for _ in range(n):
+            r = s1.mpc_step()
+        s2.steps_async(0, n)
+        s2.sync()
+        st = s2.state()
+        np.testing.assert_array_equal(st["xt"], r.xt)
+        np.testing.assert_array_equal(st["u"], r.u)
+        if cfg.term_global:
+            g1, i1 = s1.global_resid()
+            g2, i2 = s2.global_resid()
+            assert i1 == i2
+            np.testing.assert_array_equal(g1, g2)
+        assert s2.counters()["inexact"] == 0
+
+
 def test_errors_are_loud(Solver):
     with pytest.raises(_lib.PiadmmError, match="H must be"):
         Solver(config.matlab_pi(H=64), scenario.tiled(1, 64, n_steps=1))
