@@ -372,6 +372,8 @@ struct QP {
   int mmax;               // capacity of fac (rows)
   bool kready;            // K holds K_s^-1 for the current rho (the pair builds it lazily:
                           // a QP that the warm-label polish certifies never needs it)
+  double* Y;              // pair: dual active-set columns P^-1 n_a (shares the K_s^-1 region)
+  int ycap;               // pair: columns Y holds
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
   // Row s of vehicle v = s / 2: even = box (lanes < H), odd = rate (lanes < H-1), 4 = hinge
@@ -1290,6 +1292,282 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
   return false;
 }
 
+
+// ============================================================ dual active set (pair QP)
+// Goldfarb-Idnani dual active-set method on the pair QP in hinge form, in Schur-complement
+// form.  From the unconstrained minimiser x0 = -P^-1 q it adds the most violated one-sided
+// constraint n_p'x >= b_p at a time (box/rate row r: side 0 = a_r'x >= lo, side 1 =
+// -a_r'x >= -hi; hinge row: a_r'x >= h with multiplier cap beta), taking partial (dual)
+// steps that drop a constraint whose multiplier reaches 0.  The active set's Schur
+// complement S = N P^-1 N' is kept as a Cholesky factor L (LDS, insertion order): an add
+// appends one row (its forward-solve vector w and sqrt(S_pp - w'w)), a drop deletes row k and
+// restores the trailing block by a rank-one update.  Y holds the columns P^-1 n_a.  Each step
+// costs two m-step triangular solves, one m-column pass over Y and a few wave reductions --
+// no K_s^-1 and no ADMM.  On the recorded bench pair QPs (tools/gi_sim.py) it certifies every
+// one in 28 steps on average (max 51) where ADMM + PDAS took ~45 ADMM iterations and ~6
+// full reduced solves.  A hinge multiplier reaching the cap, a full factor or the step limit
+// return false and the caller falls back to ADMM + PDAS; the result is certified by the same
+// KKT test either way.
+__device__ __forceinline__ double tri_fwd(const double* L, int ld, double linv, double b, int m) {
+  const int l = lid();
+  for (int k = 0; k < m; ++k) {
+    const double Llk = (l > k && l < m) ? L[l * ld + k] : 0.0;
+    const double zk = rdl(b * linv, k);
+    if (l == k) b = zk;
+    b -= Llk * zk;
+  }
+  return (l < m) ? b : 0.0;
+}
+__device__ __forceinline__ double tri_bwd(const double* L, int ld, double linv, double b, int m) {
+  const int l = lid();
+  for (int k = m - 1; k >= 0; --k) {
+    const double Lkl = (l < k) ? L[k * ld + l] : 0.0;
+    const double xk = rdl(b * linv, k);
+    if (l == k) b = xk;
+    b -= Lkl * xk;
+  }
+  return (l < m) ? b : 0.0;
+}
+
+// P^-1 n for the one-sided constraint (row id, sign sg): lane = variable (one value per vehicle)
+template <int NV>
+__device__ __forceinline__ void pinv_row(const QP<NV>& P, int row, double sg, double* out) {
+  const int l = lid(), H = P.H;
+  const int lc = (l < H) ? l : 0;
+  const RowT r = row_terms(P, row);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int i = v * H + lc;
+    double val;
+    if (NV == 2 && r.hk >= 0) {
+      val = (v ? P.g2 : P.g1) * P.Pinv[4 * H * H + r.hk * P.n + i];
+    } else {
+      val = r.c0 * P.Pinv[r.i0 * P.n + i] + r.c1 * P.Pinv[r.i1 * P.n + i];
+    }
+    out[v] = (l < H) ? sg * val : 0.0;
+  }
+}
+
+constexpr int GI_MAX_STEPS = 256;
+template <int NV>
+__device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x, double* y, int& nsteps) {
+  constexpr int NR = QP<NV>::NR;
+  const int l = lid(), H = P.H, ld = P.fld, H2 = NV * H;
+  double* vb_ax = P.vb + 192;      // [192, 192 + NR*H): (A v) by row id
+  int* wc = P.ib;                  // active constraint codes 2*row + side, insertion order
+  double* L = P.fac;
+  double* Y = P.Y;
+  const int cap = min(P.mmax - 1, P.ycap);
+  P.kready = false;                // Y overwrites the K_s^-1 region
+  if (l == 0) P.fstate[0] = -1;    // and L the cached PDAS factor
+  double x0[NV], xc[NV];
+  gemv_sym<true>(P, P.Pinv, P.q, x0);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xc[v] = x0[v] = -x0[v];
+  int m = 0, wbits = 0;
+  double ua = 0.0, linv = 0.0;     // lane a < m: multiplier and 1/L_aa of active constraint a
+  bool done = false;
+  while (!done) {
+    // ---- most violated constraint outside the active set
+    double ax[NR];
+    A_mul(P, xc, ax);
+    double best = 0.0;
+    int code = -1;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      if (!P.valid(s)) continue;
+      const double tp = P.tol * (1.0 + fabs(P.lo(s)));
+      if (!((wbits >> (2 * s)) & 1)) {
+        const double sv = ax[s] - P.lo(s);
+        if (sv < -tp && sv < best) { best = sv; code = 2 * (s * H + l); }
+      }
+      if (!P.hinge(s) && !((wbits >> (2 * s + 1)) & 1)) {
+        const double sv = P.hi(s) - ax[s];
+        if (sv < -tp && sv < best) { best = sv; code = 2 * (s * H + l) + 1; }
+      }
+    }
+    const double bmin = wmin(best);
+    if (!(bmin < 0.0)) break;
+    const int pl = __ffsll((unsigned long long)__ballot(code >= 0 && best == bmin)) - 1;
+    const int pc = rdli(code, pl);
+    const int prow = pc >> 1, pside = pc & 1, ps = prow / H, pk = prow - ps * H;
+    const double sgp = pside ? -1.0 : 1.0;
+    const bool phinge = P.hinge(ps);
+    double sp = rdl(pside ? P.hi(ps) - ax[ps] : ax[ps] - P.lo(ps), pk);   // slack of p (< 0)
+    double yp[NV];
+    pinv_row(P, prow, sgp, yp);
+    {
+      double ay[NR];
+      A_mul(P, yp, ay);
+      if (l < H) {
+#pragma unroll
+        for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ay[s];
+      }
+    }
+    wsync();
+    const double spp = sgp * vb_ax[prow];  // n_p' P^-1 n_p
+    double up = 0.0;
+    while (true) {
+      if (++nsteps > GI_MAX_STEPS) return false;
+      const int myc = (l < m) ? wc[l] : 0;
+      const double va = (l < m) ? ((myc & 1) ? -1.0 : 1.0) * vb_ax[myc >> 1] : 0.0;   // n_a' y_p
+      const double w = tri_fwd(L, ld, linv, va, m);
+      const double r = tri_bwd(L, ld, linv, w, m);
+      // z = y_p - Y r
+      double z[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) z[v] = yp[v];
+      {
+        const int lc = (l < H) ? l : 0;
+        for (int a0 = 0; a0 < m; a0 += GEMV_U) {
+          double yv[GEMV_U][NV], rv[GEMV_U];
+#pragma unroll
+          for (int u = 0; u < GEMV_U; ++u) {
+            const int a = min(a0 + u, m - 1);
+            rv[u] = (a0 + u < m) ? rdl(r, a) : 0.0;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) yv[u][v] = Y[a * H2 + v * H + lc];
+          }
+#pragma unroll
+          for (int u = 0; u < GEMV_U; ++u)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) z[v] -= rv[u] * yv[u][v];
+        }
+      }
+      const double lpp2 = spp - wsum(w * w);                   // n_p' z
+      const double t2 = (lpp2 > DEP_TOL * spp) ? -sp / lpp2 : INFINITY;
+      // dual step limits: an active multiplier reaching 0 (drop) or a hinge one reaching beta
+      const bool hin_a = (l < m) && P.hinge((myc >> 1) / H);
+      const double tdrop = (l < m && r > 0.0) ? ua / r : INFINITY;
+      const double tcap = (hin_a && r < 0.0) ? (P.beta - ua) / (-r) : INFINITY;
+      const double t1 = wmin(tdrop);
+      const double tc = fmin(wmin(tcap), phinge ? P.beta - up : INFINITY);
+      const double t = fmin(t1, t2);
+      if (!(t < INFINITY) || tc <= t) return false;   // unbounded dual step / hinge saturates
+      if (t2 < INFINITY) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xc[v] += t * z[v];
+        sp += t * lpp2;
+      }
+      if (l < m) ua -= t * r;
+      up += t;
+      if (t2 <= t1) {
+        // ---- add p: L row m = (w', sqrt(lpp2)), Y column m = y_p
+        if (m >= cap) return false;
+        const double lmm = sqrt(lpp2);
+        if (l < m) L[m * ld + l] = w;
+        if (l == m) {
+          L[m * ld + m] = lmm;
+          linv = 1.0 / lmm;
+          ua = up;
+          wc[m] = pc;
+        }
+        if (l < H) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) Y[m * H2 + v * H + l] = yp[v];
+        }
+        if (l == pk) wbits |= 1 << (2 * ps + pside);
+        ++m;
+        if (P.gmem) gsync();
+        else wsync();
+        break;
+      }
+      // ---- drop active constraint k: delete row/column k of L, rank-one update of the
+      // trailing block with the deleted column, compact L, Y, codes and multipliers
+      const int k = __ffsll((unsigned long long)__ballot(l < m && tdrop == t1)) - 1;
+      const int kc = rdli(myc, k);
+      if (l == (kc >> 1) % H) wbits &= ~(1 << (2 * ((kc >> 1) / H) + (kc & 1)));
+      {
+        double xv = (l > k && l < m) ? L[l * ld + k] : 0.0;
+        for (int j = k + 1; j < m; ++j) {
+          const double Ljj = L[j * ld + j];
+          const double xj = rdl(xv, j);
+          const double rr = sqrt(Ljj * Ljj + xj * xj);
+          const double cc = rr / Ljj, sn = xj / Ljj;
+          if (l == j) L[j * ld + j] = rr;
+          if (l > j && l < m) {
+            const double Lij = (L[l * ld + j] + sn * xv) / cc;
+            xv = cc * xv - sn * Lij;
+            L[l * ld + j] = Lij;
+          }
+        }
+        wsync();
+        // compact: row i <- row i+1 (i >= k), column j <- column j+1 (j >= k); lane = column
+        for (int i = k; i < m - 1; ++i) {
+          const double v = (l < m - 1) ? L[(i + 1) * ld + l + (l >= k ? 1 : 0)] : 0.0;
+          wsync();
+          if (l <= i) L[i * ld + l] = v;
+          wsync();
+        }
+        const int cnext = (l + 1 < m) ? wc[l + 1] : 0;
+        wsync();
+        if (l >= k && l < m - 1) wc[l] = cnext;
+        const double un = shdn(ua, 1);
+        if (l >= k) ua = (l < m - 1) ? un : 0.0;
+        for (int a = k; a < m - 1; ++a) {
+          if (l < H) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) Y[a * H2 + v * H + l] = Y[(a + 1) * H2 + v * H + l];
+          }
+        }
+        --m;
+        if (P.gmem) gsync();
+        else wsync();
+        linv = (l < m) ? 1.0 / L[l * ld + l] : 0.0;
+      }
+    }
+  }
+  // ---- exact solution of the final active set (the reduced solve with this factor):
+  // lam = S^-1 (N x0 - b), x = x0 - Y lam;  kernel multipliers y_a = sign_a * lam_a
+  {
+    double ax0[NR];
+    A_mul(P, x0, ax0);
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ax0[s] - P.lo(s);   // lower-side residual
+    }
+    wsync();
+    const int myc = (l < m) ? wc[l] : 0;
+    const int rw = myc >> 1, rs = rw / H;
+    double rhs = 0.0;
+    if (l < m) {
+      // upper side (box / rate rows only, uniform bounds): -(a'x0 - hi)
+      const double blo = (rs & 1) ? -P.dumax : -P.umax;
+      rhs = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
+    }
+    const double lam = tri_bwd(L, ld, linv, tri_fwd(L, ld, linv, rhs, m), m);
+    double xs[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xs[v] = x0[v];
+    const int lc = (l < H) ? l : 0;
+    for (int a = 0; a < m; ++a) {
+      const double la = rdl(lam, a);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) xs[v] -= la * Y[a * H2 + v * H + lc];
+    }
+    wsync();
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = 0.0;
+    }
+    wsync();
+    if (l < m) vb_ax[rw] = (myc & 1) ? -lam : lam;
+    wsync();
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = (l < H) ? xs[v] : 0.0;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      const bool lo_in = (wbits >> (2 * s)) & 1, hi_in = (wbits >> (2 * s + 1)) & 1;
+      y[s] = (P.valid(s) && l < H && (lo_in || hi_in)) ? vb_ax[s * H + l] : 0.0;
+      if (P.hinge(s)) lab[s] = lo_in ? HKINK : HZERO;
+      else lab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
+      if (!P.valid(s)) lab[s] = 0;
+    }
+    wsync();
+  }
+  return true;
+}
+
 // OSQP-style adaptive rho (in the scaled space): rho *= sqrt((|r_prim|/|Ax,z|) / (|r_dual|/|Px,A'y,q|)).
 // Returns the proposed factor (1 when inside [0.2, 5]).
 template <int NV>
@@ -1337,7 +1615,7 @@ constexpr int ADAPT_EVERY = PIADMM_ADAPT_EVERY;
 template <int NV, bool TWO>
 __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
                                         bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
-                                        double* x_out, int& n_admm, int& n_pdas) {
+                                        double* x_out, int& n_admm, int& n_pdas, int& n_gi) {
   constexpr int NR = QP<NV>::NR;
   double x[NV], y[NR];
   bool ok = false;
@@ -1348,6 +1626,22 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
 #pragma unroll
     for (int s = 0; s < NR; ++s) flab[s] = lab[s];
     ok = pdas(P, lab, x, y, n_pdas);
+  }
+  if constexpr (NV == 2) {
+    // pair QP: dual active set first (no K_s^-1, no ADMM); certified by the KKT test, and
+    // when that fails, polished from its labels before the ADMM fallback
+    if (!ok && P.ycap > 0) {
+      int ngi = 0;
+      signed char glab[NR];
+      if (gi_solve(P, glab, x, y, ngi)) {
+        signed char nl[NR];
+        ok = kkt_check(P, glab, x, y, nl);
+#pragma unroll
+        for (int s = 0; s < NR; ++s) lab[s] = glab[s];
+        if (!ok) ok = pdas(P, lab, x, y, n_pdas);
+      }
+      n_gi += ngi;
+    }
   }
   signed char plab[NR];
 #pragma unroll
@@ -1842,6 +2136,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     qe.mmax = WAVE;
     qe.gmem = big;
     qe.xld = 0;
+    // dual active-set columns in the K_s^-1 region (4H^2 doubles, or 2H^2 with fp32 images)
+    qe.Y = Ke ? Ke : (double*)Kef;
+    qe.ycap = ((Ke ? 4 : 2) * H * H) / (2 * H);
     // Ke doubles as the H x 2H staging of the per-scenario pair tables; with fp32 images in
     // LDS mode the fp32 region (2H^2 doubles of space) takes that role
     setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke ? Ke : (double*)Kef, deff);
@@ -1871,7 +2168,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   int flag = first ? 0 : A.cst[(size_t)ci * 4 + 0];
   int aliased = first ? 0 : A.cst[(size_t)ci * 4 + 1];
   int iters = it0;
-  int n_xqp = 0, n_zqp = 0, n_admm_x = 0, n_admm_z = 0, n_pdas_x = 0, n_pdas_z = 0, n_inexact = 0;
+  int n_xqp = 0, n_zqp = 0, n_admm_x = 0, n_admm_z = 0, n_pdas_x = 0, n_pdas_z = 0, n_inexact = 0, n_gi = 0;
   bool act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
   double dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
   double* resid = A.resid + ((size_t)slot * A.C + ci) * c.max_outer * 2;   // slot: step of the launch
@@ -1905,7 +2202,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int stx = qp_solve<1, false>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
-                               qx.fld, ustar, n_admm_x, n_pdas_x);
+                               qx.fld, ustar, n_admm_x, n_pdas_x, n_gi);
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
       ++n_xqp;
@@ -1957,7 +2254,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       // (big mode, two columns per lane, in HBM)
       const int ste = qp_solve<2, BIG>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
                                big ? Ke : scr, big ? 2 * H : LD, uh,
-                               n_admm_z, n_pdas_z);
+                               n_admm_z, n_pdas_z, n_gi);
       STAMP_ADD(ST_ZQP, t_zq);
       status_e |= ste;
       ++n_zqp;
