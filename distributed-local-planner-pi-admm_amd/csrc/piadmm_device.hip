@@ -39,7 +39,7 @@ __device__ unsigned long long* g_stamps;
 enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL, ST_ZSTEP, ST_ZQP, ST_ZRED,
                  ST_KERNEL, ST_RED_GEMV, ST_RED_S, ST_RED_CHOL, ST_RED_X, ST_ADMM, ST_XQ, ST_TERM,
                  ST_SZ_RUIZ, ST_SZ_KMAT, ST_SZ_GJ, ST_SZ_PRE, ST_ZR_GEMV, ST_ZR_S, ST_ZR_CHOL, ST_ZR_X,
-                 ST_ZR_SOLVE, ST_XR_SOLVE, ST_ZKKT, ST_XKKT };
+                 ST_ZR_SOLVE, ST_XR_SOLVE, ST_ZKKT, ST_XKKT, ST_GI_SEARCH, ST_GI_SOLVE, ST_GI_UPD };
 
 // ============================================================ wave primitives
 __device__ __forceinline__ int lid() { return (int)__lane_id(); }
@@ -89,21 +89,6 @@ __device__ __forceinline__ double shdn(double v, int o) {
   double t = __shfl_down(v, (unsigned)o);
   return lid() + o < WAVE ? t : 0.0;
 }
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ double wmax(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-  return v;
-}
-__device__ __forceinline__ double wmin(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-  return v;
-}
 __device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
 __device__ __forceinline__ bool wall(bool p) { return __ballot(!p) == 0ull; }
 
@@ -115,6 +100,33 @@ __device__ __forceinline__ double dppd_rows(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, ROWS, 0xf, false);
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
+// DPP move in which lanes without a valid source (or outside ROWS) keep their own value:
+// the identity for min / max.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dppd_keep(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const int l0 = (int)(unsigned)(b & 0xffffffffull), h0 = (int)(unsigned)(b >> 32);
+  const int lo = __builtin_amdgcn_update_dpp(l0, l0, CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(h0, h0, CTRL, ROWS, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// Wave-wide min / max / sum of a double, broadcast to every lane: the same DPP scan as
+// scan_incl (row_shr 1,2,4,8, then row_bcast:15 / row_bcast:31) ending in lane 63, read back
+// through SGPRs -- a few VALU cycles per stage instead of the LDS round trip of a
+// ds_bpermute per stage (__shfl_xor).
+template <bool MAX>
+__device__ __forceinline__ double wext(double v) {
+  auto op = [](double a, double b) { return MAX ? fmax(a, b) : fmin(a, b); };
+  v = op(v, dppd_keep<0x111, 0xf>(v));
+  v = op(v, dppd_keep<0x112, 0xf>(v));
+  v = op(v, dppd_keep<0x114, 0xf>(v));
+  v = op(v, dppd_keep<0x118, 0xf>(v));
+  v = op(v, dppd_keep<0x142, 0xa>(v));
+  v = op(v, dppd_keep<0x143, 0xc>(v));
+  return rdl(v, 63);
+}
+__device__ __forceinline__ double wmax(double v) { return wext<true>(v); }
+__device__ __forceinline__ double wmin(double v) { return wext<false>(v); }
 
 // Inclusive prefix / suffix sums over the 64 lanes (time lanes 0..H, H <= 63).  Four DPP
 // row shifts inside each 16-lane row; the prefix carries across rows with the GFX9
@@ -138,6 +150,8 @@ __device__ __forceinline__ double scan_incl_rev(double v) {
   const double c = (l < 16) ? r1 + (r2 + r3) : ((l < 32) ? r2 + r3 : ((l < 48) ? r3 : 0.0));
   return v + c;
 }
+__device__ __forceinline__ double wsum(double v) { return rdl(scan_incl(v), 63); }
+
 // T(t, j) = (t-1-j)+ is the rollout's double integrator (casadi/PI_ADMM_class.py:59-69:
 // theta accumulates u, x/y accumulate theta).  "hinge lane" k holds time t = k+1.
 // T_apply : var lanes u_j        -> hinge lanes (T u)_{k+1} = sum_{j<=k-1} (k-j) u_j
@@ -1308,23 +1322,45 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
 // full reduced solves.  A hinge multiplier reaching the cap, a full factor or the step limit
 // return false and the caller falls back to ADMM + PDAS; the result is certified by the same
 // KKT test either way.
+// Triangular solves with lane = row, the factor's column (fwd) / row (bwd) entries of a batch
+// of TRI_U steps loaded before the batch's dependent chain: one LDS latency per batch
+// instead of one per step.
+constexpr int TRI_U = 8;
 __device__ __forceinline__ double tri_fwd(const double* L, int ld, double linv, double b, int m) {
   const int l = lid();
-  for (int k = 0; k < m; ++k) {
-    const double Llk = (l > k && l < m) ? L[l * ld + k] : 0.0;
-    const double zk = rdl(b * linv, k);
-    if (l == k) b = zk;
-    b -= Llk * zk;
+  const int lr = (l < m) ? l : 0;
+  for (int k0 = 0; k0 < m; k0 += TRI_U) {
+    double Lv[TRI_U];
+#pragma unroll
+    for (int u = 0; u < TRI_U; ++u) Lv[u] = L[lr * ld + min(k0 + u, 63)];
+#pragma unroll
+    for (int u = 0; u < TRI_U; ++u) {
+      const int k = k0 + u;
+      if (k < m) {
+        const double zk = rdl(b * linv, k);
+        if (l == k) b = zk;
+        if (l > k && l < m) b -= Lv[u] * zk;
+      }
+    }
   }
   return (l < m) ? b : 0.0;
 }
 __device__ __forceinline__ double tri_bwd(const double* L, int ld, double linv, double b, int m) {
   const int l = lid();
-  for (int k = m - 1; k >= 0; --k) {
-    const double Lkl = (l < k) ? L[k * ld + l] : 0.0;
-    const double xk = rdl(b * linv, k);
-    if (l == k) b = xk;
-    b -= Lkl * xk;
+  const int lc = (l < m) ? l : 0;
+  for (int k0 = m - 1; k0 >= 0; k0 -= TRI_U) {
+    double Lv[TRI_U];
+#pragma unroll
+    for (int u = 0; u < TRI_U; ++u) Lv[u] = L[max(k0 - u, 0) * ld + lc];
+#pragma unroll
+    for (int u = 0; u < TRI_U; ++u) {
+      const int k = k0 - u;
+      if (k >= 0) {
+        const double xk = rdl(b * linv, k);
+        if (l == k) b = xk;
+        if (l < k) b -= Lv[u] * xk;
+      }
+    }
   }
   return (l < m) ? b : 0.0;
 }
@@ -1368,6 +1404,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
   double ua = 0.0, linv = 0.0;     // lane a < m: multiplier and 1/L_aa of active constraint a
   bool done = false;
   while (!done) {
+    unsigned long long t_gs = STAMP_T();
     // ---- most violated constraint outside the active set
     double ax[NR];
     A_mul(P, xc, ax);
@@ -1407,8 +1444,10 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
     wsync();
     const double spp = sgp * vb_ax[prow];  // n_p' P^-1 n_p
     double up = 0.0;
+    STAMP_ADD(ST_GI_SEARCH, t_gs);
     while (true) {
       if (++nsteps > GI_MAX_STEPS) return false;
+      unsigned long long t_gv = STAMP_T();
       const int myc = (l < m) ? wc[l] : 0;
       const double va = (l < m) ? ((myc & 1) ? -1.0 : 1.0) * vb_ax[myc >> 1] : 0.0;   // n_a' y_p
       const double w = tri_fwd(L, ld, linv, va, m);
@@ -1435,6 +1474,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
         }
       }
       const double lpp2 = spp - wsum(w * w);                   // n_p' z
+      STAMP_ADD(ST_GI_SOLVE, t_gv);
+      unsigned long long t_gu = STAMP_T();
       const double t2 = (lpp2 > DEP_TOL * spp) ? -sp / lpp2 : INFINITY;
       // dual step limits: an active multiplier reaching 0 (drop) or a hinge one reaching beta
       const bool hin_a = (l < m) && P.hinge((myc >> 1) / H);
@@ -1470,6 +1511,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
         ++m;
         if (P.gmem) gsync();
         else wsync();
+        STAMP_ADD(ST_GI_UPD, t_gu);
         break;
       }
       // ---- drop active constraint k: delete row/column k of L, rank-one update of the
@@ -1515,6 +1557,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
         else wsync();
         linv = (l < m) ? 1.0 / L[l * ld + l] : 0.0;
       }
+      STAMP_ADD(ST_GI_UPD, t_gu);
     }
   }
   // ---- exact solution of the final active set (the reduced solve with this factor):
@@ -2201,8 +2244,13 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
+#ifdef PIADMM_DIAG_NO_XQP   // diagnostic timing build only: skip the x-step QP
+      const int stx = 0;
+      ustar[0] = 1e-3 * qx.q[0];
+#else
       const int stx = qp_solve<1, false>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n_admm_x, n_pdas_x, n_gi);
+#endif
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
       ++n_xqp;
@@ -2211,7 +2259,11 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       const double u = around(ustar[0], c.round_decimals);
       double px, py, pth;
       unsigned long long t_r = STAMP_T();
+#ifdef PIADMM_DIAG_NO_ROLL  // diagnostic timing build only: skip the rollout
+      px = py = pth = u;
+#else
       rollout(S.xt + 3 * w, A.spd[a], (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+#endif
       STAMP_ADD(ST_XROLL, t_r);
       if (l <= H) {
         S.pos[(w * 2 + 0) * H1 + l] = px;
