@@ -79,8 +79,8 @@ def latest_traffic(workload: str):
                 tj = json.load(f)
         except (OSError, ValueError):
             continue
-        if tj.get("workload") == workload:
-            return tj.get("hbm_bytes_per_launch")
+        if tj.get("workload") == workload and tj.get("hbm_bytes_per_step"):
+            return tj["hbm_bytes_per_step"]
     return None
 
 
@@ -124,7 +124,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # default warmup = default steps: the warmup launch and the timed launch of k_mpc_step have
+    # the same size, so rocprofv3's per-kernel average over the run compares with avg_launch_ms
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle timing (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--natural", action="store_true", help="natural (global) termination, not the headline")
@@ -196,7 +198,8 @@ def main():
     bytes_launch = algorithmic_bytes(cnt, H) / n_launch
     achieved = bytes_launch / avg_launch_s / 1e9
 
-    traffic = latest_traffic(f"tiled{N_TILES}_H{H}_matlab_pi_fixed{MAX_OUTER}")
+    traffic_step = latest_traffic(f"tiled{N_TILES}_H{H}_matlab_pi_fixed{MAX_OUTER}") if not args.natural else None
+    traffic = traffic_step * K / n_launch if traffic_step else None
 
     line = {
         "metric": "PI-ADMM outer iterations/sec (and ms/MPC step) at N_agents×H; 1/2/4/8 GPU",

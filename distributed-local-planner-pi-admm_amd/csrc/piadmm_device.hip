@@ -25,12 +25,15 @@ namespace pd {
 
 // Diagnostic phase stamps (separate build, never in the measured library).
 #ifdef PIADMM_STAMPS
+// cycles accumulate in LDS (one ds_add_u64 per stamp, lane 0) and are flushed to g_stamps
+// once per launch, so that a stamp costs an LDS atomic, not a global one
 __device__ unsigned long long* g_stamps;
+__shared__ unsigned long long s_stamps[32];
 #define STAMP_T() __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, t0)                                                                   \
   do {                                                                                        \
     const unsigned long long _d = __builtin_amdgcn_s_memtime() - (t0);                       \
-    if (__lane_id() == 0 && g_stamps) atomicAdd(&g_stamps[blockIdx.x * 32 + (slot)], _d);   \
+    if (__lane_id() == 0) atomicAdd(&s_stamps[(slot)], _d);                                  \
   } while (0)
 #else
 #define STAMP_T() 0ull
@@ -388,6 +391,8 @@ struct QP {
                           // a QP that the warm-label polish certifies never needs it)
   double* Y;              // pair: dual active-set columns P^-1 n_a (shares the K_s^-1 region)
   int ycap;               // pair: columns Y holds
+  bool scaled;            // Ruiz scaling computed (the pair computes it only when ADMM is needed)
+  const double* Kcache;   // x-step: HBM copy of K_s^-1, loaded into K only when ADMM is needed
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
   // Row s of vehicle v = s / 2: even = box (lanes < H), odd = rate (lanes < H-1), 4 = hinge
@@ -1690,7 +1695,38 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
 #pragma unroll
   for (int s = 0; s < NR; ++s) plab[s] = -1;
   if (!ok && !P.kready) {
-    build_K<NV, TWO>(P, kscr, kld);
+    if (!P.scaled) {
+      // the warm ADMM state is in identity scaling (x, A x, y): move it to the Ruiz space
+      unsigned long long t_r = STAMP_T();
+      ruiz(P);
+      STAMP_ADD(ST_SZ_RUIZ, t_r);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) xs[v] = (P.D[v] != 0.0) ? xs[v] / P.D[v] : 0.0;
+#pragma unroll
+      for (int s = 0; s < NR; ++s) {
+        zs[s] = P.valid(s) ? P.E[s] * zs[s] : 0.0;
+        ys[s] = P.valid(s) ? ys[s] / P.E[s] : 0.0;
+      }
+      P.scaled = true;
+    }
+    if (NV == 1 && P.Kcache) {
+      // the per-scenario HBM copy (same penalty): batched loads, then the LDS stores
+      const int l = lid(), n = P.n;
+      for (int i0 = 0; i0 < n; i0 += 8) {
+        double kv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kv[u] = (l < n) ? P.Kcache[min(i0 + u, n - 1) * n + l] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (l < n && i0 + u < n) {
+            if (P.kf32) P.Kf[(i0 + u) * n + l] = (float)kv[u];
+            else P.K[(i0 + u) * n + l] = kv[u];
+          }
+        }
+      }
+    } else {
+      build_K<NV, TWO>(P, kscr, kld);
+    }
     P.kready = true;
     if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
     wsync();
@@ -1708,6 +1744,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       if (f != 1.0) {
         P.rho = fmin(fmax(P.rho * f, 1e-6), 1e6);
         build_K<NV, TWO>(P, kscr, kld);
+        P.Kcache = nullptr;      // the cached copy is for the old penalty
         if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
         wsync();
       }
@@ -1832,6 +1869,8 @@ __device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, doubl
   P.alpha = c.admm_alpha;
   P.tol = c.qp_tol;
   P.kready = true;      // setup_agent loads or builds K_s^-1
+  P.scaled = true;
+  P.Kcache = nullptr;
 }
 
 // x-step QP of agent a (cost_function_primal, PI_ADMM_class.py:114-135, constraints :172-192):
@@ -1852,12 +1891,9 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
     P.D[0] = in ? sc[li] : 0.0;
     P.E[0] = in ? sc[HCAP + li] : 0.0;
     P.E[1] = (l < H - 1) ? sc[2 * HCAP + li] : 0.0;
-    if (P.kf32) {
-      for (int i = 0; i < H; ++i)
-        if (in) P.Kf[i * H + l] = (float)Kc[i * H + l];
-    } else if (P.K != Kc) {
-      for (int i = 0; i < H; ++i)
-        if (in) P.K[i * H + l] = Kc[i * H + l];
+    if (P.kf32 || P.K != Kc) {   // LDS image of K_s^-1: loaded by qp_solve when ADMM is needed
+      P.Kcache = Kc;
+      P.kready = false;
     }
     wsync();
     return;
@@ -1950,9 +1986,17 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
     gsync();                    // the tables are read back through L2 by the polish
   }
   STAMP_ADD(ST_SZ_PRE, t_pre);
-  unsigned long long t_r = STAMP_T();
-  ruiz(P);
-  STAMP_ADD(ST_SZ_RUIZ, t_r);
+  // identity scaling: the dual active set and the polish work unscaled; the Ruiz
+  // equilibration of the ADMM space is computed by qp_solve only when ADMM is needed
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    P.D[v] = in ? 1.0 : 0.0;
+    P.E[2 * v] = in ? 1.0 : 0.0;
+    P.E[2 * v + 1] = (l < H - 1) ? 1.0 : 0.0;
+  }
+  P.E[4] = P.valid(4) ? 1.0 : 0.0;
+  P.scaled = false;
+  P.Kcache = nullptr;
   P.kready = false;     // K_s^-1 is built by qp_solve when ADMM is first needed
 }
 // ============================================================ the MPC-step kernel
@@ -2497,12 +2541,13 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     if (!last_launch) {
       double* qs = A.qs_e + (size_t)e * 12 * WAVE;
       signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
-      qs[l] = xs_e[0];
-      qs[WAVE + l] = xs_e[1];
+      // unscaled (the next launch restarts in identity scaling, setup_pair)
+      qs[l] = qe.D[0] * xs_e[0];
+      qs[WAVE + l] = qe.D[1] * xs_e[1];
 #pragma unroll
       for (int s = 0; s < 5; ++s) {
-        qs[(2 + s) * WAVE + l] = zs_e[s];
-        qs[(7 + s) * WAVE + l] = ys_e[s];
+        qs[(2 + s) * WAVE + l] = (qe.E[s] != 0.0) ? zs_e[s] / qe.E[s] : 0.0;
+        qs[(7 + s) * WAVE + l] = qe.E[s] * ys_e[s];
         ql[s * WAVE + l] = lab_e[s];
       }
     }
@@ -2525,10 +2570,17 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 // workgroup (same CU: the barrier's workgroup-scope fences order it).
 template <bool BIG>
 __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
+#ifdef PIADMM_STAMPS
+  if (threadIdx.x < 32) s_stamps[threadIdx.x] = 0ull;
+  __syncthreads();
+#endif
   for (int k = 0; k < nsteps; ++k) {
     mpc_step_body<BIG>(A, t0 + k, it0, it1, flags, k);
     __syncthreads();
   }
+#ifdef PIADMM_STAMPS
+  if (threadIdx.x < 32 && g_stamps) atomicAdd(&g_stamps[blockIdx.x * 32 + threadIdx.x], s_stamps[threadIdx.x]);
+#endif
 }
 
 // Global termination partials of outer iteration `it` (one workgroup): rk, sk summed over

@@ -9,9 +9,9 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--steps 5 --warmup 1 --no-cpu"
+ARGS="--no-cpu"   # bench.py defaults: a 10-step warmup launch, then the 10-step timed launch
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o bench --output-format csv -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o bench --output-format csv -- python3 bench.py $ARGS > $OUT/write.log 2>&1
-python3 tools/traffic.py $OUT $TAG > $OUT/traffic.log 2>&1
+python3 tools/traffic.py $OUT $TAG 10 > $OUT/traffic.log 2>&1
 echo PROFILE_DONE

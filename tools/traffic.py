@@ -13,6 +13,7 @@ import shutil
 import sys
 
 out, tag = sys.argv[1], sys.argv[2]
+steps_per_launch = int(sys.argv[3]) if len(sys.argv) > 3 else 10   # bench.py default: 10-step launches
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -47,7 +48,8 @@ if fetch and write:
     f = sum(fetch) / len(fetch)
     w = sum(write) / len(write)
     res.update(fetch_size_kb_raw=f, write_size_kb_raw=w,
-               hbm_bytes_per_launch=(2.0 * f + w) * 1024.0,
+               hbm_bytes_per_launch=(2.0 * f + w) * 1024.0, steps_per_launch=steps_per_launch,
+               hbm_bytes_per_step=(2.0 * f + w) * 1024.0 / steps_per_launch,
                note="traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE 1/2 correction)")
 json.dump(res, open(os.path.join(prof, f"traffic_{tag}.json"), "w"), indent=1)
 print(json.dumps(res))
