@@ -2193,7 +2193,11 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   int status_e = 0;
   Geo ge1, ge2;
   double c1x = 0.0, c1y = 0.0, c2x = 0.0, c2y = 0.0;
+#ifdef PIADMM_DIAG_NO_PAIR   // diagnostic timing build only: no pair QP code at all
+  if (false) {
+#else
   if (w == 0 && e >= 0) {
+#endif
     unsigned long long t0 = STAMP_T();
     ge1 = make_geo(S.xt + 0, A.spd[a0], c);
     ge2 = make_geo(S.xt + 3, A.spd[a0 + 1], c);
@@ -2331,7 +2335,11 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     if (!act && flag == 0 && !c.fixed_iters && !global) break;   // no edge ever: stop (:115-116)
     flag = 1;
     // -------- z-step + dual update on the colliding pair (casadi/main.py:121-162)
+#ifdef PIADMM_DIAG_NO_PAIR
+    if (false) {
+#else
     if (act && w == 0) {
+#endif
       unsigned long long t_z = STAMP_T();
       const bool tl = l <= H;
       double bx[2], by[2];
