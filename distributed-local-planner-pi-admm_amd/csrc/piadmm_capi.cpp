@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -206,6 +207,12 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   pd::DevArgs& A = h->a;
   A = pd::DevArgs{};
   A.cfg = h->cfg;
+  // PIADMM_PAIR_SOLVER=admm: pair QPs skip the dual active set and take the ADMM + PDAS path
+  // (the fallback), so that tests can check both solvers against each other and the oracle
+  {
+    const char* ps = std::getenv("PIADMM_PAIR_SOLVER");
+    A.pair_gi = (ps && std::strcmp(ps, "admm") == 0) ? 0 : 1;
+  }
   A.N = N;
   A.E = n_edges;
   A.C = h->C;
@@ -261,6 +268,7 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.Kx_cache, (size_t)N * H * H);
   rc |= dalloc(h, &A.xcache_rho, (size_t)N);
   rc |= dalloc(h, &A.ecache, E);
+  rc |= dalloc(h, &A.gi_ws, E * (2 + pd::WAVE));
 #ifdef PIADMM_STAMPS
   rc |= dalloc(h, &A.stamps, C * 32);
 #endif

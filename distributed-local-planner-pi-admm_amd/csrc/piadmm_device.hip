@@ -393,6 +393,8 @@ struct QP {
   int ycap;               // pair: columns Y holds
   bool scaled;            // Ruiz scaling computed (the pair computes it only when ADMM is needed)
   const double* Kcache;   // x-step: HBM copy of K_s^-1, loaded into K only when ADMM is needed
+  int* gws;               // pair: HBM warm working set of the dual active set (GI_WS ints)
+  int tstep;              // MPC step index (warm-set bookkeeping)
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
   // Row s of vehicle v = s / 2: even = box (lanes < H), odd = rate (lanes < H-1), 4 = hinge
@@ -1390,6 +1392,13 @@ __device__ __forceinline__ void pinv_row(const QP<NV>& P, int row, double sg, do
 }
 
 constexpr int GI_MAX_STEPS = 256;
+constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t, codes
+// Warm start (receding horizon): the previous MPC step's final active set, shifted one time
+// slot (tools/gi_sim.py + the warm-start prototype: 28 -> 3.6 GI steps per bench pair QP),
+// is appended row by row (dependent rows skipped), its equality-constrained minimiser formed
+// and constraints with negative (or beyond-cap) multipliers dropped until the start is dual
+// feasible -- the state GI requires -- before the usual adds.  Any starting set is only a
+// guess: the minimiser and its certificate do not depend on it.
 template <int NV>
 __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x, double* y, int& nsteps) {
   constexpr int NR = QP<NV>::NR;
@@ -1407,8 +1416,162 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
   for (int v = 0; v < NV; ++v) xc[v] = x0[v] = -x0[v];
   int m = 0, wbits = 0;
   double ua = 0.0, linv = 0.0;     // lane a < m: multiplier and 1/L_aa of active constraint a
-  bool done = false;
-  while (!done) {
+
+  // y_p = P^-1 n_p (lane = variable), A y_p to vb_ax; returns n_p' P^-1 n_p
+  auto prep = [&](int pc, double* yp) -> double {
+    const int prow = pc >> 1;
+    const double sgp = (pc & 1) ? -1.0 : 1.0;
+    pinv_row(P, prow, sgp, yp);
+    double ay[NR];
+    A_mul(P, yp, ay);
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ay[s];
+    }
+    wsync();
+    return sgp * vb_ax[prow];
+  };
+  // w = L^-1 (N y_p) for the current active set (lane a < m)
+  auto fwd = [&]() -> double {
+    const int myc = (l < m) ? wc[l] : 0;
+    const double va = (l < m) ? ((myc & 1) ? -1.0 : 1.0) * vb_ax[myc >> 1] : 0.0;   // n_a' y_p
+    return tri_fwd(L, ld, linv, va, m);
+  };
+  // append constraint pc: L row m = (w', sqrt(lpp2)), Y column m = y_p
+  auto append = [&](int pc, const double* yp, double w, double lpp2, double u0) {
+    const int prow = pc >> 1, ps = prow / H, pk = prow - ps * H;
+    const double lmm = sqrt(lpp2);
+    if (l < m) L[m * ld + l] = w;
+    if (l == m) {
+      L[m * ld + m] = lmm;
+      linv = 1.0 / lmm;
+      ua = u0;
+      wc[m] = pc;
+    }
+    if (l < H) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) Y[m * H2 + v * H + l] = yp[v];
+    }
+    if (l == pk) wbits |= 1 << (2 * ps + (pc & 1));
+    ++m;
+    if (P.gmem) gsync();
+    else wsync();
+  };
+  // drop active constraint k: delete row/column k of L, rank-one update of the trailing block
+  // with the deleted column, compact L, Y, codes and multipliers
+  auto drop = [&](int k) {
+    const int kc = rdli((l < m) ? wc[l] : 0, k);
+    if (l == (kc >> 1) % H) wbits &= ~(1 << (2 * ((kc >> 1) / H) + (kc & 1)));
+    double xv = (l > k && l < m) ? L[l * ld + k] : 0.0;
+    for (int j = k + 1; j < m; ++j) {
+      const double Ljj = L[j * ld + j];
+      const double xj = rdl(xv, j);
+      const double rr = sqrt(Ljj * Ljj + xj * xj);
+      const double cc = rr / Ljj, sn = xj / Ljj;
+      if (l == j) L[j * ld + j] = rr;
+      if (l > j && l < m) {
+        const double Lij = (L[l * ld + j] + sn * xv) / cc;
+        xv = cc * xv - sn * Lij;
+        L[l * ld + j] = Lij;
+      }
+    }
+    wsync();
+    // compact: row i <- row i+1 (i >= k), column j <- column j+1 (j >= k); lane = column
+    for (int i = k; i < m - 1; ++i) {
+      const double v = (l < m - 1) ? L[(i + 1) * ld + l + (l >= k ? 1 : 0)] : 0.0;
+      wsync();
+      if (l <= i) L[i * ld + l] = v;
+      wsync();
+    }
+    const int cnext = (l + 1 < m) ? wc[l + 1] : 0;
+    wsync();
+    if (l >= k && l < m - 1) wc[l] = cnext;
+    const double un = shdn(ua, 1);
+    if (l >= k) ua = (l < m - 1) ? un : 0.0;
+    for (int a = k; a < m - 1; ++a) {
+      if (l < H) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) Y[a * H2 + v * H + l] = Y[(a + 1) * H2 + v * H + l];
+      }
+    }
+    --m;
+    if (P.gmem) gsync();
+    else wsync();
+    linv = (l < m) ? 1.0 / L[l * ld + l] : 0.0;
+  };
+  // multipliers of the equality-constrained minimiser on the active set (signed normals):
+  // lam = S^-1 (N x0 - b); kernel multiplier of row a = sign_a * lam_a, GI multiplier -lam_a
+  auto eqp_lam = [&]() -> double {
+    double ax0[NR];
+    A_mul(P, x0, ax0);
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ax0[s] - P.lo(s);   // lower-side residual
+    }
+    wsync();
+    double rhs = 0.0;
+    if (l < m) {
+      const int myc = wc[l], rw = myc >> 1, rs = rw / H;
+      // upper side (box / rate rows only, uniform bounds): -(a'x0 - hi)
+      const double blo = (rs & 1) ? -P.dumax : -P.umax;
+      rhs = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
+    }
+    return tri_bwd(L, ld, linv, tri_fwd(L, ld, linv, rhs, m), m);
+  };
+  auto x_of = [&](double lam) {
+    const int lc = (l < H) ? l : 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xc[v] = x0[v];
+    for (int a = 0; a < m; ++a) {
+      const double la = rdl(lam, a);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) xc[v] -= la * Y[a * H2 + v * H + lc];
+    }
+  };
+
+  // ---- warm start from the stored active set (this step's, or the previous step's shifted)
+  if (P.gws) {
+    const int gm = P.gws[0], gt = P.gws[1];
+    const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
+    if ((same || prev) && gm > 0 && gm <= WAVE) {
+      int code = (l < gm) ? P.gws[2 + l] : -1;
+      if (prev && code >= 0) {
+        const int row = code >> 1, s0 = row / H, k = row - s0 * H;
+        const bool keep = P.hinge(s0) ? (k >= 2) : (k >= 1);
+        code = keep ? 2 * (row - 1) + (code & 1) : -1;
+      }
+      if (NV == 2 && P.g1 == 0.0 && P.g2 == 0.0 && code >= 0 && P.hinge((code >> 1) / H)) code = -1;
+      for (int i = 0; i < gm; ++i) {
+        const int pc = rdli(code, i);
+        if (pc < 0 || m >= cap) continue;
+        double yp[NV];
+        const double spp = prep(pc, yp);
+        const double w = fwd();
+        const double lpp2 = spp - wsum(w * w);
+        if (lpp2 > DEP_TOL * spp) append(pc, yp, w, lpp2, 0.0);   // else dependent: skip
+      }
+      // dual feasibility: drop the most negative (or beyond-cap hinge) multiplier until none
+      double lam = 0.0;
+      while (m > 0) {
+        lam = eqp_lam();
+        const int myc = (l < m) ? wc[l] : 0;
+        const double u = -lam;
+        double sc = 0.0;
+        if (l < m) {
+          if (u < 0.0) sc = u;
+          else if (P.hinge((myc >> 1) / H) && u > P.beta) sc = P.beta - u;
+        }
+        const double smin = wmin(sc);
+        if (!(smin < 0.0)) break;
+        const int k = __ffsll((unsigned long long)__ballot(l < m && sc == smin)) - 1;
+        drop(k);
+      }
+      ua = (l < m) ? -lam : 0.0;
+      x_of(lam);
+    }
+  }
+
+  while (true) {
     unsigned long long t_gs = STAMP_T();
     // ---- most violated constraint outside the active set
     double ax[NR];
@@ -1433,29 +1596,16 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
     const int pl = __ffsll((unsigned long long)__ballot(code >= 0 && best == bmin)) - 1;
     const int pc = rdli(code, pl);
     const int prow = pc >> 1, pside = pc & 1, ps = prow / H, pk = prow - ps * H;
-    const double sgp = pside ? -1.0 : 1.0;
     const bool phinge = P.hinge(ps);
     double sp = rdl(pside ? P.hi(ps) - ax[ps] : ax[ps] - P.lo(ps), pk);   // slack of p (< 0)
     double yp[NV];
-    pinv_row(P, prow, sgp, yp);
-    {
-      double ay[NR];
-      A_mul(P, yp, ay);
-      if (l < H) {
-#pragma unroll
-        for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ay[s];
-      }
-    }
-    wsync();
-    const double spp = sgp * vb_ax[prow];  // n_p' P^-1 n_p
+    const double spp = prep(pc, yp);       // n_p' P^-1 n_p
     double up = 0.0;
     STAMP_ADD(ST_GI_SEARCH, t_gs);
     while (true) {
       if (++nsteps > GI_MAX_STEPS) return false;
       unsigned long long t_gv = STAMP_T();
-      const int myc = (l < m) ? wc[l] : 0;
-      const double va = (l < m) ? ((myc & 1) ? -1.0 : 1.0) * vb_ax[myc >> 1] : 0.0;   // n_a' y_p
-      const double w = tri_fwd(L, ld, linv, va, m);
+      const double w = fwd();
       const double r = tri_bwd(L, ld, linv, w, m);
       // z = y_p - Y r
       double z[NV];
@@ -1483,6 +1633,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
       unsigned long long t_gu = STAMP_T();
       const double t2 = (lpp2 > DEP_TOL * spp) ? -sp / lpp2 : INFINITY;
       // dual step limits: an active multiplier reaching 0 (drop) or a hinge one reaching beta
+      const int myc = (l < m) ? wc[l] : 0;
       const bool hin_a = (l < m) && P.hinge((myc >> 1) / H);
       const double tdrop = (l < m && r > 0.0) ? ua / r : INFINITY;
       const double tcap = (hin_a && r < 0.0) ? (P.beta - ua) / (-r) : INFINITY;
@@ -1498,101 +1649,22 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
       if (l < m) ua -= t * r;
       up += t;
       if (t2 <= t1) {
-        // ---- add p: L row m = (w', sqrt(lpp2)), Y column m = y_p
         if (m >= cap) return false;
-        const double lmm = sqrt(lpp2);
-        if (l < m) L[m * ld + l] = w;
-        if (l == m) {
-          L[m * ld + m] = lmm;
-          linv = 1.0 / lmm;
-          ua = up;
-          wc[m] = pc;
-        }
-        if (l < H) {
-#pragma unroll
-          for (int v = 0; v < NV; ++v) Y[m * H2 + v * H + l] = yp[v];
-        }
-        if (l == pk) wbits |= 1 << (2 * ps + pside);
-        ++m;
-        if (P.gmem) gsync();
-        else wsync();
+        append(pc, yp, w, lpp2, up);
         STAMP_ADD(ST_GI_UPD, t_gu);
         break;
       }
-      // ---- drop active constraint k: delete row/column k of L, rank-one update of the
-      // trailing block with the deleted column, compact L, Y, codes and multipliers
-      const int k = __ffsll((unsigned long long)__ballot(l < m && tdrop == t1)) - 1;
-      const int kc = rdli(myc, k);
-      if (l == (kc >> 1) % H) wbits &= ~(1 << (2 * ((kc >> 1) / H) + (kc & 1)));
-      {
-        double xv = (l > k && l < m) ? L[l * ld + k] : 0.0;
-        for (int j = k + 1; j < m; ++j) {
-          const double Ljj = L[j * ld + j];
-          const double xj = rdl(xv, j);
-          const double rr = sqrt(Ljj * Ljj + xj * xj);
-          const double cc = rr / Ljj, sn = xj / Ljj;
-          if (l == j) L[j * ld + j] = rr;
-          if (l > j && l < m) {
-            const double Lij = (L[l * ld + j] + sn * xv) / cc;
-            xv = cc * xv - sn * Lij;
-            L[l * ld + j] = Lij;
-          }
-        }
-        wsync();
-        // compact: row i <- row i+1 (i >= k), column j <- column j+1 (j >= k); lane = column
-        for (int i = k; i < m - 1; ++i) {
-          const double v = (l < m - 1) ? L[(i + 1) * ld + l + (l >= k ? 1 : 0)] : 0.0;
-          wsync();
-          if (l <= i) L[i * ld + l] = v;
-          wsync();
-        }
-        const int cnext = (l + 1 < m) ? wc[l + 1] : 0;
-        wsync();
-        if (l >= k && l < m - 1) wc[l] = cnext;
-        const double un = shdn(ua, 1);
-        if (l >= k) ua = (l < m - 1) ? un : 0.0;
-        for (int a = k; a < m - 1; ++a) {
-          if (l < H) {
-#pragma unroll
-            for (int v = 0; v < NV; ++v) Y[a * H2 + v * H + l] = Y[(a + 1) * H2 + v * H + l];
-          }
-        }
-        --m;
-        if (P.gmem) gsync();
-        else wsync();
-        linv = (l < m) ? 1.0 / L[l * ld + l] : 0.0;
-      }
+      drop(__ffsll((unsigned long long)__ballot(l < m && tdrop == t1)) - 1);
       STAMP_ADD(ST_GI_UPD, t_gu);
     }
   }
   // ---- exact solution of the final active set (the reduced solve with this factor):
   // lam = S^-1 (N x0 - b), x = x0 - Y lam;  kernel multipliers y_a = sign_a * lam_a
   {
-    double ax0[NR];
-    A_mul(P, x0, ax0);
-    if (l < H) {
-#pragma unroll
-      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ax0[s] - P.lo(s);   // lower-side residual
-    }
-    wsync();
+    const double lam = eqp_lam();
+    x_of(lam);
     const int myc = (l < m) ? wc[l] : 0;
-    const int rw = myc >> 1, rs = rw / H;
-    double rhs = 0.0;
-    if (l < m) {
-      // upper side (box / rate rows only, uniform bounds): -(a'x0 - hi)
-      const double blo = (rs & 1) ? -P.dumax : -P.umax;
-      rhs = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
-    }
-    const double lam = tri_bwd(L, ld, linv, tri_fwd(L, ld, linv, rhs, m), m);
-    double xs[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) xs[v] = x0[v];
-    const int lc = (l < H) ? l : 0;
-    for (int a = 0; a < m; ++a) {
-      const double la = rdl(lam, a);
-#pragma unroll
-      for (int v = 0; v < NV; ++v) xs[v] -= la * Y[a * H2 + v * H + lc];
-    }
+    const int rw = myc >> 1;
     wsync();
     if (l < H) {
 #pragma unroll
@@ -1602,7 +1674,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
     if (l < m) vb_ax[rw] = (myc & 1) ? -lam : lam;
     wsync();
 #pragma unroll
-    for (int v = 0; v < NV; ++v) x[v] = (l < H) ? xs[v] : 0.0;
+    for (int v = 0; v < NV; ++v) x[v] = (l < H) ? xc[v] : 0.0;
 #pragma unroll
     for (int s = 0; s < NR; ++s) {
       const bool lo_in = (wbits >> (2 * s)) & 1, hi_in = (wbits >> (2 * s + 1)) & 1;
@@ -1610,6 +1682,14 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
       if (P.hinge(s)) lab[s] = lo_in ? HKINK : HZERO;
       else lab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
       if (!P.valid(s)) lab[s] = 0;
+    }
+    // this step's active set: the next solve's warm start
+    if (P.gws) {
+      if (l < m) P.gws[2 + l] = myc;
+      if (l == 0) {
+        P.gws[0] = m;
+        P.gws[1] = P.tstep;
+      }
     }
     wsync();
   }
@@ -2229,7 +2309,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     qe.xld = 0;
     // dual active-set columns in the K_s^-1 region (4H^2 doubles, or 2H^2 with fp32 images)
     qe.Y = Ke ? Ke : (double*)Kef;
-    qe.ycap = ((Ke ? 4 : 2) * H * H) / (2 * H);
+    qe.ycap = A.pair_gi ? ((Ke ? 4 : 2) * H * H) / (2 * H) : 0;
+    qe.gws = A.gi_ws + (size_t)e * GI_WS;
+    qe.tstep = t;
     // Ke doubles as the H x 2H staging of the per-scenario pair tables; with fp32 images in
     // LDS mode the fp32 region (2H^2 doubles of space) takes that role
     setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke ? Ke : (double*)Kef, deff);

@@ -23,6 +23,7 @@ enum HingeLab : signed char { HZERO = 0, HKINK = 1, HLINEAR = 2 };   // hinge ro
 struct DevArgs {
   piadmm_config_t cfg;
   int N, E, C, T;
+  int pair_gi;              // 1: pair QPs try the dual active set first (env PIADMM_PAIR_SOLVER)
   // scenario (read-only during a step)
   const double* spd;        // N
   const double* ref;        // N*2*T
@@ -71,6 +72,7 @@ struct DevArgs {
   double* Kx_cache;         // N*H*H agent K_s^-1 for the penalty xcache_rho[a] (per scenario)
   double* xcache_rho;       // N   penalty of the cached agent setup (NaN: none)
   int* ecache;              // E   1 when the pair's speed-only tables are built
+  int* gi_ws;               // E*(2+64) the pair's last dual active set: m, step t, codes
 };
 
 // Big mode: rows of the per-wave x-step factor scratch (working sets of up to H + 2 rows:

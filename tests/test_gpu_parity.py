@@ -233,6 +233,34 @@ def test_persistent_launch_equals_single_steps(Solver, H, fixed):
         assert s2.counters()["inexact"] == 0
 
 
+@pytest.mark.parametrize("H", [20, 30, 40])
+def test_pair_solvers_agree(Solver, H, monkeypatch):
+    """The pair QP's dual active set (default) and its ADMM + PDAS fallback
+    (PIADMM_PAIR_SOLVER=admm) certify the same minimiser: identical iteration counts and
+    residual histories, states equal to 1e-10, and the oracle agrees with both."""
+    cfg = config.matlab_pi(H=H)
+    scn = scenario.tiled(12, H, n_steps=8, perturb=True, seed=11)
+    orc = O.Oracle(cfg, scn)
+    with Solver(cfg, scn) as s_gi:
+        monkeypatch.setenv("PIADMM_PAIR_SOLVER", "admm")
+        s_admm = Solver(cfg, scn)
+        monkeypatch.delenv("PIADMM_PAIR_SOLVER")
+        try:
+            for _ in range(6):
+                ro, r1, r2 = orc.mpc_step(), s_gi.mpc_step(), s_admm.mpc_step()
+                np.testing.assert_array_equal(r1.iters, r2.iters)
+                np.testing.assert_array_equal(r1.iters, ro.iters)
+                np.testing.assert_allclose(r1.xt, r2.xt, rtol=1e-10, atol=1e-10)
+                np.testing.assert_allclose(r1.xt, ro.xt, rtol=1e-8, atol=1e-8)
+                np.testing.assert_allclose(r1.u, ro.u, rtol=0, atol=1e-8)
+                assert np.all(r1.status == 0) and np.all(r2.status == 0)
+            c1, c2 = s_gi.counters(), s_admm.counters()
+            assert c1["z_qps"] == c2["z_qps"] > 0
+            assert c1["admm_z"] == 0 and c2["admm_z"] > 0     # GI certified every pair QP
+        finally:
+            s_admm.close()
+
+
 def test_errors_are_loud(Solver):
     with pytest.raises(_lib.PiadmmError, match="H must be"):
         Solver(config.matlab_pi(H=64), scenario.tiled(1, 64, n_steps=1))
