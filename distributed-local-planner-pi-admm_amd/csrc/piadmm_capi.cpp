@@ -270,7 +270,7 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.ecache, E);
   rc |= dalloc(h, &A.gi_ws, E * (2 + pd::WAVE));
 #ifdef PIADMM_STAMPS
-  rc |= dalloc(h, &A.stamps, C * 32);
+  rc |= dalloc(h, &A.stamps, C * 64);
 #endif
   if (rc) return PIADMM_E_HIP;
   HIPCHK(h, hipMemcpyAsync(d_spd, spd, N * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -522,8 +522,8 @@ int32_t piadmm_global_resid(piadmm_handle_t h, double* resid_out, int32_t* iters
 int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n) {
   if (!h || !out) return fail(h, PIADMM_E_ARG, "null argument");
   if (!h->a.stamps) return fail(h, PIADMM_E_STATE, "library built without PIADMM_STAMPS");
-  if (n < h->C * 32) return fail(h, PIADMM_E_ARG, "buffer too small");
-  HIPCHK(h, hipMemcpy(out, h->a.stamps, (size_t)h->C * 32 * 8, hipMemcpyDeviceToHost));
+  if (n < h->C * 64) return fail(h, PIADMM_E_ARG, "buffer too small");
+  HIPCHK(h, hipMemcpy(out, h->a.stamps, (size_t)h->C * 64 * 8, hipMemcpyDeviceToHost));
   return PIADMM_OK;
 }
 
@@ -532,7 +532,7 @@ int32_t piadmm_reset_counters(piadmm_handle_t h) {
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
   HIPCHK(h, hipSetDevice(h->cfg.device));
   HIPCHK(h, hipMemsetAsync(h->a.counters, 0, (size_t)h->C * 8 * 8, h->stream));
-  if (h->a.stamps) HIPCHK(h, hipMemsetAsync(h->a.stamps, 0, (size_t)h->C * 32 * 8, h->stream));
+  if (h->a.stamps) HIPCHK(h, hipMemsetAsync(h->a.stamps, 0, (size_t)h->C * 64 * 8, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PIADMM_OK;
 }

@@ -28,7 +28,7 @@ namespace pd {
 // cycles accumulate in LDS (one ds_add_u64 per stamp, lane 0) and are flushed to g_stamps
 // once per launch, so that a stamp costs an LDS atomic, not a global one
 __device__ unsigned long long* g_stamps;
-__shared__ unsigned long long s_stamps[32];
+__shared__ unsigned long long s_stamps[64];
 #define STAMP_T() __builtin_amdgcn_s_memtime()
 #define STAMP_ADD(slot, t0)                                                                   \
   do {                                                                                        \
@@ -42,7 +42,8 @@ __shared__ unsigned long long s_stamps[32];
 enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL, ST_ZSTEP, ST_ZQP, ST_ZRED,
                  ST_KERNEL, ST_RED_GEMV, ST_RED_S, ST_RED_CHOL, ST_RED_X, ST_ADMM, ST_XQ, ST_TERM,
                  ST_SZ_RUIZ, ST_SZ_KMAT, ST_SZ_GJ, ST_SZ_PRE, ST_ZR_GEMV, ST_ZR_S, ST_ZR_CHOL, ST_ZR_X,
-                 ST_ZR_SOLVE, ST_XR_SOLVE, ST_ZKKT, ST_XKKT, ST_GI_SEARCH, ST_GI_SOLVE, ST_GI_UPD };
+                 ST_ZR_SOLVE, ST_XR_SOLVE, ST_ZKKT, ST_XKKT, ST_GI_SEARCH, ST_GI_SOLVE, ST_GI_UPD,
+                 ST_SYNC_A, ST_TERMW, ST_SYNC_B, ST_RSX_PRE, ST_QEPI, ST_ROUND, NSTAMP = 64 };
 
 // ============================================================ wave primitives
 __device__ __forceinline__ int lid() { return (int)__lane_id(); }
@@ -1155,6 +1156,7 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
 
 __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed char* lab, double* x, double* y) {
   const int l = lid(), H = P.H;
+  unsigned long long t_pre = STAMP_T();
   double* vb_q = P.vb;             // [0,64) q
   double* vb_b = P.vb + 64;        // [64,128) rhs b of W rows
   double* vb_lam = P.vb + 128;     // [128,192)
@@ -1195,6 +1197,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
     if (l == 0) P.fstate[0] = m;
     wsync();
   }
+  STAMP_ADD(ST_RSX_PRE, t_pre);
   unsigned long long t_rs = STAMP_T();
   // one fused pass: x = -G q + g (lane = variable), lam = -X q - beta (lane = W row)
   double ag = 0.0, ax = 0.0;
@@ -1847,6 +1850,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       }
     }
   }
+  unsigned long long t_ep = STAMP_T();
   int st = PIADMM_QP_OK;
   if (ok) {
     // warm ADMM state at the exact optimum
@@ -1873,6 +1877,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
     fin &= isfinite(x_out[v]);
   }
   if (!wall(fin)) st |= PIADMM_QP_NAN;
+  if (NV == 1) STAMP_ADD(ST_QEPI, t_ep);
   return st;
 }
 // ============================================================ per-step setup
@@ -2386,7 +2391,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       ++n_xqp;
       n_inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
       warm_x = true;
+      unsigned long long t_rd = STAMP_T();
       const double u = around(ustar[0], c.round_decimals);
+      STAMP_ADD(ST_ROUND, t_rd);
       double px, py, pth;
       unsigned long long t_r = STAMP_T();
 #ifdef PIADMM_DIAG_NO_ROLL  // diagnostic timing build only: skip the rollout
@@ -2402,7 +2409,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       if (l < H) S.u[w * H + l] = u;
       STAMP_ADD(ST_XSTEP, t_xs);
     }
+    unsigned long long t_sa = STAMP_T();
     __syncthreads();
+    STAMP_ADD(ST_SYNC_A, t_sa);
     // -------- collision graph (casadi/main.py:110-118), computed by every wave
     act = false;
     if (e >= 0 && na == 2) {
@@ -2516,24 +2525,36 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       }
       STAMP_ADD(ST_ZSTEP, t_z);
     }
+    // -------- termination (casadi/main.py:164-181; MATLAB :191-210).  Wave 0 (which wrote
+    // S.sc) records the residuals and, unless the component stops, last_iter_hat_pos before
+    // the barrier; after it every wave takes the same stop decision from S.sc.  One barrier per
+    // half-iteration: S.sc is rewritten only after the next iteration's first barrier.
+    if (w == 0) {
+      unsigned long long t_tw = STAMP_T();
+      wsync();
+      const double rk0 = act ? S.sc[0] : 0.0;
+      const double sk0 = act ? S.sc[1] : 0.0;
+      const double dc0 = act ? S.sc[2] : dis_chk;
+      if (l == 0) {
+        resid[2 * it + 0] = rk0;
+        resid[2 * it + 1] = sk0;
+      }
+      const bool stop0 = !c.fixed_iters && !global && rk0 <= c.eps_pri && sk0 <= c.eps_dual &&
+                         (!c.term_dist_check || dc0 > deff);
+      if (!stop0 && !c.alias_dual_residual)
+        for (int i = l; i < 4 * H1; i += WAVE) S.last[i] = S.hat[i];
+      STAMP_ADD(ST_TERMW, t_tw);
+    }
+    unsigned long long t_sb = STAMP_T();
     __syncthreads();
-    // -------- termination (casadi/main.py:164-181; MATLAB :191-210)
+    STAMP_ADD(ST_SYNC_B, t_sb);
     const double rk = act ? S.sc[0] : 0.0;
     const double sk = act ? S.sc[1] : 0.0;
     if (act) dis_chk = S.sc[2];
-    if (threadIdx.x == 0) {
-      resid[2 * it + 0] = rk;
-      resid[2 * it + 1] = sk;
-    }
     if (!c.fixed_iters && !global && rk <= c.eps_pri && sk <= c.eps_dual &&
         (!c.term_dist_check || dis_chk > deff))
       break;
-    if (c.alias_dual_residual) {
-      aliased = 1;
-    } else {
-      for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) S.last[i] = S.hat[i];
-    }
-    __syncthreads();
+    if (c.alias_dual_residual) aliased = 1;
   }
   __syncthreads();
   STAMP_ADD(ST_KERNEL, t_k);
@@ -2661,7 +2682,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 template <bool BIG>
 __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
 #ifdef PIADMM_STAMPS
-  if (threadIdx.x < 32) s_stamps[threadIdx.x] = 0ull;
+  if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
   __syncthreads();
 #endif
   for (int k = 0; k < nsteps; ++k) {
@@ -2669,7 +2690,7 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t0, int n
     __syncthreads();
   }
 #ifdef PIADMM_STAMPS
-  if (threadIdx.x < 32 && g_stamps) atomicAdd(&g_stamps[blockIdx.x * 32 + threadIdx.x], s_stamps[threadIdx.x]);
+  if (threadIdx.x < 64 && g_stamps) atomicAdd(&g_stamps[blockIdx.x * 64 + threadIdx.x], s_stamps[threadIdx.x]);
 #endif
 }
 

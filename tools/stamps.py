@@ -8,7 +8,7 @@ from piadmm import config, scenario
 from piadmm.solver import PI_ADMM_MI355X
 NAMES = ['setup_x', 'setup_z', 'xstep', 'xqp', 'xred', 'xroll', 'zstep', 'zqp', 'zred', 'kernel',
          'red_gemv', 'red_S', 'red_chol', 'red_x', 'admm', 'xq', 'term', 'sz_ruiz', 'sz_kmat', 'sz_gj', 'sz_pre',
-         'zr_gemv', 'zr_S', 'zr_chol', 'zr_x', 'zr_solve', 'xr_solve', 'zkkt', 'xkkt', 'gi_search', 'gi_solve', 'gi_upd']
+         'zr_gemv', 'zr_S', 'zr_chol', 'zr_x', 'zr_solve', 'xr_solve', 'zkkt', 'xkkt', 'gi_search', 'gi_solve', 'gi_upd', 'sync_a', 'term_w0', 'sync_b', 'rsx_pre', 'qp_epi', 'round']
 tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
@@ -18,9 +18,9 @@ s = PI_ADMM_MI355X(cfg, scn)
 s.reset_counters()
 ms = s.time_steps(0, steps)
 cnt = s.counters()
-buf = (ctypes.c_uint64 * (s.C * 32))()
-s._check(s.lib.piadmm_debug_stamps(s._h, buf, s.C * 32))
-st = np.array(buf, dtype=np.float64).reshape(s.C, 32)
+buf = (ctypes.c_uint64 * (s.C * 64))()
+s._check(s.lib.piadmm_debug_stamps(s._h, buf, s.C * 64))
+st = np.array(buf, dtype=np.float64).reshape(s.C, 64)
 print(f"tiles={tiles} H={H} steps={steps} event_ms={ms:.3f} counters={cnt}")
 tot = st[:, 9].mean()
 for i, n in enumerate(NAMES):

@@ -12,13 +12,13 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 cfg = config.matlab_pi(H=H, fixed_iters=1, max_outer=100)
 scn = scenario.tiled(128, H, n_steps=steps + 2)
 s = PI_ADMM_MI355X(cfg, scn)
-buf = (ctypes.c_uint64 * (s.C * 32))()
+buf = (ctypes.c_uint64 * (s.C * 64))()
 prev = np.zeros(s.C)
 rows = []
 for t in range(steps):
     ms = s.time_steps(t, 1)
-    s._check(s.lib.piadmm_debug_stamps(s._h, buf, s.C * 32))
-    k = np.array(buf, dtype=np.float64).reshape(s.C, 32)[:, 9]
+    s._check(s.lib.piadmm_debug_stamps(s._h, buf, s.C * 64))
+    k = np.array(buf, dtype=np.float64).reshape(s.C, 64)[:, 9]
     rows.append(k - prev)
     prev = k
     print(f"t={t:2d} {ms:6.2f} ms  max {rows[-1].max():10.0f} mean {rows[-1].mean():10.0f} argmax {rows[-1].argmax()}", flush=True)
