@@ -190,10 +190,11 @@ def main():
     outer_total = world * cnt["outer_iters"] / max(solver.C, 1)      # job iterations x ranks
     value = outer_total / wall
     # k_mpc_step launches in the timed region: one persistent launch per steps_per_launch()
-    # MPC steps (fixed iterations), or one per outer iteration plus one per step (natural
-    # global termination, where each launch's share of the device time is taken as equal)
+    # MPC steps (fixed iterations; natural global termination on one rank, where the stop
+    # test runs in-kernel behind a grid barrier), or -- natural termination across ranks --
+    # one per outer iteration plus one per step (each launch's share of the time taken equal)
     spl = solver.steps_per_launch()
-    n_launch = -(-K // spl) if not args.natural else int(cnt["outer_iters"] / max(solver.C, 1)) + K
+    n_launch = -(-K // spl) if spl > 1 else int(cnt["outer_iters"] / max(solver.C, 1)) + K
     avg_launch_s = (ev_ms / 1e3) / n_launch
     bytes_launch = algorithmic_bytes(cnt, H) / n_launch
     achieved = bytes_launch / avg_launch_s / 1e9
@@ -222,14 +223,15 @@ def main():
             "agents_per_gpu": 2 * N_TILES, "horizon": H,
             "outer_iters_per_step": outer_total / world / K,
             "parallelism": f"components sharded over {world} GPU(s); " + (
-                "one RCCL all-reduce of the termination partials per outer iteration" if args.natural else
+                ("one RCCL all-reduce of the termination partials per outer iteration" if world > 1 else
+                 "stop test in-kernel behind a grid barrier (cooperative launch)") if args.natural else
                 "one RCCL all-reduce of the residual history per MPC step") + (" (single rank: none)" if world == 1 else ""),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
             "kernel": "pd::k_mpc_step", "avg_launch_ms": avg_launch_s * 1e3,
-            "steps_per_launch": spl if not args.natural else None, "launches": n_launch,
+            "steps_per_launch": spl, "launches": n_launch,
             "algorithmic_bytes_per_launch": bytes_launch,
             "note": "latency-bound: one dependent ADMM/PDAS chain per wave; see DESIGN.md",
         },

@@ -34,6 +34,7 @@ struct piadmm_ctx {
   std::vector<double> ghist;     // global (rk, sk) history of the last step
   int giters = 0;
   int step_cap = 1;              // MPC steps per persistent launch (resid slots)
+  bool coop = false;             // term_global natural termination decided in-kernel (one rank)
 };
 
 namespace {
@@ -269,6 +270,9 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.xcache_rho, (size_t)N);
   rc |= dalloc(h, &A.ecache, E);
   rc |= dalloc(h, &A.gi_ws, E * (2 + pd::WAVE));
+  rc |= dalloc(h, &A.gpart, (size_t)2 * C * 5);
+  rc |= dalloc(h, &A.ghist, (size_t)h->step_cap * std::max(h->cfg.max_outer, 1) * 2);
+  rc |= dalloc(h, &A.giters, (size_t)h->step_cap);
 #ifdef PIADMM_STAMPS
   rc |= dalloc(h, &A.stamps, C * 64);
 #endif
@@ -299,6 +303,15 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   A.comp_edge = d_ce;
   A.edges = d_ed;
   A.nbr_cnt = d_nb;
+  // natural global termination without a communicator (one rank): the stop test in-kernel
+  // behind a grid barrier, when every workgroup can be resident (cooperative launch);
+  // PIADMM_NO_COOP=1 keeps the host-decided path (one launch per outer iteration, the path
+  // every rank of a sharded job takes, with the RCCL all-reduce) for tests and comparisons
+  {
+    const char* nc = std::getenv("PIADMM_NO_COOP");
+    h->coop = h->cfg.term_global && !h->cfg.fixed_iters && !(nc && nc[0] == '1') &&
+              pd::coop_fits(A, h->cfg.device);
+  }
   h->have_scn = true;
   return PIADMM_OK;
 }
@@ -310,6 +323,7 @@ int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
   HIPCHK(h, hipMemcpyAsync(h->a.xt, xt, (size_t)h->N * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
   // a new state breaks the receding-horizon sequence: no label warm start for the next step
   HIPCHK(h, hipMemsetAsync(h->a.warm_ok, 0, (size_t)h->N * sizeof(int), h->stream));
+  if (h->E) HIPCHK(h, hipMemsetAsync(h->a.gi_ws, 0, (size_t)h->E * (2 + pd::WAVE) * sizeof(int), h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PIADMM_OK;
 }
@@ -352,6 +366,23 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
       HIPCHK(h, hipMemcpyAsync(h->h_part, last, (size_t)2 * M * sizeof(double), hipMemcpyDeviceToHost, s));
       HIPCHK(h, hipStreamSynchronize(s));
       h->ghist.assign(h->h_part, h->h_part + 2 * M);
+    }
+    return PIADMM_OK;
+  }
+  if (h->coop && !h->comm &&
+      pd::launch_mpc_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL | pd::F_COOP, s) != 0) {
+    (void)hipGetLastError();       // the cooperative launch was refused: host-decided path from now on
+    h->coop = false;
+  }
+  if (h->coop && !h->comm) {
+    if (sync_outputs) {
+      int gi = 0;
+      HIPCHK(h, hipMemcpyAsync(h->h_part, h->a.ghist + (size_t)(n - 1) * 2 * M, (size_t)2 * M * sizeof(double),
+                               hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipMemcpyAsync(&gi, h->a.giters + (n - 1), sizeof(int), hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      h->ghist.assign(h->h_part, h->h_part + 2 * M);
+      h->giters = gi;
     }
     return PIADMM_OK;
   }
@@ -458,7 +489,8 @@ int32_t piadmm_n_components(piadmm_handle_t h) { return h && h->have_scn ? h->C 
 
 int32_t piadmm_steps_per_launch(piadmm_handle_t h) {
   if (!h || !h->have_scn) return 0;
-  return (h->cfg.term_global && !h->cfg.fixed_iters) ? 1 : h->step_cap;
+  if (h->cfg.term_global && !h->cfg.fixed_iters) return (h->coop && !h->comm) ? h->step_cap : 1;
+  return h->step_cap;
 }
 
 int32_t piadmm_get_counters(piadmm_handle_t h, uint64_t* out) {

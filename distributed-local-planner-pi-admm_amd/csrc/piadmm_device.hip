@@ -15,6 +15,7 @@
 // Schur complement S = A_W P^-1 A_W' (Cholesky in LDS) and accepted only when
 // the KKT conditions hold.  So the answer is the exact QP minimiser, not an
 // eps=1e-3 OSQP iterate.  tools/qp_sim.py is the NumPy prototype of this math.
+#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -2108,7 +2109,8 @@ __device__ __forceinline__ double delay_norm(const piadmm_config_t& c, double th
 // stop decision taken by the host from all-reduced partials, then a LAST launch with no
 // iterations for the outputs and the propagation.
 template <bool BIG>
-__device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot) {
+__device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
+                                              int& nbar) {
   extern __shared__ double lds[];
   __shared__ int s_int[NW * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
   const piadmm_config_t& c = A.cfg;
@@ -2171,6 +2173,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   const bool first = (flags & F_FIRST) != 0;
   const bool last_launch = (flags & F_LAST) != 0;
   const bool global = (flags & F_GLOBAL) != 0;
+  const bool coop = (flags & F_COOP) != 0;   // global stop decided in-kernel (cooperative launch)
+  int gflag = 0;                             // coop: some pair ever collided (casadi/main.py:115)
+  bool nanlast = (flags & F_NANLAST) != 0;
   // ---- seeds (casadi/main.py:48-49) and zero per-step state (:52-63)
   if ((int)threadIdx.x < na) {
     const int a = a0 + threadIdx.x;
@@ -2352,6 +2357,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   double* resid = A.resid + ((size_t)slot * A.C + ci) * c.max_outer * 2;   // slot: step of the launch
   if (first)
     for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
+  if (coop && ci == 0)
+    for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) A.ghist[(size_t)slot * 2 * c.max_outer + i] = NAN;
   // reference positions of the own agent at time lanes (fixed for the step)
   double rx_own = 0.0, ry_own = 0.0;
   if (w < na && l <= H) {
@@ -2554,6 +2561,48 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     if (!c.fixed_iters && !global && rk <= c.eps_pri && sk <= c.eps_dual &&
         (!c.term_dist_check || dis_chk > deff))
       break;
+    if (coop && !c.fixed_iters) {
+      // -------- global termination over all components, in-kernel (single rank): the
+      // partials of k_term_partials, one grid barrier, every workgroup sums them in the same
+      // order and applies the host's stop rules (piadmm_capi.cpp run_steps) identically.
+      // Double-buffered by the parity of the launch's barrier count (iterations and steps),
+      // so one barrier per iteration suffices; agent-scope atomic accesses keep the
+      // partials out of the non-coherent per-CU cache.
+      double* part = A.gpart + (size_t)(nbar & 1) * A.C * 5;
+      ++nbar;
+      if (threadIdx.x == 0) {
+        const bool seen = (e >= 0) && (dis_chk == dis_chk);
+        const double pv[5] = {rk, sk, (e >= 0 && act) ? 1.0 : 0.0, seen ? 1.0 : 0.0,
+                              (seen && !(dis_chk > deff)) ? 1.0 : 0.0};
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+          __hip_atomic_store(&part[ci * 5 + q], pv[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      cooperative_groups::this_grid().sync();
+      if (threadIdx.x == 0) {
+        double tot[5] = {0, 0, 0, 0, 0};
+        for (int k = 0; k < A.C; ++k)
+#pragma unroll
+          for (int q = 0; q < 5; ++q)
+            tot[q] += __hip_atomic_load(&part[k * 5 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) S.sc[16 + q] = tot[q];
+      }
+      __syncthreads();
+      const double trk = S.sc[16], tsk = S.sc[17], tact = S.sc[18], tseen = S.sc[19], tbad = S.sc[20];
+      __syncthreads();
+      if (tact == 0.0 && gflag == 0) {       // no pair collides anywhere: stop (:115-116)
+        nanlast = true;
+        break;
+      }
+      gflag = 1;
+      if (ci == 0 && threadIdx.x == 0) {
+        A.ghist[((size_t)slot * c.max_outer + it) * 2 + 0] = trk;
+        A.ghist[((size_t)slot * c.max_outer + it) * 2 + 1] = tsk;
+      }
+      const bool dist_ok = tseen > 0.0 && tbad == 0.0;
+      if (trk <= c.eps_pri && tsk <= c.eps_dual && (!c.term_dist_check || dist_ok)) break;
+    }
     if (c.alias_dual_residual) aliased = 1;
   }
   __syncthreads();
@@ -2589,7 +2638,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     }
     A.cst[(size_t)ci * 4 + 0] = flag;
     A.cst[(size_t)ci * 4 + 1] = aliased;
-    if ((flags & F_NANLAST) && iters > 0) {      // global stop at the collision test of this iteration
+    if (coop && ci == 0) A.giters[slot] = iters;
+    if (nanlast && iters > 0) {      // global stop at the collision test of this iteration
       resid[2 * (iters - 1) + 0] = NAN;
       resid[2 * (iters - 1) + 1] = NAN;
     }
@@ -2685,8 +2735,9 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t0, int n
   if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
   __syncthreads();
 #endif
+  int nbar = 0;   // grid barriers so far (coop): parity of the termination partials
   for (int k = 0; k < nsteps; ++k) {
-    mpc_step_body<BIG>(A, t0 + k, it0, it1, flags, k);
+    mpc_step_body<BIG>(A, t0 + k, it0, it1, flags, k, nbar);
     __syncthreads();
   }
 #ifdef PIADMM_STAMPS
@@ -2778,11 +2829,32 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return -1;
     attr[big] = sh;
   }
+  if (flags & F_COOP) {
+    // every workgroup must be resident for the grid barrier: the cooperative launch fails
+    // (and the caller falls back to host-decided termination) rather than deadlock
+    DevArgs aa = a;
+    void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
+    return hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NW * WAVE), args, (unsigned)sh, s) == hipSuccess ? 0 : -1;
+  }
   if (big)
     hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
   else
     hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Can every workgroup of a k_mpc_step launch be resident at once (cooperative launch)?
+bool coop_fits(const DevArgs& a, int device) {
+  int coopok = 0, ncu = 0, per = 0;
+  if (hipDeviceGetAttribute(&coopok, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !coopok)
+    return false;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return false;
+  const size_t sh = lds_bytes(a.cfg.H, a.cfg.precision);
+  const bool big = a.cfg.H > HMAX;
+  const void* fn = big ? (const void*)k_mpc_step<true> : (const void*)k_mpc_step<false>;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NW * WAVE, sh) != hipSuccess) return false;
+  return (long long)per * ncu >= (long long)a.C;
 }
 
 int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s) {

@@ -73,6 +73,9 @@ struct DevArgs {
   double* xcache_rho;       // N   penalty of the cached agent setup (NaN: none)
   int* ecache;              // E   1 when the pair's speed-only tables are built
   int* gi_ws;               // E*(2+64) the pair's last dual active set: m, step t, codes
+  double* gpart;            // 2*C*5 coop: per-component termination partials (iteration parity)
+  double* ghist;            // step_cap*max_outer*2 coop: global (rk, sk) history per step
+  int* giters;              // step_cap coop: global outer iterations per step
 };
 
 // Big mode: rows of the per-wave x-step factor scratch (working sets of up to H + 2 rows:
@@ -115,10 +118,12 @@ constexpr int F_FIRST = 1;    // first launch of the step: seeds, zero / warm pe
 constexpr int F_LAST = 2;     // last launch: outputs, propagation, cross-step warm labels
 constexpr int F_GLOBAL = 4;   // termination decided outside (term_global): no per-component stop
 constexpr int F_NANLAST = 8;  // the global loop stopped at the collision test of iteration it0-1
+constexpr int F_COOP = 16;    // global termination decided in-kernel (cooperative launch, one rank)
 
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s);
 int launch_resid_history(const DevArgs& a, int nsteps, double* out, hipStream_t s);
 int launch_pair_deff(const DevArgs& a, hipStream_t s);
+bool coop_fits(const DevArgs& a, int device);
 
 }  // namespace pd

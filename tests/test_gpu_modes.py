@@ -63,6 +63,34 @@ def test_global_termination_without_any_collision(Solver):
     compare(Solver, config.matlab_pi(H=10, term_global=1), scenario.tiled(3, 10, n_steps=12, seed=3), 3)
 
 
+def test_in_kernel_global_termination_equals_host_decision(Solver, monkeypatch):
+    """Natural global termination on one rank runs the stop test in-kernel behind a grid
+    barrier (cooperative launch, several MPC steps per launch); the host-decided path
+    (PIADMM_NO_COOP=1: one launch per outer iteration) gives the same job."""
+    cfg = config.matlab_pi(H=30, term_global=1)
+    scn = scenario.tiled(24, 30, n_steps=12, perturb=True, seed=4)
+    with Solver(cfg, scn) as s1:
+        monkeypatch.setenv("PIADMM_NO_COOP", "1")
+        s2 = Solver(cfg, scn)
+        monkeypatch.delenv("PIADMM_NO_COOP")
+        try:
+            assert s1.steps_per_launch() > 1 and s2.steps_per_launch() == 1
+            for _ in range(5):
+                r1, r2 = s1.mpc_step(), s2.mpc_step()
+                assert r1.global_iters == r2.global_iters
+                np.testing.assert_array_equal(r1.iters, r2.iters)
+                np.testing.assert_allclose(r1.global_resid, r2.global_resid, rtol=1e-12, atol=1e-12)
+                np.testing.assert_allclose(r1.xt, r2.xt, rtol=1e-12, atol=1e-12)
+            s1.steps_async(5, 4)
+            s2.steps_async(5, 4)
+            s1.sync()
+            s2.sync()
+            np.testing.assert_allclose(s1.state()["xt"], s2.state()["xt"], rtol=1e-12, atol=1e-12)
+            assert s1.global_resid()[1] == s2.global_resid()[1]
+        finally:
+            s2.close()
+
+
 @pytest.mark.parametrize("preset", ["casadi_default", "matlab_pi"])
 def test_warm_duals_match_oracle(Solver, preset):
     compare(Solver, config.PRESETS[preset](H=15, warm_duals=1), scenario.tiled(2, 15, n_steps=30, seed=5), 20)
