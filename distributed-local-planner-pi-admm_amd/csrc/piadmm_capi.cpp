@@ -213,6 +213,8 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   {
     const char* ps = std::getenv("PIADMM_PAIR_SOLVER");
     A.pair_gi = (ps && std::strcmp(ps, "admm") == 0) ? 0 : 1;
+    const char* xs = std::getenv("PIADMM_X_SOLVER");      // "pdas": one-step label moves + ADMM only
+    A.x_gi = (xs && std::strcmp(xs, "pdas") == 0) ? 0 : 1;
   }
   A.N = N;
   A.E = n_edges;

@@ -1292,10 +1292,11 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
 }
 
 template <int NV>
-__device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y, int& nsolve) {
+__device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y, int& nsolve,
+                                     int steps = PDAS_STEPS) {
   constexpr int NR = QP<NV>::NR;
   signed char nl[NR];
-  for (int it = 0; it < PDAS_STEPS; ++it) {
+  for (int it = 0; it < steps; ++it) {
     ++nsolve;
     unsigned long long t_r = STAMP_T();
     bool rs_ok;
@@ -1404,7 +1405,8 @@ constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t
 // feasible -- the state GI requires -- before the usual adds.  Any starting set is only a
 // guess: the minimiser and its certificate do not depend on it.
 template <int NV>
-__device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x, double* y, int& nsteps) {
+__device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, signed char* lab, double* x, double* y,
+                                         int& nsteps) {
   constexpr int NR = QP<NV>::NR;
   const int l = lid(), H = P.H, ld = P.fld, H2 = NV * H;
   double* vb_ax = P.vb + 192;      // [192, 192 + NR*H): (A v) by row id
@@ -1533,8 +1535,18 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
     }
   };
 
-  // ---- warm start from the stored active set (this step's, or the previous step's shifted)
+  // warm row: append unless linearly dependent on the rows already in (multiplier set later)
+  auto warm_add = [&](int pc) {
+    if (m >= cap) return;
+    double yp[NV];
+    const double spp = prep(pc, yp);
+    const double w = fwd();
+    const double lpp2 = spp - wsum(w * w);
+    if (lpp2 > DEP_TOL * spp) append(pc, yp, w, lpp2, 0.0);
+  };
+  bool warm = false;
   if (P.gws) {
+    // ---- pair: the stored active set (this step's, or the previous step's shifted)
     const int gm = P.gws[0], gt = P.gws[1];
     const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
     if ((same || prev) && gm > 0 && gm <= WAVE) {
@@ -1547,13 +1559,27 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, signed char* lab, double* x,
       if (NV == 2 && P.g1 == 0.0 && P.g2 == 0.0 && code >= 0 && P.hinge((code >> 1) / H)) code = -1;
       for (int i = 0; i < gm; ++i) {
         const int pc = rdli(code, i);
-        if (pc < 0 || m >= cap) continue;
-        double yp[NV];
-        const double spp = prep(pc, yp);
-        const double w = fwd();
-        const double lpp2 = spp - wsum(w * w);
-        if (lpp2 > DEP_TOL * spp) append(pc, yp, w, lpp2, 0.0);   // else dependent: skip
+        if (pc >= 0) warm_add(pc);
       }
+      warm = true;
+    }
+  } else if (wlab) {
+    // ---- x-step: the rows the current labels hold at a bound
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      const bool in = P.valid(s) && wlab[s] != 0;
+      unsigned long long bm = __ballot(in);
+      const int side = (!P.hinge(s) && wlab[s] == UPPER) ? 1 : 0;
+      while (bm) {
+        const int k = __ffsll(bm) - 1;
+        bm &= bm - 1;
+        warm_add(2 * (s * H + k) + rdli(side, k));
+      }
+    }
+    warm = true;
+  }
+  if (warm) {
+    {
       // dual feasibility: drop the most negative (or beyond-cap hinge) multiplier until none
       double lam = 0.0;
       while (m > 0) {
@@ -1757,7 +1783,30 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
   if (warm_lab) {
 #pragma unroll
     for (int s = 0; s < NR; ++s) flab[s] = lab[s];
-    ok = pdas(P, lab, x, y, n_pdas);
+    if (NV == 1 && P.ycap > 0) {
+      // x-step: the warm labels' reduced solve (a cached-table hit in the steady state); when
+      // its certificate fails, the dual active set warm-started from those labels finds the
+      // new working set in a few steps, and one reduced solve on it certifies (instead of a
+      // table rebuild per one-step PDAS label move, then ADMM)
+      ok = pdas(P, lab, x, y, n_pdas, 1);
+      if (!ok) {
+        int ngi = 0;
+        signed char glab[NR];
+        if (gi_solve(P, flab, glab, x, y, ngi)) {
+#pragma unroll
+          for (int s = 0; s < NR; ++s) lab[s] = glab[s];
+          ok = pdas(P, lab, x, y, n_pdas);
+        }
+        n_gi += ngi;
+        if (!ok) {
+#pragma unroll
+          for (int s = 0; s < NR; ++s) lab[s] = flab[s];
+          ok = pdas(P, lab, x, y, n_pdas);
+        }
+      }
+    } else {
+      ok = pdas(P, lab, x, y, n_pdas);
+    }
   }
   if constexpr (NV == 2) {
     // pair QP: dual active set first (no K_s^-1, no ADMM); certified by the KKT test, and
@@ -1765,7 +1814,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
     if (!ok && P.ycap > 0) {
       int ngi = 0;
       signed char glab[NR];
-      if (gi_solve(P, glab, x, y, ngi)) {
+      if (gi_solve(P, nullptr, glab, x, y, ngi)) {
         signed char nl[NR];
         ok = kkt_check(P, glab, x, y, nl);
 #pragma unroll
@@ -1986,6 +2035,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
   }
   ruiz(P);
   build_K<1, false>(P, xfac, P.fld, Kc);
+  P.Kcache = Kc;        // the same matrix: a later reload (after the x-step's dual active set) is a copy
   for (int i = 0; i < H; ++i)
     if (in) xfac[i * P.fld + l] = P_entry(P, 0, i, l);
   wsync();
@@ -2250,6 +2300,12 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     qx.fstate = xfs;
     qx.fld = big ? xrows(H) + 1 : HMAX + 1;
     qx.mmax = big ? xrows(H) : HMAX;
+    // dual active set for the x-step's working-set changes: Y in this wave's K_s^-1 region
+    // (LDS mode; K_s^-1 is reloaded from its HBM copy if ADMM runs later)
+    qx.gws = nullptr;
+    qx.tstep = t;
+    qx.Y = big ? nullptr : (f32 ? (double*)(Kxf + w * H * H) : Kx + w * H * H);
+    qx.ycap = (big || !A.x_gi) ? 0 : (f32 ? (H * H / 2) / H : H);
     nnb = A.nbr_cnt[a];
     setup_agent(A, a, qx, gx, xfac);
     // receding-horizon warm start: the previous step's final labels shifted by one time
@@ -2568,6 +2624,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       // Double-buffered by the parity of the launch's barrier count (iterations and steps),
       // so one barrier per iteration suffices; agent-scope atomic accesses keep the
       // partials out of the non-coherent per-CU cache.
+      unsigned long long t_gb = STAMP_T();
       double* part = A.gpart + (size_t)(nbar & 1) * A.C * 5;
       ++nbar;
       if (threadIdx.x == 0) {
@@ -2579,18 +2636,28 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
           __hip_atomic_store(&part[ci * 5 + q], pv[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       cooperative_groups::this_grid().sync();
-      if (threadIdx.x == 0) {
-        double tot[5] = {0, 0, 0, 0, 0};
-        for (int k = 0; k < A.C; ++k)
+      {
+        // all threads load (components tid, tid + 128, ...), then five threads sum the
+        // per-thread partials in thread order: a fixed order, identical in every workgroup
+        double v[5] = {0, 0, 0, 0, 0};
+        for (int k = threadIdx.x; k < A.C; k += blockDim.x)
 #pragma unroll
           for (int q = 0; q < 5; ++q)
-            tot[q] += __hip_atomic_load(&part[k * 5 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[q] += __hip_atomic_load(&part[k * 5 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double* red = vec_all;           // the waves' vector buffers are free between QP solves
 #pragma unroll
-        for (int q = 0; q < 5; ++q) S.sc[16 + q] = tot[q];
+        for (int q = 0; q < 5; ++q) red[q * NW * WAVE + threadIdx.x] = v[q];
+        __syncthreads();
+        if (threadIdx.x < 5) {
+          double tot = 0.0;
+          for (int k = 0; k < NW * WAVE; ++k) tot += red[threadIdx.x * NW * WAVE + k];
+          S.sc[16 + threadIdx.x] = tot;
+        }
       }
       __syncthreads();
       const double trk = S.sc[16], tsk = S.sc[17], tact = S.sc[18], tseen = S.sc[19], tbad = S.sc[20];
       __syncthreads();
+      STAMP_ADD(ST_TERM, t_gb);
       if (tact == 0.0 && gflag == 0) {       // no pair collides anywhere: stop (:115-116)
         nanlast = true;
         break;
@@ -2607,6 +2674,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   }
   __syncthreads();
   STAMP_ADD(ST_KERNEL, t_k);
+  unsigned long long t_epi = STAMP_T();
 
   // ---- work counters (accumulated across launches; one workgroup owns row ci)
   {
@@ -2720,6 +2788,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) edge_hbm[k][(size_t)e * 4 * H1 + i] = edge_lds[k][i];
     if (threadIdx.x == 0) A.status[A.N + e] = status_e;
   }
+  STAMP_ADD(ST_RED_X, t_epi);
 }
 
 // Persistent multi-step launch (the reference's `for num_step` loop,

@@ -24,6 +24,7 @@ struct DevArgs {
   piadmm_config_t cfg;
   int N, E, C, T;
   int pair_gi;              // 1: pair QPs try the dual active set first (env PIADMM_PAIR_SOLVER)
+  int x_gi;                 // 1: x-step working-set changes by the dual active set (env PIADMM_X_SOLVER)
   // scenario (read-only during a step)
   const double* spd;        // N
   const double* ref;        // N*2*T

@@ -261,6 +261,35 @@ def test_pair_solvers_agree(Solver, H, monkeypatch):
             s_admm.close()
 
 
+@pytest.mark.parametrize("H", [15, 30, 40])
+def test_xstep_solvers_agree(Solver, H, monkeypatch):
+    """x-step working-set changes by the dual active set (default) or by one-step PDAS label
+    moves + ADMM (PIADMM_X_SOLVER=pdas): the same certified minimisers, iteration counts and
+    residual histories, and both match the oracle."""
+    cfg = config.matlab_pi(H=H)
+    scn = scenario.tiled(10, H, n_steps=8, perturb=True, seed=21)
+    orc = O.Oracle(cfg, scn)
+    with Solver(cfg, scn) as s_gi:
+        monkeypatch.setenv("PIADMM_X_SOLVER", "pdas")
+        s_pd = Solver(cfg, scn)
+        monkeypatch.delenv("PIADMM_X_SOLVER")
+        try:
+            for _ in range(6):
+                ro, r1, r2 = orc.mpc_step(), s_gi.mpc_step(), s_pd.mpc_step()
+                np.testing.assert_array_equal(r1.iters, r2.iters)
+                np.testing.assert_array_equal(r1.iters, ro.iters)
+                np.testing.assert_allclose(r1.xt, r2.xt, rtol=1e-10, atol=1e-10)
+                np.testing.assert_allclose(r1.u, ro.u, rtol=0, atol=1e-8)
+                np.testing.assert_allclose(r1.xt, ro.xt, rtol=1e-8, atol=1e-8)
+                assert np.all(r1.status == 0) and np.all(r2.status == 0)
+            c1, c2 = s_gi.counters(), s_pd.counters()
+            assert c1["x_qps"] == c2["x_qps"]
+            if H <= 32:      # LDS mode: the x-step's dual active set replaces ADMM
+                assert c1["admm_x"] < c2["admm_x"]
+        finally:
+            s_pd.close()
+
+
 def test_errors_are_loud(Solver):
     with pytest.raises(_lib.PiadmmError, match="H must be"):
         Solver(config.matlab_pi(H=64), scenario.tiled(1, 64, n_steps=1))

@@ -12,7 +12,8 @@ NAMES = ['setup_x', 'setup_z', 'xstep', 'xqp', 'xred', 'xroll', 'zstep', 'zqp', 
 tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-cfg = config.matlab_pi(H=H, fixed_iters=1, max_outer=100)
+natural = len(sys.argv) > 4 and sys.argv[4] == "natural"
+cfg = config.matlab_pi(H=H, fixed_iters=0 if natural else 1, max_outer=100, term_global=int(natural))
 scn = scenario.tiled(tiles, H, n_steps=steps)
 s = PI_ADMM_MI355X(cfg, scn)
 s.reset_counters()
