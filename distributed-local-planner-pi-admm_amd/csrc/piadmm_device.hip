@@ -1183,7 +1183,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
       vb_b[pos[s]] = (lab[s] == LOWER) ? P.lo(s) : P.hi(s);
     }
   }
-  if (l < H) vb_q[l] = P.q[0];
+  vb_q[l] = (l < H) ? P.q[0] : 0.0;   // zero-padded to 64: the fused pass loads it unconditionally
   wsync();
   const int myid = (l < m) ? ids[l] : 0;
   const int key = myid + ((l < m && vb_b[l] > 0.0) ? (1 << 20) : 0);
@@ -1210,7 +1210,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
 #pragma unroll
       for (int u = 0; u < GEMV_U; ++u) {
         const int j = min(j0 + u, H - 1);
-        qv[u] = (j0 + u < H) ? vb_q[j] : 0.0;
+        qv[u] = vb_q[j0 + u];          // 0 beyond H (j0 + u < 64)
         gv[u] = G[j * H + lc];
         xv[u] = XT[j * P.xld + la];
       }
