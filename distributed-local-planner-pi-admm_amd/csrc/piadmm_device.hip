@@ -394,6 +394,8 @@ struct QP {
   double* Y;              // pair: dual active-set columns P^-1 n_a (shares the K_s^-1 region)
   int ycap;               // pair: columns Y holds
   bool scaled;            // Ruiz scaling computed (the pair computes it only when ADMM is needed)
+  bool wraw;              // the warm ADMM state holds the last certified (x, y) unscaled (zs unset):
+                          // converted to the scaled (xs, zs, ys) only when ADMM actually runs
   const double* Kcache;   // x-step: HBM copy of K_s^-1, loaded into K only when ADMM is needed
   int* gws;               // pair: HBM warm working set of the dual active set (GI_WS ints)
   int tstep;              // MPC step index (warm-set bookkeeping)
@@ -1763,6 +1765,22 @@ __device__ __forceinline__ double rho_ratio(const QP<NV>& P, const double* xs, c
   return (ratio > 5.0 || ratio < 0.2) ? ratio : 1.0;
 }
 
+// Raw warm state (x, y of the last certified solve, unscaled) -> scaled ADMM state.
+template <int NV>
+__device__ __forceinline__ void warm_to_scaled(QP<NV>& P, double* xs, double* zs, double* ys) {
+  constexpr int NR = QP<NV>::NR;
+  double ax[NR];
+  A_mul(P, xs, ax);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xs[v] = (P.D[v] != 0.0) ? xs[v] / P.D[v] : 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    zs[s] = P.valid(s) ? P.E[s] * ax[s] : 0.0;
+    ys[s] = P.valid(s) ? ys[s] / P.E[s] : 0.0;
+  }
+  P.wraw = false;
+}
+
 // Solve one QP.  (xs, zs, ys) is the warm ADMM state (scaled), lab the warm labels.
 // P.rho may be adapted (K^-1 rebuilt in the scratch kscr, stride kld) and persists.
 // Returns PIADMM_QP_* flags; x_out = unscaled minimiser.
@@ -1830,6 +1848,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
   if (!ok && !P.kready) {
     if (!P.scaled) {
       // the warm ADMM state is in identity scaling (x, A x, y): move it to the Ruiz space
+      if (P.wraw) warm_to_scaled(P, xs, zs, ys);     // identity D, E: (x, A x, y)
       unsigned long long t_r = STAMP_T();
       ruiz(P);
       STAMP_ADD(ST_SZ_RUIZ, t_r);
@@ -1864,6 +1883,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
     if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
     wsync();
   }
+  if (!ok && P.wraw) warm_to_scaled(P, xs, zs, ys);
   for (int it = 1; !ok && it <= max_inner; ++it) {
     unsigned long long t_a = STAMP_T();
     admm_iter(P, xs, zs, ys);
@@ -1903,16 +1923,12 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
   unsigned long long t_ep = STAMP_T();
   int st = PIADMM_QP_OK;
   if (ok) {
-    // warm ADMM state at the exact optimum
-    double ax[NR];
-    A_mul(P, x, ax);
+    // warm ADMM state at the exact optimum, kept raw until an ADMM iteration needs it
 #pragma unroll
-    for (int v = 0; v < NV; ++v) xs[v] = (P.D[v] != 0.0) ? x[v] / P.D[v] : 0.0;
+    for (int v = 0; v < NV; ++v) xs[v] = x[v];
 #pragma unroll
-    for (int s = 0; s < NR; ++s) {
-      zs[s] = P.valid(s) ? P.E[s] * ax[s] : 0.0;
-      ys[s] = P.valid(s) ? y[s] / P.E[s] : 0.0;
-    }
+    for (int s = 0; s < NR; ++s) ys[s] = P.valid(s) ? y[s] : 0.0;
+    P.wraw = true;
   } else {
     st |= PIADMM_QP_INEXACT;
 #pragma unroll
@@ -2005,6 +2021,7 @@ __device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, doubl
   P.tol = c.qp_tol;
   P.kready = true;      // setup_agent loads or builds K_s^-1
   P.scaled = true;
+  P.wraw = false;
   P.Kcache = nullptr;
 }
 
@@ -2132,6 +2149,7 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
   }
   P.E[4] = P.valid(4) ? 1.0 : 0.0;
   P.scaled = false;
+  P.wraw = false;
   P.Kcache = nullptr;
   P.kready = false;     // K_s^-1 is built by qp_solve when ADMM is first needed
 }
@@ -2740,6 +2758,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       if (l == 0) A.xcache_rho[a] = qx.rho;
     }
     if (!last_launch) {
+      if (qx.wraw) warm_to_scaled(qx, xs_x, zs_x, ys_x);
       double* qs = A.qs_x + (size_t)a * 5 * WAVE;
       signed char* ql = A.ql_x + (size_t)a * 2 * WAVE;
       qs[l] = xs_x[0];
@@ -2768,6 +2787,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   if (w == 0 && e >= 0) {
     if (l == 0) A.rho_e[e] = qe.rho;
     if (!last_launch) {
+      if (qe.wraw) warm_to_scaled(qe, xs_e, zs_e, ys_e);
       double* qs = A.qs_e + (size_t)e * 12 * WAVE;
       signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
       // unscaled (the next launch restarts in identity scaling, setup_pair)
