@@ -580,6 +580,10 @@ __device__ __forceinline__ void At_mul(const QP<NV>& P, const double* w, double*
 // Loads are issued GEMV_U deep before their first use so that the pair's L2-resident
 // tables cost one latency per batch, not one per column.
 constexpr int GEMV_U = 8;
+#ifndef PIADMM_XGEMV_U
+#define PIADMM_XGEMV_U 8
+#endif
+constexpr int XGEMV_U = PIADMM_XGEMV_U;   // batch of the x-step fused pass (registers in flight)
 template <bool BD, int NV, typename Ptr>
 __device__ __forceinline__ void gemv_sym(const QP<NV>& P, Ptr M, const double* r, double* y) {
   const int l = lid();
@@ -1207,17 +1211,18 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
   {
     const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
     const double* G = P.G;
-    for (int j0 = 0; j0 < H; j0 += GEMV_U) {
-      double qv[GEMV_U], gv[GEMV_U], xv[GEMV_U];
+    constexpr int XU = XGEMV_U;
+    for (int j0 = 0; j0 < H; j0 += XU) {
+      double qv[XU], gv[XU], xv[XU];
 #pragma unroll
-      for (int u = 0; u < GEMV_U; ++u) {
+      for (int u = 0; u < XU; ++u) {
         const int j = min(j0 + u, H - 1);
         qv[u] = vb_q[j0 + u];          // 0 beyond H (j0 + u < 64)
         gv[u] = G[j * H + lc];
         xv[u] = XT[j * P.xld + la];
       }
 #pragma unroll
-      for (int u = 0; u < GEMV_U; ++u) {
+      for (int u = 0; u < XU; ++u) {
         ag += gv[u] * qv[u];
         ax += xv[u] * qv[u];
       }
@@ -2215,7 +2220,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   double* fdiag_all = vec_all + NW * 512;                // NW x 256
   CompLds S;
   S.pos = fdiag_all + NW * 256;
-  S.xt = S.pos + 4 * H1;
+  S.xt = S.pos + 8 * H1;   // pos_old double-buffered by outer-iteration parity
   S.seed = S.xt + 6;
   S.u = S.seed + 4;
   S.hat = S.u + 2 * H;
@@ -2259,7 +2264,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     double* const edge_lds[5] = {S.hat, S.lam, S.S, S.D, S.last};
     double* const edge_hbm[5] = {A.hat, A.lam, A.Sacc, A.Dacc, A.last};
     if (first) {
-      for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) S.pos[i] = 0.0;
+      for (int i = threadIdx.x; i < 8 * H1; i += blockDim.x) S.pos[i] = 0.0;
       // casadi/main.py:52-63 resets hat, lam (and the PI accumulators) every MPC step; with
       // warm_duals they continue from the previous step shifted by one slot (a12)
       for (int k = 0; k < 5; ++k)
@@ -2274,7 +2279,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     } else {
       // state of the previous launch of this step
       for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
-        S.pos[i] = (i < na * 2 * H1) ? A.pos_old[(size_t)a0 * 2 * H1 + i] : 0.0;
+        S.pos[((it0 - 1) & 1) * 4 * H1 + i] = (i < na * 2 * H1) ? A.pos_old[(size_t)a0 * 2 * H1 + i] : 0.0;
       for (int i = threadIdx.x; i < na * H; i += blockDim.x) S.u[i] = A.u[(size_t)a0 * H + i];
       for (int k = 0; k < 5; ++k)
         for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
@@ -2443,6 +2448,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 
   for (int it = it0; it < it1; ++it) {
     iters = it + 1;
+    // this iteration's pos_old buffer: a wave may start the next iteration's x-step while
+    // the other still reads this one's positions (no second barrier without a z-step)
+    double* const pos = S.pos + (it & 1) * 4 * H1;
     // -------- x-step: every agent of the component (casadi/main.py:81-106)
     if (w < na) {
       unsigned long long t_xs = STAMP_T();
@@ -2484,8 +2492,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 #endif
       STAMP_ADD(ST_XROLL, t_r);
       if (l <= H) {
-        S.pos[(w * 2 + 0) * H1 + l] = px;
-        S.pos[(w * 2 + 1) * H1 + l] = py;
+        pos[(w * 2 + 0) * H1 + l] = px;
+        pos[(w * 2 + 1) * H1 + l] = py;
       }
       if (l < H) S.u[w * H + l] = u;
       STAMP_ADD(ST_XSTEP, t_xs);
@@ -2498,8 +2506,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     if (e >= 0 && na == 2) {
       bool hit = false;
       if (l <= H) {
-        const double dx = S.pos[0 * H1 + l] - S.pos[2 * H1 + l];
-        const double dy = S.pos[1 * H1 + l] - S.pos[3 * H1 + l];
+        const double dx = pos[0 * H1 + l] - pos[2 * H1 + l];
+        const double dy = pos[1 * H1 + l] - pos[3 * H1 + l];
         hit = (dx * dx + dy * dy) < thr;
       }
       act = wany(hit);
@@ -2515,10 +2523,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       unsigned long long t_z = STAMP_T();
       const bool tl = l <= H;
       double bx[2], by[2];
-      bx[0] = tl ? S.pos[0 * H1 + l] + S.lam[0 * H1 + l] - c1x : 0.0;
-      by[0] = tl ? S.pos[1 * H1 + l] + S.lam[1 * H1 + l] - c1y : 0.0;
-      bx[1] = tl ? S.pos[2 * H1 + l] + S.lam[2 * H1 + l] - c2x : 0.0;
-      by[1] = tl ? S.pos[3 * H1 + l] + S.lam[3 * H1 + l] - c2y : 0.0;
+      bx[0] = tl ? pos[0 * H1 + l] + S.lam[0 * H1 + l] - c1x : 0.0;
+      by[0] = tl ? pos[1 * H1 + l] + S.lam[1 * H1 + l] - c1y : 0.0;
+      bx[1] = tl ? pos[2 * H1 + l] + S.lam[2 * H1 + l] - c2x : 0.0;
+      by[1] = tl ? pos[3 * H1 + l] + S.lam[3 * H1 + l] - c2y : 0.0;
       const double w1 = tl ? ge1.ax * bx[0] + ge1.ay * by[0] : 0.0;
       const double w2 = tl ? ge2.ax * bx[1] + ge2.ay * by[1] : 0.0;
       const double q1 = Tt_apply(shdn(w1, 1)), q2 = Tt_apply(shdn(w2, 1));
@@ -2545,8 +2553,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       // dual update (plain :161-162 / PI + anti-windup MATLAB :156-188)
       double px[2], py[2];
       for (int v = 0; v < 2; ++v) {
-        px[v] = tl ? S.pos[(2 * v + 0) * H1 + l] : 0.0;
-        py[v] = tl ? S.pos[(2 * v + 1) * H1 + l] : 0.0;
+        px[v] = tl ? pos[(2 * v + 0) * H1 + l] : 0.0;
+        py[v] = tl ? pos[(2 * v + 1) * H1 + l] : 0.0;
       }
       double dist = 0.0;
       {
@@ -2622,12 +2630,16 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       }
       const bool stop0 = !c.fixed_iters && !global && rk0 <= c.eps_pri && sk0 <= c.eps_dual &&
                          (!c.term_dist_check || dc0 > deff);
-      if (!stop0 && !c.alias_dual_residual)
+      // last_iter_hat_pos = hat_pos_old: only a z-step changes hat, so the copy is needed
+      // only after one (S.last already equals hat otherwise)
+      if (act && !stop0 && !c.alias_dual_residual)
         for (int i = l; i < 4 * H1; i += WAVE) S.last[i] = S.hat[i];
       STAMP_ADD(ST_TERMW, t_tw);
     }
+    // second barrier only after a z-step (it wrote hat, lam, S, D, last and S.sc); without
+    // one every wave takes the stop decision from its registers (rk = sk = 0)
     unsigned long long t_sb = STAMP_T();
-    __syncthreads();
+    if (act) __syncthreads();
     STAMP_ADD(ST_SYNC_B, t_sb);
     const double rk = act ? S.sc[0] : 0.0;
     const double sk = act ? S.sc[1] : 0.0;
@@ -2741,7 +2753,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   }
   if (w < na) {
     const int a = a0 + w;
-    for (int i = l; i < 2 * H1; i += WAVE) A.pos_old[(size_t)a * 2 * H1 + i] = S.pos[w * 2 * H1 + i];
+    const double* posl = S.pos + ((iters - 1) & 1) * 4 * H1;   // the last executed iteration's buffer
+    for (int i = l; i < 2 * H1; i += WAVE) A.pos_old[(size_t)a * 2 * H1 + i] = posl[w * 2 * H1 + i];
     const double u = (l < H) ? S.u[w * H + l] : 0.0;
     if (l < H) A.u[(size_t)a * H + l] = u;
     if (l == 0) {

@@ -106,7 +106,7 @@ inline size_t lds_bytes(int H, int precision = 0) {
   d += NW * 512;                   // per-wave vector buffers
   d += NW * 256;                   // per-wave factor diagonals (x, z)
   size_t H1 = H + 1;
-  d += 2 * 2 * H1;                 // pos_old
+  d += 2 * 2 * 2 * H1;             // pos_old (two buffers: outer-iteration parity)
   d += 2 * 3 + 2 * 2 + 2 * H;      // xt, seeds, u
   d += 5 * 2 * 2 * H1;             // hat, lam, S, D, last_hat
   d += 32;                         // scalars
