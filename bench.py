@@ -21,8 +21,10 @@ Components never straddle ranks; the ranks join one RCCL communicator (the uniqu
 id travels over torch.distributed's gloo group, which is otherwise only the
 harness's barrier and max-over-ranks timer).
 
---natural: natural termination instead (one launch + one RCCL all-reduce of the
-termination partials per outer iteration, host decision), reported as its own line.
+--natural: natural termination instead, reported as its own line: on one rank the stop
+test runs in-kernel behind a grid barrier (cooperative launch, several steps per launch);
+across ranks one launch + one RCCL all-reduce of the termination partials per outer
+iteration, host decision.
 
 Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
 """
