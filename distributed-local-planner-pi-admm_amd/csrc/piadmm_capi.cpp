@@ -252,6 +252,7 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.Gx_g, big ? (size_t)N * (H * H + H) : 1);
   rc |= dalloc(h, &A.XT_g, big ? (size_t)N * H1 * pd::XLDG : 1);
   rc |= dalloc(h, &A.Ke_g, big ? E * 4 * H * H : 1);
+  rc |= dalloc(h, &A.Yx_g, big ? (size_t)N * pd::WAVE * H : 1);
   rc |= dalloc(h, &A.tab_e, E * 8 * H * H);
   rc |= dalloc(h, &A.warm_ok, (size_t)N);
   rc |= dalloc(h, &A.Sacc, E * 4 * H1);

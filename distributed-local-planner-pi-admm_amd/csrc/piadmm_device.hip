@@ -393,6 +393,7 @@ struct QP {
                           // a QP that the warm-label polish certifies never needs it)
   double* Y;              // pair: dual active-set columns P^-1 n_a (shares the K_s^-1 region)
   int ycap;               // pair: columns Y holds
+  bool y_in_k;            // Y shares the K_s^-1 region (a GI solve invalidates K_s^-1)
   bool scaled;            // Ruiz scaling computed (the pair computes it only when ADMM is needed)
   bool wraw;              // the warm ADMM state holds the last certified (x, y) unscaled (zs unset):
                           // converted to the scaled (xs, zs, ys) only when ADMM actually runs
@@ -1421,7 +1422,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   double* L = P.fac;
   double* Y = P.Y;
   const int cap = min(P.mmax - 1, P.ycap);
-  P.kready = false;                // Y overwrites the K_s^-1 region
+  if (P.y_in_k) P.kready = false;  // Y overwrites the K_s^-1 region
   if (l == 0) P.fstate[0] = -1;    // and L the cached PDAS factor
   double x0[NV], xc[NV];
   gemv_sym<true>(P, P.Pinv, P.q, x0);
@@ -2327,8 +2328,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     // (LDS mode; K_s^-1 is reloaded from its HBM copy if ADMM runs later)
     qx.gws = nullptr;
     qx.tstep = t;
-    qx.Y = big ? nullptr : (f32 ? (double*)(Kxf + w * H * H) : Kx + w * H * H);
-    qx.ycap = (big || !A.x_gi) ? 0 : (f32 ? (H * H / 2) / H : H);
+    // (big mode: a per-agent HBM buffer, K_s^-1 stays intact)
+    qx.Y = big ? A.Yx_g + (size_t)a * WAVE * H : (f32 ? (double*)(Kxf + w * H * H) : Kx + w * H * H);
+    qx.ycap = !A.x_gi ? 0 : (big ? WAVE : (f32 ? (H * H / 2) / H : H));
+    qx.y_in_k = !big;
     nnb = A.nbr_cnt[a];
     setup_agent(A, a, qx, gx, xfac);
     // receding-horizon warm start: the previous step's final labels shifted by one time
@@ -2399,6 +2402,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     // dual active-set columns in the K_s^-1 region (4H^2 doubles, or 2H^2 with fp32 images)
     qe.Y = Ke ? Ke : (double*)Kef;
     qe.ycap = A.pair_gi ? ((Ke ? 4 : 2) * H * H) / (2 * H) : 0;
+    qe.y_in_k = true;
     qe.gws = A.gi_ws + (size_t)e * GI_WS;
     qe.tstep = t;
     // Ke doubles as the H x 2H staging of the per-scenario pair tables; with fp32 images in
