@@ -398,6 +398,7 @@ struct QP {
   bool wraw;              // the warm ADMM state holds the last certified (x, y) unscaled (zs unset):
                           // converted to the scaled (xs, zs, ys) only when ADMM actually runs
   const double* Kcache;   // x-step: HBM copy of K_s^-1, loaded into K only when ADMM is needed
+  mutable int csig;       // x-step: per-lane working-set signature of the cached X', G
   int* gws;               // pair: HBM warm working set of the dual active set (GI_WS ints)
   int tstep;              // MPC step index (warm-set bookkeeping)
 
@@ -1183,28 +1184,30 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
     m += __popcll(bm);
   }
   if (m > P.mmax) return false;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (inW[s]) {
-      ids[pos[s]] = s * H + l;
-      vb_b[pos[s]] = (lab[s] == LOWER) ? P.lo(s) : P.hi(s);
-    }
-  }
   vb_q[l] = (l < H) ? P.q[0] : 0.0;   // zero-padded to 64: the fused pass loads it unconditionally
-  wsync();
-  const int myid = (l < m) ? ids[l] : 0;
-  const int key = myid + ((l < m && vb_b[l] > 0.0) ? (1 << 20) : 0);
-  const bool cached = (P.fstate[0] == m) && wall(l >= m || cids[l] == key);
-  if (!cached) {
+  // the working set with its bound sides as a per-lane signature (this lane's box and rate
+  // rows) in a register: a hit on the cached X', G is one ballot, no LDS round trip
+  const int sig = (inW[0] ? (int)lab[0] : 0) | ((inW[1] ? (int)lab[1] : 0) << 2);
+  if (!(P.fstate[0] >= 0 && wall(sig == P.csig))) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (inW[s]) {
+        ids[pos[s]] = s * H + l;
+        vb_b[pos[s]] = (lab[s] == LOWER) ? P.lo(s) : P.hi(s);
+      }
+    }
+    wsync();
+    const int myid = (l < m) ? ids[l] : 0;
     if (!param_build_x(P, m, myid, ids, vb_b)) {
       if (l == 0) P.fstate[0] = -1;
       wsync();
       return false;
     }
-    if (l < m) cids[l] = key;
+    P.csig = sig;
     if (l == 0) P.fstate[0] = m;
-    wsync();
   }
+  (void)cids;
+  wsync();
   STAMP_ADD(ST_RSX_PRE, t_pre);
   unsigned long long t_rs = STAMP_T();
   // one fused pass: x = -G q + g (lane = variable), lam = -X q - beta (lane = W row)
@@ -2029,6 +2032,7 @@ __device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, doubl
   P.scaled = true;
   P.wraw = false;
   P.Kcache = nullptr;
+  P.csig = -1;
 }
 
 // x-step QP of agent a (cost_function_primal, PI_ADMM_class.py:114-135, constraints :172-192):
