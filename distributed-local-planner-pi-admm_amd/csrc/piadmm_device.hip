@@ -364,6 +364,8 @@ struct QP {
   static constexpr int NR = (NV == 1) ? 2 : 5;
   int H, n;
   double q[NV];
+  double wq;              // x-step: w' with q = T'-apply(w') (PI_ADMM_class.py:114-135 gradient)
+  bool qvalid;            // q holds T'-apply(wq) (the x-step's fused pass needs only wq)
   double D[NV];
   double E[NR];
   double h0;              // hinge lower bound (pair only; 0 on invalid lanes)
@@ -1160,6 +1162,24 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
     if (P.gmem) gsync();
     else wsync();
   }
+  // fold q = T'-apply(w') into the tables: row k of G T' (and X T') is
+  // sum_{j<k} (k - j) row j -- two running sums per lane, in place (read before write)
+  {
+    double s1 = 0.0, s2 = 0.0, t1 = 0.0, t2 = 0.0;
+    const int la = (l < m) ? l : 0;
+    for (int k = 0; k < H; ++k) {
+      const double gk = P.G[k * H + (l < H ? l : 0)];
+      const double xk = XT[k * P.xld + la];
+      if (l < H) P.G[k * H + l] = s2;
+      if (l < m) XT[k * P.xld + l] = t2;
+      s1 += gk;
+      s2 += s1;
+      t1 += xk;
+      t2 += t1;
+    }
+    if (P.gmem) gsync();
+    else wsync();
+  }
   return true;
 }
 
@@ -1184,7 +1204,9 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
     m += __popcll(bm);
   }
   if (m > P.mmax) return false;
-  vb_q[l] = (l < H) ? P.q[0] : 0.0;   // zero-padded to 64: the fused pass loads it unconditionally
+  // w' (q = T'-apply(w'), folded into the tables: G T', X T'), zero-padded to 64 so that the
+  // fused pass loads it unconditionally
+  vb_q[l] = (l < H) ? P.wq : 0.0;
   // the working set with its bound sides as a per-lane signature (this lane's box and rate
   // rows) in a register: a hit on the cached X', G is one ballot, no LDS round trip
   const int sig = (inW[0] ? (int)lab[0] : 0) | ((inW[1] ? (int)lab[1] : 0) << 2);
@@ -1774,6 +1796,19 @@ __device__ __forceinline__ double rho_ratio(const QP<NV>& P, const double* xs, c
   return (ratio > 5.0 || ratio < 0.2) ? ratio : 1.0;
 }
 
+// x-step: the linear term q = T'-apply(w') is formed only when a path other than the fused
+// parametric pass needs it (dual active set, ADMM)
+template <int NV>
+__device__ __forceinline__ void ensure_q(QP<NV>& P) {
+  if constexpr (NV == 1) {
+    if (!P.qvalid) {
+      const double qv = Tt_apply(P.wq);
+      P.q[0] = (lid() < P.H) ? qv : 0.0;
+      P.qvalid = true;
+    }
+  }
+}
+
 // Raw warm state (x, y of the last certified solve, unscaled) -> scaled ADMM state.
 template <int NV>
 __device__ __forceinline__ void warm_to_scaled(QP<NV>& P, double* xs, double* zs, double* ys) {
@@ -1819,6 +1854,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       if (!ok) {
         int ngi = 0;
         signed char glab[NR];
+        ensure_q(P);
         if (gi_solve(P, flab, glab, x, y, ngi)) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = glab[s];
@@ -1892,6 +1928,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
     if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
     wsync();
   }
+  if (!ok) ensure_q(P);
   if (!ok && P.wraw) warm_to_scaled(P, xs, zs, ys);
   for (int it = 1; !ok && it <= max_inner; ++it) {
     unsigned long long t_a = STAMP_T();
@@ -2471,14 +2508,15 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
         vy = vy + c.rho * (cy_own - S.hat[(d * 2 + 1) * H1 + l] + S.lam[(d * 2 + 1) * H1 + l]);
       }
       const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
-      const double qv = Tt_apply(shdn(wt, 1));
-      qx.q[0] = (l < H) ? qv : 0.0;
+      const double wsh = shdn(wt, 1);
+      qx.wq = (l < H) ? wsh : 0.0;
+      qx.qvalid = false;
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
 #ifdef PIADMM_DIAG_NO_XQP   // diagnostic timing build only: skip the x-step QP
       const int stx = 0;
-      ustar[0] = 1e-3 * qx.q[0];
+      ustar[0] = 1e-3 * qx.wq;
 #else
       const int stx = qp_solve<1, false>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n_admm_x, n_pdas_x, n_gi);
@@ -2540,6 +2578,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       const double q1 = Tt_apply(shdn(w1, 1)), q2 = Tt_apply(shdn(w2, 1));
       qe.q[0] = (l < H) ? -c.rho * q1 : 0.0;
       qe.q[1] = (l < H) ? -c.rho * q2 : 0.0;
+      qe.qvalid = true;
       double uh[2];
       unsigned long long t_zq = STAMP_T();
       // K_s^-1 of the pair is built in the LDS scratch and copied (2H <= 64), or in place
