@@ -1210,7 +1210,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
   // the working set with its bound sides as a per-lane signature (this lane's box and rate
   // rows) in a register: a hit on the cached X', G is one ballot, no LDS round trip
   const int sig = (inW[0] ? (int)lab[0] : 0) | ((inW[1] ? (int)lab[1] : 0) << 2);
-  if (!(P.fstate[0] >= 0 && wall(sig == P.csig))) {
+  if (!wall(sig == P.csig)) {       // csig = -1 whenever the tables are not valid
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (inW[s]) {
@@ -1222,6 +1222,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
     const int myid = (l < m) ? ids[l] : 0;
     if (!param_build_x(P, m, myid, ids, vb_b)) {
       if (l == 0) P.fstate[0] = -1;
+      P.csig = -1;
       wsync();
       return false;
     }
@@ -1449,6 +1450,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   const int cap = min(P.mmax - 1, P.ycap);
   if (P.y_in_k) P.kready = false;  // Y overwrites the K_s^-1 region
   if (l == 0) P.fstate[0] = -1;    // and L the cached PDAS factor
+  P.csig = -1;                     // (x-step: the factor scratch the parametric tables were built in)
   double x0[NV], xc[NV];
   gemv_sym<true>(P, P.Pinv, P.q, x0);
 #pragma unroll
