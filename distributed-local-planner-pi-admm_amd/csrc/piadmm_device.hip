@@ -1580,6 +1580,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     if (lpp2 > DEP_TOL * spp) append(pc, yp, w, lpp2, 0.0);
   };
   bool warm = false;
+  unsigned long long t_wb = STAMP_T();
   if (P.gws) {
     // ---- pair: the stored active set (this step's, or the previous step's shifted)
     const int gm = P.gws[0], gt = P.gws[1];
@@ -1613,6 +1614,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     }
     warm = true;
   }
+  STAMP_ADD(NV == 2 ? ST_ZR_GEMV : ST_ZR_X, t_wb);
+  unsigned long long t_wf = STAMP_T();
   if (warm) {
     {
       // dual feasibility: drop the most negative (or beyond-cap hinge) multiplier until none
@@ -1635,6 +1638,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       x_of(lam);
     }
   }
+  STAMP_ADD(NV == 2 ? ST_ZR_S : ST_ZR_CHOL, t_wf);
 
   while (true) {
     unsigned long long t_gs = STAMP_T();

@@ -8,7 +8,7 @@ from piadmm import config, scenario
 from piadmm.solver import PI_ADMM_MI355X
 NAMES = ['setup_x', 'setup_z', 'xstep', 'xqp', 'xred', 'xroll', 'zstep', 'zqp', 'zred', 'kernel',
          'red_gemv', 'red_S', 'red_chol', 'red_x', 'admm', 'xq', 'term', 'sz_ruiz', 'sz_kmat', 'sz_gj', 'sz_pre',
-         'zr_gemv', 'zr_S', 'zr_chol', 'zr_x', 'zr_solve', 'xr_solve', 'zkkt', 'xkkt', 'gi_search', 'gi_solve', 'gi_upd', 'sync_a', 'term_w0', 'sync_b', 'rsx_pre', 'qp_epi', 'round']
+         'zwarm_build', 'zwarm_feas', 'xwarm_feas', 'xwarm_build', 'zr_solve', 'xr_solve', 'zkkt', 'xkkt', 'gi_search', 'gi_solve', 'gi_upd', 'sync_a', 'term_w0', 'sync_b', 'rsx_pre', 'qp_epi', 'round']
 tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
