@@ -1,20 +1,24 @@
 // piadmm_device.hip -- MI355X (gfx950) kernels of the batched PI-ADMM consensus solver.
 //
 // One workgroup = one connected component of the candidate-pair graph (two
-// agents and their pair in the tiled scenario); one launch = one whole MPC step
-// of the reference loop (casadi/main.py:43-201): seeds, per-step setup of every
-// QP, the outer ADMM loop with device-side termination, and propagation.  The
-// components are independent, so no inter-workgroup communication exists.
+// agents and their pair in the tiled scenario); one persistent launch = up to 32
+// MPC steps of the reference loop (casadi/main.py:43-201) per component: seeds,
+// per-step setup of every QP, the outer ADMM loop with device-side termination,
+// and propagation.  Components are independent; the only inter-workgroup step is
+// the grid barrier of the reference's global stopping test (cooperative launch).
 //
 // Wave layout: wave w solves agent w's x-step; wave 0 also owns the pair.
-// Lane k <-> time/variable index k (H <= 32).  All arithmetic is fp64.
+// Lane k <-> time/variable index k (H <= 63).  All arithmetic is fp64.
 //
-// Per QP the solver is an OSQP-style ADMM in a Ruiz-scaled space (K^-1 staged
-// in LDS) whose iterates feed a primal-dual active-set (PDAS) polish: the
-// reduced KKT system of a guessed active set is solved exactly through the
-// Schur complement S = A_W P^-1 A_W' (Cholesky in LDS) and accepted only when
-// the KKT conditions hold.  So the answer is the exact QP minimiser, not an
-// eps=1e-3 OSQP iterate.  tools/qp_sim.py is the NumPy prototype of this math.
+// Every QP answer is the exact minimiser, certified by a complete KKT test:
+//  * the pair QP and the x-step's working-set changes by a Goldfarb-Idnani dual
+//    active set (Schur complement N P^-1 N' as an appended / rank-one-downdated
+//    Cholesky factor in LDS), warm-started from the previous active set;
+//  * the x-step's steady state by one fused pass over parametric tables of the
+//    current working set (x = -G T' w' + g, lam = -X T' w' - beta);
+//  * as the fallback, an OSQP-style ADMM in a Ruiz-scaled space feeding a
+//    primal-dual active-set (PDAS) polish on the reduced KKT system.
+// tools/qp_sim.py and tools/gi_sim.py are the NumPy prototypes of this math.
 #include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
