@@ -1214,7 +1214,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
   // the working set with its bound sides as a per-lane signature (this lane's box and rate
   // rows) in a register: a hit on the cached X', G is one ballot, no LDS round trip
   const int sig = (inW[0] ? (int)lab[0] : 0) | ((inW[1] ? (int)lab[1] : 0) << 2);
-  if (!wall(sig == P.csig)) {       // csig = -1 whenever the tables are not valid
+  if (__builtin_expect(!wall(sig == P.csig), 0)) {   // csig = -1 whenever the tables are not valid
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (inW[s]) {
@@ -1861,7 +1861,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       // new working set in a few steps, and one reduced solve on it certifies (instead of a
       // table rebuild per one-step PDAS label move, then ADMM)
       ok = pdas(P, lab, x, y, n_pdas, 1);
-      if (!ok) {
+      if (__builtin_expect(!ok, 0)) {
         int ngi = 0;
         signed char glab[NR];
         ensure_q(P);
@@ -2574,7 +2574,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 #ifdef PIADMM_DIAG_NO_PAIR
     if (false) {
 #else
-    if (act && w == 0) {
+    if (__builtin_expect(act && w == 0, 0)) {     // cold: about once per MPC step
 #endif
       unsigned long long t_z = STAMP_T();
       const bool tl = l <= H;
