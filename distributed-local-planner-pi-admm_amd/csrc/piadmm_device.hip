@@ -867,7 +867,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
   }
   double ax0[NR];
   A_mul(P, x0, ax0);
-  if (m > P.mmax) return false;
+  if (__builtin_expect(m > P.mmax, 0)) return false;
 #pragma unroll
   for (int s = 0; s < NR; ++s) {
     if (l < H) vb_ax[s * H + l] = ax0[s];
@@ -1207,7 +1207,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
     pos[s] = m + __popcll(bm & ltmask);
     m += __popcll(bm);
   }
-  if (m > P.mmax) return false;
+  if (__builtin_expect(m > P.mmax, 0)) return false;
   // w' (q = T'-apply(w'), folded into the tables: G T', X T'), zero-padded to 64 so that the
   // fused pass loads it unconditionally
   vb_q[l] = (l < H) ? P.wq : 0.0;
@@ -1341,11 +1341,11 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
     if constexpr (NV == 1) rs_ok = reduced_solve_x(P, lab, x, y);
     else rs_ok = reduced_solve(P, lab, x, y);
     STAMP_ADD(NV == 1 ? ST_XRED : ST_ZRED, t_r);
-    if (!rs_ok) return false;
+    if (__builtin_expect(!rs_ok, 0)) return false;
     unsigned long long t_k = STAMP_T();
     const bool kok = kkt_check(P, lab, x, y, nl);
     STAMP_ADD(NV == 1 ? ST_XKKT : ST_ZKKT, t_k);
-    if (kok) return true;
+    if (__builtin_expect(kok, 1)) return true;
     bool same = true;
 #pragma unroll
     for (int s = 0; s < NR; ++s) same &= (nl[s] == lab[s]);
@@ -1900,7 +1900,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
   signed char plab[NR];
 #pragma unroll
   for (int s = 0; s < NR; ++s) plab[s] = -1;
-  if (!ok && !P.kready) {
+  if (__builtin_expect(!ok && !P.kready, 0)) {
     if (!P.scaled) {
       // the warm ADMM state is in identity scaling (x, A x, y): move it to the Ruiz space
       if (P.wraw) warm_to_scaled(P, xs, zs, ys);     // identity D, E: (x, A x, y)
@@ -1938,9 +1938,9 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
     if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
     wsync();
   }
-  if (!ok) ensure_q(P);
+  if (__builtin_expect(!ok, 0)) ensure_q(P);
   if (!ok && P.wraw) warm_to_scaled(P, xs, zs, ys);
-  for (int it = 1; !ok && it <= max_inner; ++it) {
+  for (int it = 1; __builtin_expect(!ok, 0) && it <= max_inner; ++it) {
     unsigned long long t_a = STAMP_T();
     admm_iter(P, xs, zs, ys);
     STAMP_ADD(ST_ADMM, t_a);
@@ -2096,7 +2096,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
   const int li = l < HCAP ? l : 0;
   // P depends on the agent's speed only (make_geo): K_s^-1, P^-1 and the scaling are
   // cached in HBM per scenario and rebuilt only when the ADMM penalty differs.
-  if (A.xcache_rho[a] == P.rho) {
+  if (__builtin_expect(A.xcache_rho[a] == P.rho, 1)) {
     P.D[0] = in ? sc[li] : 0.0;
     P.E[0] = in ? sc[HCAP + li] : 0.0;
     P.E[1] = (l < H - 1) ? sc[2 * HCAP + li] : 0.0;
@@ -2155,7 +2155,7 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
 
   // ---- P_v^-1 blocks (HBM), Y = P_v^-1 T' (PGt, unscaled by g) and Z_v = T P_v^-1 T' (GPG):
   // speed-only, so built once per scenario; g1, g2 scale them on the fly (s_gather, x recovery)
-  if (!A.ecache[e]) {
+  if (__builtin_expect(!A.ecache[e], 0)) {
     double* Yl = Ke_lds;             // H x n staging (the Ke region is rebuilt below)
     double* Pi = A.tab_e + (size_t)e * 8 * H * H;
     for (int v = 0; v < 2; ++v) {
@@ -2689,14 +2689,14 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
                          (!c.term_dist_check || dc0 > deff);
       // last_iter_hat_pos = hat_pos_old: only a z-step changes hat, so the copy is needed
       // only after one (S.last already equals hat otherwise)
-      if (act && !stop0 && !c.alias_dual_residual)
+      if (__builtin_expect(act && !stop0 && !c.alias_dual_residual, 0))
         for (int i = l; i < 4 * H1; i += WAVE) S.last[i] = S.hat[i];
       STAMP_ADD(ST_TERMW, t_tw);
     }
     // second barrier only after a z-step (it wrote hat, lam, S, D, last and S.sc); without
     // one every wave takes the stop decision from its registers (rk = sk = 0)
     unsigned long long t_sb = STAMP_T();
-    if (act) __syncthreads();
+    if (__builtin_expect(act, 0)) __syncthreads();
     STAMP_ADD(ST_SYNC_B, t_sb);
     const double rk = act ? S.sc[0] : 0.0;
     const double sk = act ? S.sc[1] : 0.0;
@@ -2818,7 +2818,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       A.status[a] = status_x;
       A.rho_x[a] = qx.rho;
     }
-    if (A.xcache_rho[a] != qx.rho) {       // adaptive rho rebuilt K_s^-1 in LDS: refresh the cache
+    if (__builtin_expect(A.xcache_rho[a] != qx.rho, 0)) {   // adaptive rho rebuilt K_s^-1: refresh the cache
       double* Kc = A.Kx_cache + (size_t)a * H * H;
       if (qx.kf32) {
         for (int i = l; i < H * H; i += WAVE) Kc[i] = (double)qx.Kf[i];   // the fp32 image
