@@ -248,14 +248,14 @@ __device__ __forceinline__ void affine_c(const Geo& g, double dt, int H, double&
 // Numeric rollouts at time lanes (u at var lanes).  Linear: dynamic_update_local
 // numeric branch (PI_ADMM_class.py:56-70).  Nonlinear: dynamic_update_edge
 // numeric branch (:88-105) = MATLAB numeric dynamic_update_local (:312-330).
-__device__ __forceinline__ void rollout(const double* xt3, double s, double u, const piadmm_config_t& c, int H,
-                        bool nonlinear, double& px, double& py, double& pth) {
+// (x0, y0, theta0, s, s/L) in registers: the per-iteration x-step rollout reads no memory
+__device__ __forceinline__ void rollout_r(double x0, double y0, double th0, double s, double sl, double u,
+                                          const piadmm_config_t& c, int H, bool nonlinear, double& px, double& py,
+                                          double& pth) {
 #pragma clang fp contract(off)
   const int l = lid();
-  const double th0 = xt3[2];
-  const double sn0 = sin(th0), cs0 = cos(th0);
   // theta_k = theta_0 + sum_{j<k} (s/L u_j) dt  (wave prefix scan)
-  const double inc = (l < H) ? (s / c.L * u) * c.dt : 0.0;
+  const double inc = (l < H) ? (sl * u) * c.dt : 0.0;
   const double my_th = th0 + shup(scan_incl(inc), 1);
   // per-lane rates at time k = lane
   double xd, yd;
@@ -265,14 +265,19 @@ __device__ __forceinline__ void rollout(const double* xt3, double s, double u, c
     xd = -s * sk * my_th + (s * ck + s * my_th * sk);
     yd = s * ck * my_th + (s * sk - s * my_th * ck);
   } else {
+    const double sn0 = sin(th0), cs0 = cos(th0);
     xd = -s * sn0 * my_th + (s * cs0 + s * th0 * sn0);
     yd = s * cs0 * my_th + (s * sn0 - s * th0 * cs0);
   }
   const double xi = (l < H) ? xd * c.dt : 0.0, yi = (l < H) ? yd * c.dt : 0.0;
-  px = xt3[0] + shup(scan_incl(xi), 1);
-  py = xt3[1] + shup(scan_incl(yi), 1);
+  px = x0 + shup(scan_incl(xi), 1);
+  py = y0 + shup(scan_incl(yi), 1);
   pth = my_th;
   if (l > H) px = py = pth = 0.0;
+}
+__device__ __forceinline__ void rollout(const double* xt3, double s, double u, const piadmm_config_t& c, int H,
+                        bool nonlinear, double& px, double& py, double& pth) {
+  rollout_r(xt3[0], xt3[1], xt3[2], s, s / c.L, u, c, H, nonlinear, px, py, pth);
 }
 
 // ============================================================ in-wave dense kernels
@@ -2493,6 +2498,15 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
   if (coop && ci == 0)
     for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) A.ghist[(size_t)slot * 2 * c.max_outer + i] = NAN;
+  // the own agent's start state and speed in registers for the per-iteration rollout
+  double rl_x0 = 0.0, rl_y0 = 0.0, rl_th0 = 0.0, rl_s = 0.0, rl_sl = 0.0;
+  if (w < na) {
+    rl_x0 = S.xt[3 * w + 0];
+    rl_y0 = S.xt[3 * w + 1];
+    rl_th0 = S.xt[3 * w + 2];
+    rl_s = A.spd[a0 + w];
+    rl_sl = rl_s / c.L;
+  }
   // reference positions of the own agent at time lanes (fixed for the step)
   double rx_own = 0.0, ry_own = 0.0;
   if (w < na && l <= H) {
@@ -2544,7 +2558,17 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 #ifdef PIADMM_DIAG_NO_ROLL  // diagnostic timing build only: skip the rollout
       px = py = pth = u;
 #else
-      rollout(S.xt + 3 * w, A.spd[a], (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+      rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+#ifdef PIADMM_DIAG_ROLL2     // diagnostic timing build only: the rollout twice (same result)
+      {
+        double u2 = (l < H) ? u : 0.0, qx2, qy2, qt2;
+        asm volatile("" : "+v"(u2));
+        rollout(S.xt + 3 * w, A.spd[a], u2, c, H, nonlin_pos, qx2, qy2, qt2);
+        asm volatile("" : "+v"(qx2), "+v"(qy2), "+v"(qt2));
+        asm volatile("" : : "v"(px), "v"(py), "v"(pth));
+        px = qx2; py = qy2; pth = qt2;
+      }
+#endif
 #endif
       STAMP_ADD(ST_XROLL, t_r);
       if (l <= H) {
