@@ -2515,6 +2515,18 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     ry_own = rp[A.T + t + l];
   }
 
+  // the x-step's consensus term (cx - hat + lam) of the own direction in registers: hat and lam
+  // change only in a z-step, after which it is reloaded (behind the second barrier)
+  const bool cpl = w < na && nnb > 0 && e >= 0 && l <= H;
+  double cpx = 0.0, cpy = 0.0;
+  auto load_cp = [&]() {
+    if (cpl) {
+      const int d = w;   // agent local 0 owns hat_{v1 v2} (dir 0), agent 1 dir 1
+      cpx = cx_own - S.hat[(d * 2 + 0) * H1 + l] + S.lam[(d * 2 + 0) * H1 + l];
+      cpy = cy_own - S.hat[(d * 2 + 1) * H1 + l] + S.lam[(d * 2 + 1) * H1 + l];
+    }
+  };
+  load_cp();
   for (int it = it0; it < it1; ++it) {
     iters = it + 1;
     // this iteration's pos_old buffer: a wave may start the next iteration's x-step while
@@ -2526,10 +2538,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       const int a = a0 + w;
       const bool tl = l <= H;
       double vx = 2.0 * c.Pnorm * (cx_own - rx_own), vy = 2.0 * c.Pnorm * (cy_own - ry_own);
-      if (nnb > 0 && e >= 0 && tl) {
-        const int d = w;   // agent local 0 owns hat_{v1 v2} (dir 0), agent 1 dir 1
-        vx = vx + c.rho * (cx_own - S.hat[(d * 2 + 0) * H1 + l] + S.lam[(d * 2 + 0) * H1 + l]);
-        vy = vy + c.rho * (cy_own - S.hat[(d * 2 + 1) * H1 + l] + S.lam[(d * 2 + 1) * H1 + l]);
+      if (cpl) {
+        vx = vx + c.rho * cpx;
+        vy = vy + c.rho * cpy;
       }
       const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
       const double wsh = shdn(wt, 1);
@@ -2720,7 +2731,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     // second barrier only after a z-step (it wrote hat, lam, S, D, last and S.sc); without
     // one every wave takes the stop decision from its registers (rk = sk = 0)
     unsigned long long t_sb = STAMP_T();
-    if (__builtin_expect(act, 0)) __syncthreads();
+    if (__builtin_expect(act, 0)) {
+      __syncthreads();
+      load_cp();
+    }
     STAMP_ADD(ST_SYNC_B, t_sb);
     const double rk = act ? S.sc[0] : 0.0;
     const double sk = act ? S.sc[1] : 0.0;
