@@ -594,9 +594,9 @@ __device__ __forceinline__ void At_mul(const QP<NV>& P, const double* w, double*
 // tables cost one latency per batch, not one per column.
 constexpr int GEMV_U = 8;
 #ifndef PIADMM_XGEMV_U
-#define PIADMM_XGEMV_U 8
+#define PIADMM_XGEMV_U 15
 #endif
-constexpr int XGEMV_U = PIADMM_XGEMV_U;   // batch of the x-step fused pass (registers in flight)
+constexpr int XGEMV_U = PIADMM_XGEMV_U;   // x-step fused pass batch, LDS mode (big mode: 8; tools/xcost.py)
 template <bool BD, int NV, typename Ptr>
 __device__ __forceinline__ void gemv_sym(const QP<NV>& P, Ptr M, const double* r, double* y) {
   const int l = lid();
@@ -1192,6 +1192,7 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   return true;
 }
 
+template <int XU>
 __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed char* lab, double* x, double* y) {
   const int l = lid(), H = P.H;
   unsigned long long t_pre = STAMP_T();
@@ -1247,15 +1248,35 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
   {
     const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
     const double* G = P.G;
-    constexpr int XU = XGEMV_U;
-    for (int j0 = 0; j0 < H; j0 += XU) {
+    // full batches: row pointers advance by a stride, no clamp
+    const int Hf = H - H % XU;
+    const double* gp = G + lc;
+    const double* xp = XT + la;
+    const int xs = P.xld;
+    for (int j0 = 0; j0 < Hf; j0 += XU) {
       double qv[XU], gv[XU], xv[XU];
 #pragma unroll
       for (int u = 0; u < XU; ++u) {
-        const int j = min(j0 + u, H - 1);
-        qv[u] = vb_q[j0 + u];          // 0 beyond H (j0 + u < 64)
+        qv[u] = vb_q[j0 + u];
+        gv[u] = gp[u * H];
+        xv[u] = xp[u * xs];
+      }
+      gp += XU * H;
+      xp += XU * xs;
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        ag += gv[u] * qv[u];
+        ax += xv[u] * qv[u];
+      }
+    }
+    if (Hf < H) {                       // tail: rows clamped to H - 1, q is 0 beyond H
+      double qv[XU], gv[XU], xv[XU];
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        const int j = min(Hf + u, H - 1);
+        qv[u] = vb_q[Hf + u];
         gv[u] = G[j * H + lc];
-        xv[u] = XT[j * P.xld + la];
+        xv[u] = XT[j * xs + la];
       }
 #pragma unroll
       for (int u = 0; u < XU; ++u) {
@@ -1334,7 +1355,7 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
   return wall(ok);
 }
 
-template <int NV>
+template <int NV, int XU = XGEMV_U>
 __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y, int& nsolve,
                                      int steps = PDAS_STEPS) {
   constexpr int NR = QP<NV>::NR;
@@ -1343,7 +1364,7 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
     ++nsolve;
     unsigned long long t_r = STAMP_T();
     bool rs_ok;
-    if constexpr (NV == 1) rs_ok = reduced_solve_x(P, lab, x, y);
+    if constexpr (NV == 1) rs_ok = reduced_solve_x<XU>(P, lab, x, y);
     else rs_ok = reduced_solve(P, lab, x, y);
     STAMP_ADD(NV == 1 ? ST_XRED : ST_ZRED, t_r);
     if (__builtin_expect(!rs_ok, 0)) return false;
@@ -1847,7 +1868,7 @@ __device__ __forceinline__ void warm_to_scaled(QP<NV>& P, double* xs, double* zs
 #define PIADMM_ADAPT_EVERY 25
 #endif
 constexpr int ADAPT_EVERY = PIADMM_ADAPT_EVERY;
-template <int NV, bool TWO>
+template <int NV, bool TWO, int XU = XGEMV_U>
 __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
                                         bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
                                         double* x_out, int& n_admm, int& n_pdas, int& n_gi) {
@@ -1865,7 +1886,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       // its certificate fails, the dual active set warm-started from those labels finds the
       // new working set in a few steps, and one reduced solve on it certifies (instead of a
       // table rebuild per one-step PDAS label move, then ADMM)
-      ok = pdas(P, lab, x, y, n_pdas, 1);
+      ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
       if (__builtin_expect(!ok, 0)) {
         int ngi = 0;
         signed char glab[NR];
@@ -1873,17 +1894,17 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         if (gi_solve(P, flab, glab, x, y, ngi)) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = glab[s];
-          ok = pdas(P, lab, x, y, n_pdas);
+          ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
         }
         n_gi += ngi;
         if (!ok) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = flab[s];
-          ok = pdas(P, lab, x, y, n_pdas);
+          ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
         }
       }
     } else {
-      ok = pdas(P, lab, x, y, n_pdas);
+      ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
     }
   }
   if constexpr (NV == 2) {
@@ -1897,7 +1918,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         ok = kkt_check(P, glab, x, y, nl);
 #pragma unroll
         for (int s = 0; s < NR; ++s) lab[s] = glab[s];
-        if (!ok) ok = pdas(P, lab, x, y, n_pdas);
+        if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
       }
       n_gi += ngi;
     }
@@ -1977,7 +1998,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       if ((wall(same) || it % (8 * polish_every) == 0) && !wall(tried)) {
 #pragma unroll
         for (int s = 0; s < NR; ++s) flab[s] = lab[s];
-        ok = pdas(P, lab, x, y, n_pdas);
+        ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
       }
     }
   }
@@ -2553,7 +2574,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       const int stx = 0;
       ustar[0] = 1e-3 * qx.wq;
 #else
-      const int stx = qp_solve<1, false>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n_admm_x, n_pdas_x, n_gi);
 #endif
       STAMP_ADD(ST_XQP, t_q);
