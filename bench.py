@@ -1,53 +1,75 @@
 #!/usr/bin/env python3
-"""Benchmark: PI-ADMM outer iterations/s at 256 agents x H=30 per GPU (BASELINE.json configs[2]).
+"""Benchmark: PI-ADMM outer iterations/s and ms per MPC step (BASELINE.json metric).
 
-One "step" = one MPC step of the full PI anti-windup loop (matlab_pi preset:
-x-step QPs of all agents, collision graph, pair z-step QPs, PI + back-calculation
-dual update, residuals) run for a fixed ``max_outer`` = 100 outer iterations
-(termination disabled), plus propagation.  Inputs (scenario,
-states) are resident in HBM before the timed region; the library's MPC loop
-never returns to the host inside it.
+Workloads (BASELINE.json configs; synthetic seeded tiles of the reference's two-vehicle
+intersection, inputs resident in HBM before the timed region):
 
-  python bench.py [--gpus N --steps K --warmup W]
+  default      configs[2]: 256 agents x H30 per GPU, matlab_pi preset (PI anti-windup), the
+               reference's global termination scope, FIXED 100 outer iterations per MPC step
+                -- the headline ``value`` -- plus, in the same line, the same
+               workload under NATURAL global termination (``natural``: the latency a planner
+               sees per MPC step)
+  --config2    configs[1]: 64 agents x H20, casadi_default, fixed 200 outer iterations (C2)
+  --config5    configs[4]: 256 agents x H50 with delay tightening
+  --strong     configs[3]: 1024 agents x H30 in total, sharded over the N ranks (strong scaling)
 
-The job runs with the reference's global termination scope (term_global, quirk B9):
-all agents of all ranks form one ADMM job whose residual history (rk, sk summed over
-every pair) is the reference's.  With fixed iterations that is one fused launch per
-MPC step plus one RCCL all-reduce of the 2 x 100 residual partials over xGMI.
+One "step" = one MPC step of the full loop (x-step QPs of all agents, collision graph, pair
+z-step QPs, PI + back-calculation dual update, residuals) plus propagation; the library's MPC
+loop never returns to the host inside the timed region.
 
-N>1: launched by torch.distributed.run, one process per GPU; each rank owns its
-own 128 intersection tiles (256 agents), so per-GPU work is fixed ("weak").
-Components never straddle ranks; the ranks join one RCCL communicator (the unique
-id travels over torch.distributed's gloo group, which is otherwise only the
-harness's barrier and max-over-ranks timer).
+  python bench.py [--gpus N --steps K --warmup W] [--config2 | --config5 | --strong] [--natural]
 
---natural: natural termination instead, reported as its own line: on one rank the stop
-test runs in-kernel behind a grid barrier (cooperative launch, several steps per launch);
-across ranks one launch + one RCCL all-reduce of the termination partials per outer
-iteration, host decision.
+N > 1: one process per GPU (torch.distributed.run).  Run directly with --gpus N and no
+WORLD_SIZE in the environment, this script starts ``torch.distributed.run --nproc-per-node N``
+as a child process before anything touches the GPU and relays its output.  Each rank owns
+whole components; the ranks join one RCCL communicator (the unique id travels over the gloo
+group, which otherwise only carries the harness's barrier and max-over-ranks timer).
 
-Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects.
+Prints ONE JSON line (rank 0) with roofline, latency and cpu_baseline objects.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "distributed-local-planner-pi-admm_amd"))
 
-import numpy as np  # noqa: E402
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md)
+PEAK_FP64_TFLOPS = 78.6     # MI355X fp64 vector (256 CU x 4 SIMD x 16 lanes x 2 x 2.4 GHz)
+CLOCK_GHZ = 2.4             # max shader clock (MI355X_MICROARCH.md)
+METRIC = "PI-ADMM outer iterations/sec (and ms/MPC step) at N_agents×H; 1/2/4/8 GPU"
 
-from piadmm import _lib, config, scenario  # noqa: E402
+WORKLOADS = {
+    # name: (tiles per GPU or total, H, preset, max_outer, tighten, scaling)
+    "c3": dict(tiles=128, H=30, preset="matlab_pi", max_outer=100, tighten=0, scaling="weak",
+               desc="256 agents x H30 per GPU (128 tiles), matlab_pi preset (PI anti-windup)"),
+    "c2": dict(tiles=32, H=20, preset="casadi_default", max_outer=200, tighten=0, scaling="weak",
+               desc="64 agents x H20 per GPU (32 tiles), casadi_default preset (plain dual)"),
+    "c5": dict(tiles=128, H=50, preset="matlab_pi", max_outer=100, tighten=1, scaling="weak",
+               desc="256 agents x H50 per GPU (128 tiles), matlab_pi + delay tightening p=0.95"),
+    "c4": dict(tiles=512, H=30, preset="matlab_pi", max_outer=100, tighten=0, scaling="strong",
+               desc="1024 agents x H30 in total (512 tiles) sharded over the GPUs, matlab_pi preset"),
+}
 
-N_TILES = 128          # 256 agents
-H = 30
-MAX_OUTER = 100
-PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+def spawn_ranks(n: int) -> int:
+    """Start torch.distributed.run with n ranks as a child process (before any HIP call)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def algorithmic_bytes(cnt: dict, H: int) -> float:
@@ -71,186 +93,250 @@ def algorithmic_bytes(cnt: dict, H: int) -> float:
     return b
 
 
-def latest_traffic(workload: str):
-    """HBM bytes per launch from the newest committed PMC summary (profiles/traffic_<tag>.json,
-    tags sort by round: r01 < r01b < r01c ...) for this workload, else None."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")), reverse=True):
+def latest_profile(kind: str, workload: str):
+    """Newest committed profile summary profiles/<kind>_r*.json for this workload (tags sort by
+    round: r01 < r01b < ... < r02 < r02b), else None."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"{kind}_r*.json")), reverse=True):
         try:
             with open(path) as f:
                 tj = json.load(f)
         except (OSError, ValueError):
             continue
-        if tj.get("workload") == workload and tj.get("hbm_bytes_per_step"):
-            return tj["hbm_bytes_per_step"]
+        if tj.get("workload") == workload:
+            tj["_file"] = os.path.relpath(path, ROOT)
+            return tj
     return None
 
 
-def cpu_baseline(n_tiles: int, budget_s: float, H: int = H, tighten: int = 0) -> dict:
-    """Time the NumPy oracle (the reference's loop structure, one QP at a time) on a bounded sample."""
+def cpu_baseline(wl: dict, budget_s: float) -> dict:
+    """The CPU baseline on this host: the B-opt C++ / OpenMP build of the loop when it is built
+    (oracle/cpu_ref, all host cores), else the NumPy oracle on one core (bounded sample)."""
     sys.path.insert(0, ROOT)
+    from piadmm import config, scenario
+    n_tiles, H = wl["tiles"], wl["H"]
+    cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=1, max_outer=wl["max_outer"], tighten=wl["tighten"])
+    try:
+        from oracle import cpu_ref
+        if cpu_ref.available():
+            return cpu_ref.time_baseline(cfg, n_tiles, budget_s)
+    except ImportError:
+        pass
     from oracle import piadmm_oracle as O
     try:
         from threadpoolctl import threadpool_limits
     except ImportError:      # pragma: no cover
         threadpool_limits = None
-    cfg = config.matlab_pi(H=H, fixed_iters=1, max_outer=MAX_OUTER, tighten=tighten)
-    scn = scenario.tiled(N_TILES, H, n_steps=4)
-    done_tiles = 0
-    t_used = 0.0
+    scn = scenario.tiled(n_tiles, H, n_steps=4)
+    done, t_used = 0, 0.0
     limit = threadpool_limits(limits=1) if threadpool_limits else None   # one core
     try:
         orc = O.Oracle(cfg, scn)
-        for c in range(min(n_tiles, orc.n_comp)):
+        for c in range(orc.n_comp):
             orc.xt = scn.xt0.copy()
             orc.t = 0
             t0 = time.perf_counter()
             orc.mpc_step(components=[c])
             t_used += time.perf_counter() - t0
-            done_tiles += 1
+            done += 1
             if t_used > budget_s:
                 break
     finally:
         if limit is not None:
             limit.restore_original_limits()
-    per_tile_iter = t_used / (done_tiles * MAX_OUTER)
-    it_s = 1.0 / (per_tile_iter * N_TILES)
+    it_s = 1.0 / (t_used / (done * wl["max_outer"]) * n_tiles)
     return {"value": it_s, "unit": "outer_iters/s", "cores": 1, "kind": "port",
             "sample": f"NumPy oracle (oracle/piadmm_oracle.py, exact active-set QPs, one QP at a time "
-                      f"like casadi/main.py), MPC step t=0 of {done_tiles} of {N_TILES} tiles x "
-                      f"{MAX_OUTER} outer iterations, {t_used:.1f} s, scaled linearly to 128 tiles; "
+                      f"like casadi/main.py), MPC step t=0 of {done} of {n_tiles} tiles x "
+                      f"{wl['max_outer']} outer iterations, {t_used:.1f} s, scaled linearly to {n_tiles} tiles; "
                       f"host {platform.processor() or platform.machine()}, {os.cpu_count()} cpus visible"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    # default warmup = default steps: the warmup launch and the timed launch of k_mpc_step have
-    # the same size, so rocprofv3's per-kernel average over the run compares with avg_launch_ms
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle timing (rank 0, N=1)")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--natural", action="store_true", help="natural (global) termination, not the headline")
-    ap.add_argument("--config5", action="store_true",
-                    help="BASELINE configs[4]: H=50 with delay tightening (not the headline)")
-    args = ap.parse_args()
-    H = 50 if args.config5 else globals()["H"]
-    tighten = 1 if args.config5 else 0
-
-    lib = _lib.load()                       # HIP runtime loaded before torch (same SONAME)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-
+def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_rank: int, dist):
+    """Time K MPC steps of workload wl on this rank; returns (metrics, counters, solver info)."""
+    from piadmm import config, scenario
+    from piadmm import dist as pdist
     from piadmm.solver import PI_ADMM_MI355X
-    K, W = args.steps, args.warmup
+    H, M = wl["H"], wl["max_outer"]
+    cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=0 if natural else 1, max_outer=M, term_global=1,
+                                       tighten=wl["tighten"])
     n_steps = max(K, W, 1)
-    cfg = config.matlab_pi(H=H, fixed_iters=0 if args.natural else 1, max_outer=MAX_OUTER, term_global=1,
-                           tighten=tighten)
-    scn = scenario.tiled(N_TILES, H, n_steps=n_steps, perturb=True, seed=1000 * rank)
+    if wl["scaling"] == "strong":
+        scn = pdist.shard(scenario.tiled(wl["tiles"], H, n_steps=n_steps, perturb=True, seed=0), rank, world)
+    else:
+        scn = scenario.tiled(wl["tiles"], H, n_steps=n_steps, perturb=True, seed=1000 * rank)
     solver = PI_ADMM_MI355X(cfg, scn, device=local_rank)
-    if dist is not None:
-        from piadmm import dist as pdist
-
-        def bcast(b):
-            obj = [b]
-            dist.broadcast_object_list(obj, src=0)
-            return obj[0]
-        pdist.attach_rccl(solver, rank, world, bcast)
-
-    # warmup: W steps from t=0, then reset the state so the timed steps repeat t=0..K-1
-    if W > 0:
-        solver.steps_async(0, W)
-        solver.sync()
-    solver.set_xt(scn.xt0)
-    solver.reset_counters()
-
-    def barrier():
+    try:
+        if dist is not None:
+            def bcast(b):
+                obj = [b]
+                dist.broadcast_object_list(obj, src=0)
+                return obj[0]
+            pdist.attach_rccl(solver, rank, world, bcast)
+        # warmup: W steps from t=0 (per-scenario setup caches are built here), then the state is
+        # reset (xt0, warm labels, ADMM penalties) so the timed steps replay t = 0 .. K-1
+        if W > 0:
+            solver.steps_async(0, W)
+            solver.sync()
+        solver.set_xt(scn.xt0)
+        solver.reset_counters()
         if dist is not None:
             dist.barrier()
-
-    barrier()
-    solver.sync()
-    t0 = time.perf_counter()
-    ev_ms = solver.time_steps(0, K)          # hipEvents on the library's stream around the K launches
-    solver.sync()
-    wall = time.perf_counter() - t0
-    barrier()
-    cnt = solver.counters()
+        solver.sync()
+        t0 = time.perf_counter()
+        ev_ms = solver.time_steps(0, K)        # hipEvents on the library's stream around the launches
+        solver.sync()
+        wall = time.perf_counter() - t0
+        if dist is not None:
+            dist.barrier()
+        cnt = solver.counters()
+        spl, C, N = solver.steps_per_launch(), max(solver.C, 1), solver.N
+    finally:
+        solver.close()
     if dist is not None:
         import torch
         tt = torch.tensor([wall, ev_ms], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, ev_ms = float(tt[0]), float(tt[1])
+    job_iters = cnt["outer_iters"] / C                  # iterations of the job (every component runs them)
+    # k_mpc_step launches in the timed region: one persistent launch per steps_per_launch() steps,
+    # or (natural termination across ranks) one per outer iteration plus one per step
+    n_launch = -(-K // spl) if spl > 1 else int(job_iters) + K
+    return dict(wall=wall, ev_ms=ev_ms, job_iters=job_iters, n_launch=n_launch, spl=spl, N=N, C=C), cnt
 
-    outer_total = world * cnt["outer_iters"] / max(solver.C, 1)      # job iterations x ranks
-    value = outer_total / wall
-    # k_mpc_step launches in the timed region: one persistent launch per steps_per_launch()
-    # MPC steps (fixed iterations; natural global termination on one rank, where the stop
-    # test runs in-kernel behind a grid barrier), or -- natural termination across ranks --
-    # one per outer iteration plus one per step (each launch's share of the time taken equal)
-    spl = solver.steps_per_launch()
-    n_launch = -(-K // spl) if spl > 1 else int(cnt["outer_iters"] / max(solver.C, 1)) + K
-    avg_launch_s = (ev_ms / 1e3) / n_launch
-    bytes_launch = algorithmic_bytes(cnt, H) / n_launch
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline timing (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-natural", action="store_true", help="skip the natural-termination co-headline")
+    ap.add_argument("--natural", action="store_true", help="natural termination as the headline itself")
+    g = ap.add_mutually_exclusive_group()
+    g.add_argument("--config2", action="store_true", help="BASELINE configs[1]: 64 agents x H20")
+    g.add_argument("--config5", action="store_true", help="BASELINE configs[4]: H=50 with delay tightening")
+    g.add_argument("--strong", action="store_true", help="BASELINE configs[3]: 1024 agents sharded over N GPUs")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:
+        if args.gpus > 1:          # direct call: become the launcher, before any HIP call
+            sys.exit(spawn_ranks(args.gpus))
+        world = 1
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    from piadmm import _lib
+    lib = _lib.load()                       # HIP runtime loaded before torch (same SONAME)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    key = "c2" if args.config2 else "c5" if args.config5 else "c4" if args.strong else "c3"
+    wl = WORKLOADS[key]
+    H, M = wl["H"], wl["max_outer"]
+    K, W = args.steps, args.warmup
+    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist)
+
+    # value = units all ranks processed / the max-over-ranks wall time.  Weak scaling: one unit =
+    # one outer iteration of a rank's (256-agent) block, so all ranks processed world x job
+    # iterations; strong scaling: the unit is an outer iteration of the whole 1024-agent job.
+    units = m["job_iters"] * (world if wl["scaling"] == "weak" else 1)
+    value = units / m["wall"]
+    agents_job = m["N"] * world if wl["scaling"] == "weak" else 2 * wl["tiles"]
+    avg_launch_s = (m["ev_ms"] / 1e3) / m["n_launch"]
+    bytes_launch = algorithmic_bytes(cnt, H) / m["n_launch"]
     achieved = bytes_launch / avg_launch_s / 1e9
-
-    traffic_step = latest_traffic(f"tiled{N_TILES}_H{H}_matlab_pi_fixed{MAX_OUTER}") if not args.natural else None
-    traffic = traffic_step * K / n_launch if traffic_step else None
+    wname = f"tiled{wl['tiles']}_H{H}_{wl['preset']}_fixed{M}" + ("_tight" if wl["tighten"] else "")
+    traffic = latest_profile("traffic", wname) if not args.natural else None
+    traffic_launch = traffic["hbm_bytes_per_step"] * K / m["n_launch"] if traffic else None
+    sq = latest_profile("sq", wname) if not args.natural else None
 
     line = {
-        "metric": "PI-ADMM outer iterations/sec (and ms/MPC step) at N_agents×H; 1/2/4/8 GPU",
+        "metric": METRIC,
         "value": value,
         "unit": "outer_iters/s",
         "n_gpus": world,
         "steps": K,
         "warmup": W,
-        "ms_per_step": wall / K * 1e3,
+        "ms_per_step": m["wall"] / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl["scaling"],
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: 128 seeded tiles of the reference 2-vehicle intersection per GPU",
+        "data": f"synthetic: seeded tiles of the reference 2-vehicle intersection ({agents_job} agents in the job)",
         "config": {
-            "workload": f"256 agents x H{H} per GPU (128 tiles), matlab_pi preset (PI anti-windup), "
-                        + ("delay tightening p=0.95 (configs[4]), " if tighten else "")
-                        + (f"global natural termination (max {MAX_OUTER} outer iterations)" if args.natural else
-                           f"{MAX_OUTER} outer iterations per MPC step (fixed), global residual history"),
-            "agents_per_gpu": 2 * N_TILES, "horizon": H,
-            "outer_iters_per_step": outer_total / world / K,
+            "workload": wl["desc"] + ", " + (
+                f"global natural termination (max {M} outer iterations)" if args.natural else
+                f"{M} outer iterations per MPC step (fixed), global residual history"),
+            "agents_per_gpu": m["N"], "agents_total": agents_job, "horizon": H,
+            "outer_iters_per_step": m["job_iters"] / K,
+            "job_outer_iters_per_s": m["job_iters"] / m["wall"],
+            "agent_qps_per_s": cnt["x_qps"] * world / m["wall"],
             "parallelism": f"components sharded over {world} GPU(s); " + (
                 ("one RCCL all-reduce of the termination partials per outer iteration" if world > 1 else
                  "stop test in-kernel behind a grid barrier (cooperative launch)") if args.natural else
-                "one RCCL all-reduce of the residual history per MPC step") + (" (single rank: none)" if world == 1 else ""),
+                "one RCCL all-reduce of the residual history per persistent launch") + (
+                " (single rank: none)" if world == 1 else ""),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+            "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_launch,
             "kernel": "pd::k_mpc_step", "avg_launch_ms": avg_launch_s * 1e3,
-            "steps_per_launch": spl, "launches": n_launch,
+            "steps_per_launch": m["spl"], "launches": m["n_launch"],
             "algorithmic_bytes_per_launch": bytes_launch,
-            "note": "latency-bound: one dependent ADMM/PDAS chain per wave; see DESIGN.md",
+            "traffic_source": traffic["_file"] if traffic else None,
+            "note": "not bandwidth-bound: the algorithmic bytes stay in LDS; see latency and DESIGN.md §5",
         },
         "inner": {
             "x_qps_per_step": cnt["x_qps"] / K, "z_qps_per_step": cnt["z_qps"] / K,
+            "z_qps_per_outer_iter": cnt["z_qps"] / max(m["job_iters"], 1),
             "admm_iters_per_xqp": cnt["admm_x"] / max(cnt["x_qps"], 1),
             "admm_iters_per_zqp": cnt["admm_z"] / max(cnt["z_qps"], 1),
             "pdas_solves_per_xqp": cnt["pdas_x"] / max(cnt["x_qps"], 1),
             "pdas_solves_per_zqp": cnt["pdas_z"] / max(cnt["z_qps"], 1),
             "inexact_qps": cnt["inexact"],
         },
+        "latency": None,
+        "fp64": None,
         "cpu_baseline": None,
     }
+    # latency model: the kernel runs one dependent QP chain per wave; cycles per wave per outer
+    # iteration from this run's launch time, against the issue bound from the committed SQ counters
+    # (VALU wave-instructions x 4 cycles: a wave64 fp64 VALU op occupies a 16-lane SIMD 4 cycles)
+    cyc_iter = avg_launch_s * m["n_launch"] * CLOCK_GHZ * 1e9 / max(m["job_iters"], 1)
+    lat = {"cycles_per_outer_iter_per_wave": cyc_iter, "clock_ghz_assumed": CLOCK_GHZ}
+    if sq:
+        lat.update({k: sq[k] for k in ("valu_insts_per_wave_iter", "lds_insts_per_wave_iter",
+                                       "salu_insts_per_wave_iter", "wave_cycles_per_wave_iter") if k in sq})
+        if "valu_insts_per_wave_iter" in sq:
+            bound = 4.0 * sq["valu_insts_per_wave_iter"]
+            lat["issue_bound_cycles"] = bound
+            lat["frac"] = bound / cyc_iter
+        lat["source"] = sq["_file"]
+        if "fp64_flops_per_step" in sq:
+            gf = sq["fp64_flops_per_step"] * K / (m["ev_ms"] / 1e3) / 1e9
+            line["fp64"] = {"gflops": gf, "peak_tflops": PEAK_FP64_TFLOPS, "frac": gf / (PEAK_FP64_TFLOPS * 1e3),
+                            "source": sq["_file"] + " (SQ_INSTS_VALU_{ADD,MUL,FMA}_F64 x 64 lanes; FMA = 2)"}
+    line["latency"] = lat
+
+    if not args.natural and not args.no_natural:
+        mn, cn = run(wl, True, K, W, rank, world, local_rank, dist)
+        line["natural"] = {
+            "ms_per_step": mn["wall"] / K * 1e3,
+            "outer_iters_per_step": mn["job_iters"] / K,
+            "outer_iters_per_s": mn["job_iters"] * (world if wl["scaling"] == "weak" else 1) / mn["wall"],
+            "z_qps_per_outer_iter": cn["z_qps"] / max(mn["job_iters"], 1),
+            "steps_per_launch": mn["spl"],
+            "note": "same workload, the reference's stop test on (casadi/main.py:174-178): the per-step latency",
+        }
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(N_TILES, args.cpu_budget, H, tighten)
+        line["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
         line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
-    solver.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -1,0 +1,1675 @@
+// pd_qp.h -- the per-wave QP solver of libpiadmm: generalised QP with box / rate / hinge
+// rows, OSQP-style ADMM in a Ruiz-scaled space, PDAS polish on the reduced KKT system,
+// parametric x-step tables and the Goldfarb-Idnani dual active set (not part of the ABI).
+#pragma once
+#include "pd_common.h"
+
+namespace pd {
+
+// ============================================================ QP solver
+// Generalised QP  min 1/2 x'Px + q'x + sum_r phi_r(a_r'x)  with box rows
+// (indicator of [lo,hi]) and, for the pair, hinge rows beta*max(0, h - a'x).
+//   x-step (NV=1): P = coefP*mm*T'T + 2 D2'D2 + 2 Pcost I          (PI_ADMM_class.py:114-135)
+//   pair   (NV=2): P = blockdiag(rho*mm_v*T'T + 2 Pcost I)          (PI_ADMM_class.py:145-169)
+template <int NV>
+struct QP {
+  static constexpr int NR = (NV == 1) ? 2 : 5;
+  int H, n;
+  double q[NV];
+  double wq;              // x-step: w' with q = T'-apply(w') (PI_ADMM_class.py:114-135 gradient)
+  bool qvalid;            // q holds T'-apply(wq) (the x-step's fused pass needs only wq)
+  double D[NV];
+  double E[NR];
+  double h0;              // hinge lower bound (pair only; 0 on invalid lanes)
+  double umax, dumax;     // box / rate bounds (uniform)
+  double g1, g2;          // hinge coefficients (pair only)
+  double mm[NV];          // |M|^2 factors (ax^2 + ay^2) per vehicle
+  double coefP;           // x-step: 2 Pnorm + rho |N| ; pair: rho
+  double Pcost2;          // 2 Pcost
+  double beta, rho, sigma, alpha, tol;
+  double* K;              // LDS  n x n  scaled (P_s + sigma I + rho A_s'A_s)^-1
+  float* Kf;              // precision 1: the same matrix in fp32 (what the ADMM iteration reads)
+  bool kf32;              // ADMM reads Kf (the polish and its certificate stay fp64)
+  const double* Pinv;     // n x n unscaled P^-1 (LDS for the x-step); for the pair the HBM
+                          // table block DevArgs::tab_e: P^-1 | PGt (+4H^2) | GPG (+6H^2)
+  double* vb;             // per-wave LDS vectors (512 doubles)
+  double* XT;             // x-step: per-wave X' (H rows, stride xld) and beta (row H)
+  int xld;                // stride of XT (XLD in LDS mode, XLDG in big mode)
+  bool gmem;              // big mode: K / G / XT live in HBM (cross-lane reads need a fence)
+  double* G;              // x-step: per-wave LDS G = P^-1 - Y X (H x H, stride H), g = Y beta (row H)
+  double* fac;            // LDS factor region: L (lower), S (upper), stride fld
+  double* fdiag;          // LDS [2*64]: S_aa, 1/L_aa of the cached factor
+  int* ib;                // per-wave LDS ints: [0,64) current W ids, [64,128) cached W ids
+  int* fstate;            // LDS int: m of the cached factor (-1: none)
+  int fld;                // stride of fac
+  int mmax;               // capacity of fac (rows)
+  bool kready;            // K holds K_s^-1 for the current rho (the pair builds it lazily:
+                          // a QP that the warm-label polish certifies never needs it)
+  double* Y;              // pair: dual active-set columns P^-1 n_a (shares the K_s^-1 region)
+  int ycap;               // pair: columns Y holds
+  bool y_in_k;            // Y shares the K_s^-1 region (a GI solve invalidates K_s^-1)
+  bool scaled;            // Ruiz scaling computed (the pair computes it only when ADMM is needed)
+  bool wraw;              // the warm ADMM state holds the last certified (x, y) unscaled (zs unset):
+                          // converted to the scaled (xs, zs, ys) only when ADMM actually runs
+  const double* Kcache;   // x-step: HBM copy of K_s^-1, loaded into K only when ADMM is needed
+  mutable int csig;       // x-step: per-lane working-set signature of the cached X', G
+  int* gws;               // pair: HBM warm working set of the dual active set (GI_WS ints)
+  int tstep;              // MPC step index (warm-set bookkeeping)
+
+  __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
+  // Row s of vehicle v = s / 2: even = box (lanes < H), odd = rate (lanes < H-1), 4 = hinge
+  // (lanes 1..H-1 when the pair's geometry couples them).  Bounds are recomputed, not stored,
+  // to keep the per-lane register state of the two live QPs small.
+  __device__ __forceinline__ bool valid(int s) const {
+    const int l = lid();
+    if (hinge(s)) return l >= 1 && l < H && (g1 != 0.0 || g2 != 0.0);
+    return (s & 1) ? l < H - 1 : l < H;
+  }
+  __device__ __forceinline__ double lo(int s) const { return hinge(s) ? h0 : ((s & 1) ? -dumax : -umax); }
+  __device__ __forceinline__ double hi(int s) const { return hinge(s) ? INFINITY : ((s & 1) ? dumax : umax); }
+};
+
+template <int NV>
+__device__ constexpr int NR_HINGE() { return NV == 2 ? 4 : 0; }
+
+// Hinge rows sit at their kink at most optima (beta = 1000 makes them near-equalities);
+// like OSQP's larger rho on equality rows they get HINGE_RHO x rho (tools/qp_sim.py sweep:
+// pair-QP ADMM iterations mean 29.6 -> 20.3, max 880 -> 295).
+constexpr double HINGE_RHO = 3.0;
+template <int NV>
+__device__ __forceinline__ double rrow(const QP<NV>& P, int s) { return P.hinge(s) ? P.rho * HINGE_RHO : P.rho; }
+
+// Unscaled P x (var lanes), matrix-free: T'T via two double scans, D2'D2 via neighbours.
+template <int NV>
+__device__ __forceinline__ void P_mul(const QP<NV>& P, const double* x, double* px) {
+  const bool in = lid() < P.H;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double tx = T_apply(x[v]);
+    const double tt = Tt_apply(in ? tx : 0.0);       // T rows live on hinge lanes < H only
+    double r = P.coefP * P.mm[v] * tt + P.Pcost2 * x[v];
+    if constexpr (NV == 1) {
+      // (D2 x)_r = x_r - 2 x_{r+1} + x_{r+2}, r <= H-3 ; (D2' w)_j = w_j - 2 w_{j-1} + w_{j-2}
+      const double d2 = (lid() <= P.H - 3) ? x[v] - 2.0 * shdn(x[v], 1) + shdn(x[v], 2) : 0.0;
+      r += 2.0 * (d2 - 2.0 * shup(d2, 1) + shup(d2, 2));
+    }
+    px[v] = in ? r : 0.0;
+  }
+}
+
+// Build K_s = D P D + sigma I + rho A_s'A_s in LDS scratch m (stride ld, lane = column),
+// invert it in place and copy it to P.K (stride n).
+template <int NV>
+__device__ __forceinline__ double P_entry(const QP<NV>& P, int v, int i, int j) {
+  const double mmv = (NV == 2 && v) ? P.mm[NV - 1] : P.mm[0];
+  double e = P.coefP * mmv * TT(i, j, P.H) + (i == j ? P.Pcost2 : 0.0);
+  if constexpr (NV == 1) e += 2.0 * D2D2(i, j, P.H);
+  return e;
+}
+
+// TWO: the pair beyond H = 32 (n > 64), lane l owning columns l and l + 64 (big mode only,
+// a separate instantiation so the LDS-mode kernel carries none of it).
+template <int NV, bool TWO>
+__device__ __forceinline__ void build_K(QP<NV>& P, double* m, int ld, double* kcache = nullptr) {
+  unsigned long long t_km = STAMP_T();
+  const int l = lid();
+  const int H = P.H, n = P.n;
+  constexpr int ncol = TWO ? 2 : 1;
+  int vc[ncol], jc[ncol];
+  double Dc[ncol], gc[ncol];
+#pragma unroll
+  for (int cc = 0; cc < ncol; ++cc) {
+    const int col = l + WAVE * cc;
+    vc[cc] = (NV == 2 && col >= H) ? 1 : 0;
+    jc[cc] = col - vc[cc] * H;
+    const int src = (jc[cc] >= 0 && jc[cc] < H) ? jc[cc] : 0;
+    double Dsh[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) Dsh[v] = __shfl(P.D[v], src);
+    Dc[cc] = (NV == 2 && vc[cc] == 1) ? Dsh[NV - 1] : Dsh[0];
+    gc[cc] = (vc[cc] == 0) ? P.g1 : P.g2;
+  }
+  // hinge block of A_s'A_s: sum_{k > max(i,j)} e2_k (k-i)(k-j) = S2 - (i+j) S1 + i j S0 with
+  // suffix sums S0..S2 of e2_k k^0..2 taken at lane max(i,j)+1 (one bpermute each per row)
+  double hS0 = 0.0, hS1 = 0.0, hS2 = 0.0;
+  if constexpr (NV == 2) {
+    const double Eh2 = P.valid(NR_HINGE<NV>()) ? P.E[NR_HINGE<NV>()] * P.E[NR_HINGE<NV>()] : 0.0;
+    const double kd = (double)l;
+    hS0 = scan_incl_rev(Eh2);
+    hS1 = scan_incl_rev(Eh2 * kd);
+    hS2 = scan_incl_rev(Eh2 * kd * kd);
+  }
+  for (int r = 0; r < n; ++r) {
+    const int vr = (NV == 2 && r >= H) ? 1 : 0;
+    const int ir = r - vr * H;
+    double Dr, Ebr, Err, Errm;
+    if (NV == 2 && vr) {
+      Dr = rdl(P.D[NV - 1], ir);
+      Ebr = rdl(P.E[(2 * NV - 2) % QP<NV>::NR], ir);
+      Err = rdl(P.E[(2 * NV - 1) % QP<NV>::NR], ir);
+      Errm = (ir >= 1) ? rdl(P.E[(2 * NV - 1) % QP<NV>::NR], ir - 1) : 0.0;
+    } else {
+      Dr = rdl(P.D[0], ir);
+      Ebr = rdl(P.E[0], ir);
+      Err = rdl(P.E[1], ir);
+      Errm = (ir >= 1) ? rdl(P.E[1], ir - 1) : 0.0;
+    }
+    for (int cc = 0; cc < ncol; ++cc) {
+      const int col = l + WAVE * cc;
+      double hs = 0.0;
+      if constexpr (NV == 2) {
+        const double gr = (vr == 0) ? P.g1 : P.g2;
+        const int M = max(ir, jc[cc]) + 1;
+        const int ms = (M < H) ? M : 0;
+        const double s0 = __shfl(hS0, ms), s1 = __shfl(hS1, ms), s2 = __shfl(hS2, ms);
+        if (M < H) hs = s2 - (double)(ir + jc[cc]) * s1 + (double)ir * (double)jc[cc] * s0;
+        hs *= gr * gc[cc] * HINGE_RHO;
+      }
+      if (col < n) {
+        double ata = hs, v = 0.0;
+        if (vr == vc[cc]) {
+          v = Dr * P_entry(P, vr, ir, jc[cc]) * Dc[cc];
+          if (ir == jc[cc]) ata += Ebr * Ebr + Err * Err + Errm * Errm;
+          else if (jc[cc] == ir + 1) ata += -Err * Err;
+          else if (jc[cc] == ir - 1) ata += -Errm * Errm;
+        }
+        v += P.rho * Dr * Dc[cc] * ata + (r == col ? P.sigma : 0.0);
+        m[r * ld + col] = v;
+      }
+    }
+  }
+  wsync();
+  if (NV == 2) STAMP_ADD(ST_SZ_KMAT, t_km);
+  unsigned long long t_gj = STAMP_T();
+  if (P.gmem && m == P.K) gsync();
+  if constexpr (TWO) gj_invert2(m, n, ld, P.gmem && m == P.K);
+  else gj_invert(m, n, ld);
+  if (NV == 2) STAMP_ADD(ST_SZ_GJ, t_gj);
+  // copies: the fp64 matrix (unless built in place), its fp32 image (precision 1) and the
+  // per-scenario HBM cache (x-step); lane = column, up to two columns per lane
+  for (int col = l; col < n; col += WAVE) {
+    for (int r = 0; r < n; ++r) {
+      const double v = m[r * ld + col];
+      if (P.kf32) P.Kf[r * n + col] = (float)v;
+      else if (m != P.K) P.K[r * n + col] = v;
+      if (kcache) kcache[r * n + col] = v;
+    }
+  }
+  if (P.gmem || kcache) gsync();
+  else wsync();
+}
+template <int NV>
+__device__ __forceinline__ void A_mul(const QP<NV>& P, const double* x, double* ax) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double xn = shdn(x[v], 1);
+    ax[2 * v] = P.valid(2 * v) ? x[v] : 0.0;
+    ax[2 * v + 1] = P.valid(2 * v + 1) ? xn - x[v] : 0.0;
+  }
+  if constexpr (NV == 2) {
+    const double th = T_apply(P.g1 * x[0] + P.g2 * x[1]);
+    ax[4] = P.valid(4) ? th : 0.0;
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void At_mul(const QP<NV>& P, const double* w, double* out) {
+  const bool in = lid() < P.H;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double wr = P.valid(2 * v + 1) ? w[2 * v + 1] : 0.0;
+    const double wb = P.valid(2 * v) ? w[2 * v] : 0.0;
+    out[v] = wb - wr + shup(wr, 1);
+  }
+  if constexpr (NV == 2) {
+    const double tt = Tt_apply(P.valid(4) ? w[4] : 0.0);
+    out[0] += P.g1 * tt;
+    out[1] += P.g2 * tt;
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    if (!in) out[v] = 0.0;
+}
+
+// y = M r with M (n x n, symmetric) at row-major base (LDS or HBM), r at var lanes.
+// BD: M is block-diagonal in the NV vehicle blocks (the pair's P^-1), only those are read.
+// Loads are issued GEMV_U deep before their first use so that the pair's L2-resident
+// tables cost one latency per batch, not one per column.
+constexpr int GEMV_U = 8;
+#ifndef PIADMM_XGEMV_U
+#define PIADMM_XGEMV_U 15
+#endif
+constexpr int XGEMV_U = PIADMM_XGEMV_U;   // x-step fused pass batch, LDS mode (big mode: 8; tools/xcost.py)
+template <bool BD, int NV, typename Ptr>
+__device__ __forceinline__ void gemv_sym(const QP<NV>& P, Ptr M, const double* r, double* y) {
+  const int l = lid();
+  const int H = P.H, n = P.n;
+  if (l < H) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) P.vb[v * H + l] = r[v];
+  }
+  wsync();
+  double acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+  const int lc = (l < H) ? l : 0;
+  if constexpr (BD) {
+    for (int j0 = 0; j0 < H; j0 += GEMV_U) {
+      double mv[NV][GEMV_U], rv[NV][GEMV_U];
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u) {
+        const int j = min(j0 + u, H - 1);
+        const bool ok = j0 + u < H;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          mv[v][u] = M[(v * H + j) * n + v * H + lc];
+          rv[v][u] = ok ? P.vb[v * H + j] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] += mv[v][u] * rv[v][u];
+    }
+  } else {
+    for (int j0 = 0; j0 < n; j0 += GEMV_U) {
+      double mv[NV][GEMV_U], rv[GEMV_U];
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u) {
+        const int j = min(j0 + u, n - 1);
+        rv[u] = (j0 + u < n) ? P.vb[j] : 0.0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) mv[v][u] = M[j * n + v * H + lc];
+      }
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] += mv[v][u] * rv[u];
+    }
+  }
+  wsync();
+#pragma unroll
+  for (int v = 0; v < NV; ++v) y[v] = (l < H) ? acc[v] : 0.0;
+}
+
+// prox of phi/rho at v in scaled units for row slot s
+template <int NV>
+__device__ __forceinline__ double prox_s(const QP<NV>& P, int s, double v) {
+  const double e = P.E[s];
+  if (P.hinge(s)) {
+    const double hs = e * P.lo(s);
+    const double thr = (P.beta / e) / rrow(P, s);
+    return v >= hs ? v : (v <= hs - thr ? v + thr : hs);
+  }
+  return fmin(fmax(v, e * P.lo(s)), e * P.hi(s));
+}
+
+// label from a prox input in scaled units (ADMM state)
+template <int NV>
+__device__ __forceinline__ signed char label_scaled(const QP<NV>& P, int s, double v) {
+  const double e = P.E[s];
+  if (!P.valid(s)) return 0;
+  if (P.hinge(s)) {
+    const double hs = e * P.lo(s);
+    const double thr = (P.beta / e) / rrow(P, s);
+    return v >= hs ? HZERO : (v <= hs - thr ? HLINEAR : HKINK);
+  }
+  return v <= e * P.lo(s) ? LOWER : (v >= e * P.hi(s) ? UPPER : FREE);
+}
+
+template <int NV>
+__device__ __forceinline__ void admm_iter(const QP<NV>& P, double* xs, double* zs, double* ys) {
+  constexpr int NR = QP<NV>::NR;
+  double w[NR], t[NV], rhs[NV], xt[NV], xu[NV], a[NR];
+#pragma unroll
+  for (int s = 0; s < NR; ++s) w[s] = P.valid(s) ? P.E[s] * (rrow(P, s) * zs[s] - ys[s]) : 0.0;
+  At_mul(P, w, t);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) rhs[v] = P.sigma * xs[v] - P.D[v] * P.q[v] + P.D[v] * t[v];
+  if (P.kf32) gemv_sym<false>(P, P.Kf, rhs, xt);     // fp32 storage, fp64 accumulation
+  else gemv_sym<false>(P, P.K, rhs, xt);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xu[v] = P.D[v] * xt[v];
+  A_mul(P, xu, a);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xs[v] = P.alpha * xt[v] + (1.0 - P.alpha) * xs[v];
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (!P.valid(s)) {
+      zs[s] = ys[s] = 0.0;
+      continue;
+    }
+    const double rs = rrow(P, s);
+    const double zr = P.alpha * (P.E[s] * a[s]) + (1.0 - P.alpha) * zs[s];
+    const double vin = zr + ys[s] / rs;
+    const double zn = prox_s(P, s, vin);
+    ys[s] += rs * (zr - zn);
+    zs[s] = zn;
+  }
+}
+
+// ---- Schur-complement entry a' P^-1 b for rows given by ids (slot*H + lane).
+// A box/rate row is c0 e_{i0} + c1 e_{i1} (c1 = 0 for a box row); hinge rows use PGt/GPG.
+struct RowT {
+  int i0, i1, hk;
+  double c0, c1;
+};
+template <int NV>
+__device__ __forceinline__ RowT row_terms(const QP<NV>& P, int id) {
+  const int s = id / P.H, k = id - s * P.H;
+  RowT r;
+  if (NV == 2 && s == 4) {
+    r.hk = k;
+    r.i0 = r.i1 = 0;
+    r.c0 = r.c1 = 0.0;
+    return r;
+  }
+  const int base = (s >> 1) * P.H + k;
+  r.hk = -1;
+  if ((s & 1) == 0) {
+    r.i0 = base; r.c0 = 1.0; r.i1 = base; r.c1 = 0.0;
+  } else {
+    r.i0 = base + 1; r.c0 = 1.0; r.i1 = base; r.c1 = -1.0;
+  }
+  return r;
+}
+
+// hinge coefficient of variable i (vehicle 1: g1, vehicle 2: g2); PGt/GPG hold unscaled tables
+template <int NV>
+__device__ __forceinline__ double gvar(const QP<NV>& P, int i) { return i < P.H ? P.g1 : P.g2; }
+
+// Gather form: an entry of S = A_W P^-1 A_W' is sum_t c[t] P.Pinv[o[t]] over at most four
+// terms (the pair's PGt / GPG follow P^-1 in the same per-edge block at +4H^2 / +6H^2),
+// so a batch of entries issues all its loads before the first use.
+struct Gather4 {
+  int o[4];
+  double c[4];
+};
+template <int NV>
+__device__ __forceinline__ Gather4 s_gather(const QP<NV>& P, int ia, int ibd) {
+  const RowT a = row_terms(P, ia), b = row_terms(P, ibd);
+  const int n = P.n, HH = P.H * P.H;
+  Gather4 g;
+  if (a.hk < 0 && b.hk < 0) {
+    g.o[0] = a.i0 * n + b.i0; g.c[0] = a.c0 * b.c0;
+    g.o[1] = a.i0 * n + b.i1; g.c[1] = a.c0 * b.c1;
+    g.o[2] = a.i1 * n + b.i0; g.c[2] = a.c1 * b.c0;
+    g.o[3] = a.i1 * n + b.i1; g.c[3] = a.c1 * b.c1;
+    return g;
+  }
+  g.o[2] = g.o[3] = 0;
+  g.c[2] = g.c[3] = 0.0;
+  if (a.hk < 0 || b.hk < 0) {
+    const RowT& bx = (a.hk < 0) ? a : b;
+    const int hk = (a.hk < 0) ? b.hk : a.hk;
+    const int base = 4 * HH + hk * n;
+    g.o[0] = base + bx.i0; g.c[0] = bx.c0 * gvar(P, bx.i0);
+    g.o[1] = base + bx.i1; g.c[1] = bx.c1 * gvar(P, bx.i1);
+    return g;
+  }
+  const int base = 6 * HH + a.hk * P.H + b.hk;
+  g.o[0] = base; g.c[0] = P.g1 * P.g1;
+  g.o[1] = base + HH; g.c[1] = P.g2 * P.g2;
+  return g;
+}
+
+// Solve L L' x = b (lane a holds b_a, a < m).  L lower in fac (stride ld), linv = 1/L_aa.
+__device__ __forceinline__ double chol_solve(const double* L, int ld, double linv, double b, int m) {
+  const int l = lid();
+  for (int k = 0; k < m; ++k) {       // forward, column-oriented
+    const double Llk = (l > k && l < m) ? L[l * ld + k] : 0.0;
+    const double zk = rdl(b * linv, k);
+    if (l == k) b = zk;
+    b -= Llk * zk;
+  }
+  for (int k = m - 1; k >= 0; --k) {  // backward with L'
+    const double Lkl = (l < k) ? L[k * ld + l] : 0.0;
+    const double xk = rdl(b * linv, k);
+    if (l == k) b = xk;
+    b -= Lkl * xk;
+  }
+  return (l < m) ? b : 0.0;
+}
+
+// Left-looking Cholesky of S + delta I.  S is stored in the upper triangle of fac
+// (row a, columns b >= a) with its diagonal in sdiag (lane a); L goes to the strict
+// lower triangle and the diagonal.  A row whose pivot collapses below DEP_TOL * S_kk is
+// linearly dependent on the earlier working-set rows (degenerate vertices of the box/rate
+// polytope, e.g. u_k = -umax, u_{k+3} = +umax and the three rates between them at +dumax):
+// it is dropped (zero column of L, linv = 0, so its multiplier solves to 0), as the
+// oracle's active-set solver does.  Returns false only on a non-finite pivot.
+constexpr double DEP_TOL = 1e-10;
+__device__ __forceinline__ bool chol_factor(double* fac, int ld, double sdiag, double delta, int m, double& linv) {
+  const int l = lid();
+  for (int k = 0; k < m; ++k) {
+    double acc = 0.0;
+    if (l >= k && l < m) {
+      const double* ri = fac + l * ld;
+      const double* rk = fac + k * ld;
+      int j = 0;
+      for (; j + 4 <= k; j += 4)
+        acc += ri[j] * rk[j] + ri[j + 1] * rk[j + 1] + ri[j + 2] * rk[j + 2] + ri[j + 3] * rk[j + 3];
+      for (; j < k; ++j) acc += ri[j] * rk[j];
+    }
+    const double sik = (l == k) ? sdiag + delta : ((l > k && l < m) ? fac[k * ld + l] : 0.0);
+    const double d = sik - acc;
+    const double piv = rdl(d, k);
+    if (!isfinite(piv)) return false;
+    const bool dep = !(piv > DEP_TOL * rdl(sdiag, k));
+    const double lkk = dep ? 1.0 : sqrt(piv);
+    const double inv = dep ? 0.0 : 1.0 / lkk;
+    wsync();
+    if (l == k) {
+      fac[k * ld + k] = lkk;
+      linv = inv;
+    }
+    if (l > k && l < m) fac[l * ld + k] = d * inv;
+    wsync();
+  }
+  return true;
+}
+
+// One PDAS reduced solve for labels lab; returns false on numerical failure.
+// The Cholesky factor of S = A_W P^-1 A_W' is cached per wave and reused when the
+// working set W is unchanged (P is fixed for the whole MPC step).
+template <int NV>
+__device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char* lab, double* x, double* y) {
+  constexpr int NR = QP<NV>::NR;
+  const int l = lid();
+  const int H = P.H;
+  const int ld = P.fld;
+  double* vb_b = P.vb + 64;        // [64,128) rhs b of W rows
+  double* vb_lam = P.vb + 128;     // [128,192)
+  double* vb_ax = P.vb + 192;      // [192,512) A x0 by row id (<= 5*32 = 160)
+  int* ids = P.ib;                 // current W
+  int* cids = P.ib + 64;           // W of the cached factor
+  // q~ = q - beta G'(1_linear)
+  double qt[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) qt[v] = P.q[v];
+  if constexpr (NV == 2) {
+    const double lin = (P.valid(4) && lab[4] == HLINEAR) ? 1.0 : 0.0;
+    const double tt = Tt_apply(lin);
+    if (l < H) {
+      qt[0] -= P.beta * P.g1 * tt;
+      qt[1] -= P.beta * P.g2 * tt;
+    }
+  }
+  double x0[NV];
+  unsigned long long t_rs = STAMP_T();
+  gemv_sym<true>(P, P.Pinv, qt, x0);
+  STAMP_ADD(NV == 1 ? ST_RED_GEMV : ST_ZR_GEMV, t_rs);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) x0[v] = -x0[v];
+  // working set, compacted in slot-major order
+  bool inW[NR];
+  int pos[NR];
+  int m = 0;
+  const unsigned long long ltmask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    inW[s] = P.valid(s) && (P.hinge(s) ? (lab[s] == HKINK) : (lab[s] != FREE));
+    const unsigned long long bm = __ballot(inW[s]);
+    pos[s] = m + __popcll(bm & ltmask);
+    m += __popcll(bm);
+  }
+  double ax0[NR];
+  A_mul(P, x0, ax0);
+  if (__builtin_expect(m > P.mmax, 0)) return false;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (l < H) vb_ax[s * H + l] = ax0[s];
+    if (inW[s]) {
+      ids[pos[s]] = s * H + l;
+      vb_b[pos[s]] = P.hinge(s) ? P.lo(s) : (lab[s] == LOWER ? P.lo(s) : P.hi(s));
+    }
+  }
+  wsync();
+  if (m == 0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = x0[v];
+#pragma unroll
+    for (int s = 0; s < NR; ++s) y[s] = (P.hinge(s) && P.valid(s) && lab[s] == HLINEAR) ? -P.beta : 0.0;
+    return true;
+  }
+  const int myid = (l < m) ? ids[l] : 0;
+  const double rhs = (l < m) ? (vb_ax[myid] - vb_b[l]) : 0.0;
+  const bool cached = (P.fstate[0] == m) && wall(l >= m || cids[l] == myid);
+  double sdiag, linv;
+  if (cached) {
+    sdiag = (l < m) ? P.fdiag[l] : 0.0;
+    linv = (l < m) ? P.fdiag[64 + l] : 0.0;
+  } else {
+    // S (upper triangle) into fac: lane a = row a, columns b >= a
+    unsigned long long t_s = STAMP_T();
+    sdiag = 0.0;
+    constexpr int SB = 4;
+    for (int b0 = 0; b0 < m; b0 += SB) {
+      Gather4 gg[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) gg[u] = s_gather(P, myid, rdli(myid, min(b0 + u, m - 1)));
+      double tv[SB][4];
+#pragma unroll
+      for (int u = 0; u < SB; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tv[u][k] = P.Pinv[gg[u].o[k]];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int b = b0 + u;
+        const double sv = gg[u].c[0] * tv[u][0] + gg[u].c[1] * tv[u][1] + gg[u].c[2] * tv[u][2] + gg[u].c[3] * tv[u][3];
+        if (b < m && l <= b && l < m) {
+          if (b == l) sdiag = sv;
+          else P.fac[l * ld + b] = sv;
+        }
+      }
+    }
+    STAMP_ADD(NV == 1 ? ST_RED_S : ST_ZR_S, t_s);
+    unsigned long long t_c = STAMP_T();
+    // no diagonal shift: a dependent working-set row is dropped by its collapsed pivot
+    // (chol_factor); a shift would hide the collapse of rows with a small S_kk
+    const double delta = 0.0;
+    wsync();
+    linv = 0.0;
+    const bool fok = chol_factor(P.fac, ld, sdiag, delta, m, linv);
+    STAMP_ADD(NV == 1 ? ST_RED_CHOL : ST_ZR_CHOL, t_c);
+    if (!fok) {
+      if (l == 0) P.fstate[0] = -1;
+      wsync();
+      return false;
+    }
+    if (l < m) {
+      P.fdiag[l] = sdiag;
+      P.fdiag[64 + l] = linv;
+      cids[l] = myid;
+    }
+    if (l == 0) P.fstate[0] = m;
+    wsync();
+  }
+  unsigned long long t_sv = STAMP_T();
+  double lamv = chol_solve(P.fac, ld, linv, rhs, m);
+  // one step of iterative refinement against the unregularised S
+  {
+    double sl = 0.0;
+    for (int b = 0; b < m; ++b) {
+      const double lb = rdl(lamv, b);
+      if (l < m) {
+        const double sab = (b == l) ? sdiag : (b > l ? P.fac[l * ld + b] : P.fac[b * ld + l]);
+        sl += sab * lb;
+      }
+    }
+    const double r = (l < m) ? rhs - sl : 0.0;
+    lamv += chol_solve(P.fac, ld, linv, r, m);
+  }
+  STAMP_ADD(NV == 1 ? ST_XR_SOLVE : ST_ZR_SOLVE, t_sv);
+  if (!isfinite(lamv)) return false;
+  unsigned long long t_x = STAMP_T();
+  // x = x0 - sum_a (P^-1 a_a) lam_a
+  double xv[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xv[v] = x0[v];
+  {
+    constexpr int XB = 4;
+    const int lc = (l < H) ? l : 0;
+    for (int a0 = 0; a0 < m; a0 += XB) {
+      int o[XB][NV][2];
+      double cf[XB][NV][2], la[XB];
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        const int a = min(a0 + u, m - 1);
+        const RowT r = row_terms(P, rdli(myid, a));
+        la[u] = (a0 + u < m) ? rdl(lamv, a) : 0.0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int i = v * H + lc;
+          if (NV == 2 && r.hk >= 0) {        // (P^-1 G_k')_i, unscaled table times g_v
+            o[u][v][0] = o[u][v][1] = 4 * H * H + r.hk * P.n + i;
+            cf[u][v][0] = v ? P.g2 : P.g1;
+            cf[u][v][1] = 0.0;
+          } else {
+            o[u][v][0] = r.i0 * P.n + i; cf[u][v][0] = r.c0;
+            o[u][v][1] = r.i1 * P.n + i; cf[u][v][1] = r.c1;
+          }
+        }
+      }
+      double tv[XB][NV][2];
+#pragma unroll
+      for (int u = 0; u < XB; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+          for (int k = 0; k < 2; ++k) tv[u][v][k] = P.Pinv[o[u][v][k]];
+#pragma unroll
+      for (int u = 0; u < XB; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xv[v] -= (cf[u][v][0] * tv[u][v][0] + cf[u][v][1] * tv[u][v][1]) * la[u];
+    }
+  }
+  STAMP_ADD(NV == 1 ? ST_RED_X : ST_ZR_X, t_x);
+  if (l < m) vb_lam[l] = lamv;
+  wsync();
+#pragma unroll
+  for (int v = 0; v < NV; ++v) x[v] = (l < H) ? xv[v] : 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (inW[s]) y[s] = vb_lam[pos[s]];
+    else if (P.hinge(s) && P.valid(s) && lab[s] == HLINEAR) y[s] = -P.beta;
+    else y[s] = 0.0;
+  }
+  wsync();
+  return true;
+}
+
+// x-step (NV = 1) polish in parametric form.  P and A are fixed for the whole MPC step and
+// only q changes between outer iterations, so for a working set W with bounds b
+//   lam = S^-1 (A_W x0 - b) = -X q - beta,   x = x0 - Y lam,   x0 = -P^-1 q,
+// with Y = P^-1 A_W', S = A_W Y, X = S^-1 Y', beta = S^-1 b.  X' (rows = variables) and
+// beta (row H) are rebuilt in LDS only when W or the bound side of one of its rows changes;
+// a hit costs one fused pass over P^-1 and X' plus the x recovery.
+__device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, const int* ids, const double* vb_b) {
+  const int l = lid(), H = P.H, ld = P.fld;
+  double* fac = P.fac;
+  double* XT = P.XT;
+  // S (upper triangle, lane a = row a) from the LDS P^-1
+  unsigned long long t_s = STAMP_T();
+  double sdiag = 0.0;
+  constexpr int SB = 4;
+  for (int b0 = 0; b0 < m; b0 += SB) {
+    Gather4 gg[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) gg[u] = s_gather(P, myid, ids[min(b0 + u, m - 1)]);
+    double tv[SB][4];
+#pragma unroll
+    for (int u = 0; u < SB; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tv[u][k] = P.Pinv[gg[u].o[k]];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) {
+      const int b = b0 + u;
+      const double sv = gg[u].c[0] * tv[u][0] + gg[u].c[1] * tv[u][1] + gg[u].c[2] * tv[u][2] + gg[u].c[3] * tv[u][3];
+      if (b < m && l <= b && l < m) {
+        if (b == l) sdiag = sv;
+        else fac[l * ld + b] = sv;
+      }
+    }
+  }
+  STAMP_ADD(ST_RED_S, t_s);
+  unsigned long long t_c = STAMP_T();
+  wsync();
+  double linv = 0.0;
+  // unshifted: a dependent working-set row (degenerate vertex) is dropped by chol_factor
+  if (!chol_factor(fac, ld, sdiag, 0.0, m, linv)) return false;
+  if (l < m) P.fdiag[64 + l] = linv;
+  STAMP_ADD(ST_RED_CHOL, t_c);
+  unsigned long long t_x = STAMP_T();
+  // right-hand sides, one per lane: lane i < H -> row i of Y = P^-1 A_W', lane H -> b
+  const int li = (l <= H) ? l : H;
+  const bool own = l <= H;
+  double* xr = XT + li * P.xld;
+  constexpr int XB = 4;
+  for (int a0 = 0; a0 < m; a0 += XB) {
+    int o[XB][2];
+    double cf[XB][2];
+#pragma unroll
+    for (int u = 0; u < XB; ++u) {
+      const RowT r = row_terms(P, ids[min(a0 + u, m - 1)]);
+      const int i = (l < H) ? l : 0;
+      o[u][0] = r.i0 * H + i; cf[u][0] = r.c0;
+      o[u][1] = r.i1 * H + i; cf[u][1] = r.c1;
+    }
+    double tv[XB][2];
+#pragma unroll
+    for (int u = 0; u < XB; ++u) {
+      tv[u][0] = P.Pinv[o[u][0]];
+      tv[u][1] = P.Pinv[o[u][1]];
+    }
+#pragma unroll
+    for (int u = 0; u < XB; ++u) {
+      const int a = a0 + u;
+      if (a < m) {
+        const double v = (l < H) ? cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1] : vb_b[a];
+        if (own) xr[a] = v;
+      }
+    }
+  }
+  wsync();
+  // L L' sol = rhs for every lane's right-hand side (L broadcast from fac, lane-own sol)
+  constexpr int TB = 8;
+  for (int a = 0; a < m; ++a) {
+    double acc = xr[a];
+    for (int b0 = 0; b0 < a; b0 += TB) {
+      double Lv[TB], sv[TB];
+#pragma unroll
+      for (int u = 0; u < TB; ++u) {
+        const int b = min(b0 + u, a - 1);
+        Lv[u] = (b0 + u < a) ? fac[a * ld + b] : 0.0;
+        sv[u] = xr[b];
+      }
+#pragma unroll
+      for (int u = 0; u < TB; ++u) acc -= Lv[u] * sv[u];
+    }
+    acc *= P.fdiag[64 + a];
+    if (own) xr[a] = acc;
+  }
+  for (int a = m - 1; a >= 0; --a) {
+    double acc = xr[a];
+    for (int b0 = a + 1; b0 < m; b0 += TB) {
+      double Lv[TB], sv[TB];
+#pragma unroll
+      for (int u = 0; u < TB; ++u) {
+        const int b = min(b0 + u, m - 1);
+        Lv[u] = (b0 + u < m) ? fac[b * ld + a] : 0.0;
+        sv[u] = xr[b];
+      }
+#pragma unroll
+      for (int u = 0; u < TB; ++u) acc -= Lv[u] * sv[u];
+    }
+    acc *= P.fdiag[64 + a];
+    if (own) xr[a] = acc;
+  }
+  if (P.gmem) gsync();
+  else wsync();
+  STAMP_ADD(ST_XR_SOLVE, t_x);
+  // G = P^-1 - Y X and g = Y beta (lane j = column j): Y is re-gathered column by column
+  // into the factor scratch (the factor is not needed once X' is known), then every lane
+  // accumulates its column of Y X from LDS broadcasts of Y and its own row of X'.
+  {
+    const int lc = (l < H) ? l : 0;
+    for (int a0 = 0; a0 < m; a0 += XB) {
+      double tv[XB][2], cf[XB][2];
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        const RowT r = row_terms(P, ids[min(a0 + u, m - 1)]);
+        cf[u][0] = r.c0;
+        cf[u][1] = r.c1;
+        tv[u][0] = P.Pinv[r.i0 * H + lc];
+        tv[u][1] = P.Pinv[r.i1 * H + lc];
+      }
+#pragma unroll
+      for (int u = 0; u < XB; ++u)
+        if (a0 + u < m && l < H) fac[(a0 + u) * ld + l] = cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1];
+    }
+    wsync();
+    const double* xj = XT + lc * P.xld;
+    constexpr int GB = 8;
+    for (int i0 = 0; i0 < H; i0 += GB) {
+      double acc[GB], pv[GB];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        acc[u] = 0.0;
+        pv[u] = P.Pinv[min(i0 + u, H - 1) * H + lc];
+      }
+      for (int a = 0; a < m; ++a) {
+        const double xja = xj[a];
+        const double* ya = fac + a * ld + i0;
+#pragma unroll
+        for (int u = 0; u < GB; ++u) acc[u] += ya[u] * xja;     // rows past H are never stored
+      }
+#pragma unroll
+      for (int u = 0; u < GB; ++u)
+        if (l < H && i0 + u < H) P.G[(i0 + u) * H + l] = pv[u] - acc[u];
+    }
+    double gacc = 0.0;
+    for (int a = 0; a < m; ++a) gacc += fac[a * ld + lc] * XT[H * P.xld + a];
+    if (l < H) P.G[H * H + l] = gacc;
+    if (P.gmem) gsync();
+    else wsync();
+  }
+  // fold q = T'-apply(w') into the tables: row k of G T' (and X T') is
+  // sum_{j<k} (k - j) row j -- two running sums per lane, in place (read before write)
+  {
+    double s1 = 0.0, s2 = 0.0, t1 = 0.0, t2 = 0.0;
+    const int la = (l < m) ? l : 0;
+    for (int k = 0; k < H; ++k) {
+      const double gk = P.G[k * H + (l < H ? l : 0)];
+      const double xk = XT[k * P.xld + la];
+      if (l < H) P.G[k * H + l] = s2;
+      if (l < m) XT[k * P.xld + l] = t2;
+      s1 += gk;
+      s2 += s1;
+      t1 += xk;
+      t2 += t1;
+    }
+    if (P.gmem) gsync();
+    else wsync();
+  }
+  return true;
+}
+
+template <int XU>
+__device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed char* lab, double* x, double* y) {
+  const int l = lid(), H = P.H;
+  unsigned long long t_pre = STAMP_T();
+  double* vb_q = P.vb;             // [0,64) q
+  double* vb_b = P.vb + 64;        // [64,128) rhs b of W rows
+  double* vb_lam = P.vb + 128;     // [128,192)
+  int* ids = P.ib;                 // current W
+  int* cids = P.ib + 64;           // W (with bound sides) of the cached X', beta
+  const double* XT = P.XT;
+  bool inW[2];
+  int pos[2];
+  int m = 0;
+  const unsigned long long ltmask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    inW[s] = P.valid(s) && lab[s] != FREE;
+    const unsigned long long bm = __ballot(inW[s]);
+    pos[s] = m + __popcll(bm & ltmask);
+    m += __popcll(bm);
+  }
+  if (__builtin_expect(m > P.mmax, 0)) return false;
+  // w' (q = T'-apply(w'), folded into the tables: G T', X T'), zero-padded to 64 so that the
+  // fused pass loads it unconditionally
+  vb_q[l] = (l < H) ? P.wq : 0.0;
+  // the working set with its bound sides as a per-lane signature (this lane's box and rate
+  // rows) in a register: a hit on the cached X', G is one ballot, no LDS round trip
+  const int sig = (inW[0] ? (int)lab[0] : 0) | ((inW[1] ? (int)lab[1] : 0) << 2);
+  if (__builtin_expect(!wall(sig == P.csig), 0)) {   // csig = -1 whenever the tables are not valid
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (inW[s]) {
+        ids[pos[s]] = s * H + l;
+        vb_b[pos[s]] = (lab[s] == LOWER) ? P.lo(s) : P.hi(s);
+      }
+    }
+    wsync();
+    const int myid = (l < m) ? ids[l] : 0;
+    if (!param_build_x(P, m, myid, ids, vb_b)) {
+      if (l == 0) P.fstate[0] = -1;
+      P.csig = -1;
+      wsync();
+      return false;
+    }
+    P.csig = sig;
+    if (l == 0) P.fstate[0] = m;
+  }
+  (void)cids;
+  wsync();
+  STAMP_ADD(ST_RSX_PRE, t_pre);
+  unsigned long long t_rs = STAMP_T();
+  // one fused pass: x = -G q + g (lane = variable), lam = -X q - beta (lane = W row)
+  double ag = 0.0, ax = 0.0;
+  {
+    const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
+    const double* G = P.G;
+    // full batches: row pointers advance by a stride, no clamp
+    const int Hf = H - H % XU;
+    const double* gp = G + lc;
+    const double* xp = XT + la;
+    const int xs = P.xld;
+    for (int j0 = 0; j0 < Hf; j0 += XU) {
+      double qv[XU], gv[XU], xv[XU];
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        qv[u] = vb_q[j0 + u];
+        gv[u] = gp[u * H];
+        xv[u] = xp[u * xs];
+      }
+      gp += XU * H;
+      xp += XU * xs;
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        ag += gv[u] * qv[u];
+        ax += xv[u] * qv[u];
+      }
+    }
+    if (Hf < H) {                       // tail: rows clamped to H - 1, q is 0 beyond H
+      double qv[XU], gv[XU], xv[XU];
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        const int j = min(Hf + u, H - 1);
+        qv[u] = vb_q[Hf + u];
+        gv[u] = G[j * H + lc];
+        xv[u] = XT[j * xs + la];
+      }
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        ag += gv[u] * qv[u];
+        ax += xv[u] * qv[u];
+      }
+    }
+    if (l < m) vb_lam[l] = -ax - XT[H * P.xld + l];
+    ag = G[H * H + lc] - ag;
+  }
+  wsync();
+  STAMP_ADD(ST_RED_GEMV, t_rs);
+  x[0] = (l < H) ? ag : 0.0;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) y[s] = inW[s] ? vb_lam[pos[s]] : 0.0;
+  wsync();
+  return true;
+}
+
+// KKT test of (x, y) for labels lab; on failure fills new labels (PDAS update).
+template <int NV>
+__device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* lab, const double* x, const double* y,
+                          signed char* nlab) {
+  constexpr int NR = QP<NV>::NR;
+  double ax[NR];
+  A_mul(P, x, ax);
+  double ym = 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) ym = fmax(ym, fabs(y[s]));
+  ym = wmax(ym);
+  const double ty = P.tol * (1.0 + ym);
+  bool ok = true;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (!P.valid(s)) {
+      nlab[s] = 0;
+      continue;
+    }
+    const double tp = P.tol * (1.0 + fabs(P.lo(s)));
+    // Label update: a violated row changes state by one step only -- an active row whose
+    // multiplier has the wrong sign is released (never flipped to the opposite bound), a
+    // free row becomes active only when its bound is violated beyond the tolerance.  At a
+    // degenerate vertex (dependent rows, zero multipliers) this releases the row that
+    // received the wrong-signed multiplier instead of cycling between the two bounds.
+    if (P.hinge(s)) {
+      const double h = P.lo(s);
+      if (lab[s] == HZERO) {
+        const bool v = ax[s] < h - tp;
+        ok &= !v;
+        nlab[s] = v ? HKINK : HZERO;
+      } else if (lab[s] == HLINEAR) {
+        const bool v = ax[s] > h + tp;
+        ok &= !v;
+        nlab[s] = v ? HKINK : HLINEAR;
+      } else {
+        // a kink row must sit at h: the reduced solve drops a dependent row, which is only
+        // right when the dropped equation is implied by the others (consistent labels)
+        ok &= (y[s] <= ty) && (y[s] >= -P.beta - ty) && fabs(ax[s] - h) <= tp;
+        nlab[s] = (y[s] > ty) ? HZERO : ((y[s] < -P.beta - ty) ? HLINEAR : HKINK);
+      }
+    } else {
+      if (lab[s] == FREE) {
+        const bool vl = ax[s] < P.lo(s) - tp, vu = ax[s] > P.hi(s) + tp;
+        ok &= !vl && !vu;
+        nlab[s] = vl ? LOWER : (vu ? UPPER : FREE);
+      } else if (lab[s] == LOWER) {
+        ok &= (y[s] <= ty) && fabs(ax[s] - P.lo(s)) <= tp;   // equality too (dropped rows)
+        nlab[s] = (y[s] > ty) ? FREE : LOWER;
+      } else {
+        ok &= (y[s] >= -ty) && fabs(ax[s] - P.hi(s)) <= tp;
+        nlab[s] = (y[s] < -ty) ? FREE : UPPER;
+      }
+    }
+    ok &= isfinite(x[0]) && isfinite(y[s]);
+  }
+  return wall(ok);
+}
+
+template <int NV, int XU = XGEMV_U>
+__device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y, int& nsolve,
+                                     int steps = PDAS_STEPS) {
+  constexpr int NR = QP<NV>::NR;
+  signed char nl[NR];
+  for (int it = 0; it < steps; ++it) {
+    ++nsolve;
+    unsigned long long t_r = STAMP_T();
+    bool rs_ok;
+    if constexpr (NV == 1) rs_ok = reduced_solve_x<XU>(P, lab, x, y);
+    else rs_ok = reduced_solve(P, lab, x, y);
+    STAMP_ADD(NV == 1 ? ST_XRED : ST_ZRED, t_r);
+    if (__builtin_expect(!rs_ok, 0)) return false;
+    unsigned long long t_k = STAMP_T();
+    const bool kok = kkt_check(P, lab, x, y, nl);
+    STAMP_ADD(NV == 1 ? ST_XKKT : ST_ZKKT, t_k);
+    if (__builtin_expect(kok, 1)) return true;
+    bool same = true;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) same &= (nl[s] == lab[s]);
+    if (wall(same)) return false;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) lab[s] = nl[s];
+  }
+  return false;
+}
+
+
+// ============================================================ dual active set (pair QP)
+// Goldfarb-Idnani dual active-set method on the pair QP in hinge form, in Schur-complement
+// form.  From the unconstrained minimiser x0 = -P^-1 q it adds the most violated one-sided
+// constraint n_p'x >= b_p at a time (box/rate row r: side 0 = a_r'x >= lo, side 1 =
+// -a_r'x >= -hi; hinge row: a_r'x >= h with multiplier cap beta), taking partial (dual)
+// steps that drop a constraint whose multiplier reaches 0.  The active set's Schur
+// complement S = N P^-1 N' is kept as a Cholesky factor L (LDS, insertion order): an add
+// appends one row (its forward-solve vector w and sqrt(S_pp - w'w)), a drop deletes row k and
+// restores the trailing block by a rank-one update.  Y holds the columns P^-1 n_a.  Each step
+// costs two m-step triangular solves, one m-column pass over Y and a few wave reductions --
+// no K_s^-1 and no ADMM.  On the recorded bench pair QPs (tools/gi_sim.py) it certifies every
+// one in 28 steps on average (max 51) where ADMM + PDAS took ~45 ADMM iterations and ~6
+// full reduced solves.  A hinge multiplier reaching the cap, a full factor or the step limit
+// return false and the caller falls back to ADMM + PDAS; the result is certified by the same
+// KKT test either way.
+// Triangular solves with lane = row, the factor's column (fwd) / row (bwd) entries of a batch
+// of TRI_U steps loaded before the batch's dependent chain: one LDS latency per batch
+// instead of one per step.
+constexpr int TRI_U = 8;
+__device__ __forceinline__ double tri_fwd(const double* L, int ld, double linv, double b, int m) {
+  const int l = lid();
+  const int lr = (l < m) ? l : 0;
+  for (int k0 = 0; k0 < m; k0 += TRI_U) {
+    double Lv[TRI_U];
+#pragma unroll
+    for (int u = 0; u < TRI_U; ++u) Lv[u] = L[lr * ld + min(k0 + u, 63)];
+#pragma unroll
+    for (int u = 0; u < TRI_U; ++u) {
+      const int k = k0 + u;
+      if (k < m) {
+        const double zk = rdl(b * linv, k);
+        if (l == k) b = zk;
+        if (l > k && l < m) b -= Lv[u] * zk;
+      }
+    }
+  }
+  return (l < m) ? b : 0.0;
+}
+__device__ __forceinline__ double tri_bwd(const double* L, int ld, double linv, double b, int m) {
+  const int l = lid();
+  const int lc = (l < m) ? l : 0;
+  for (int k0 = m - 1; k0 >= 0; k0 -= TRI_U) {
+    double Lv[TRI_U];
+#pragma unroll
+    for (int u = 0; u < TRI_U; ++u) Lv[u] = L[max(k0 - u, 0) * ld + lc];
+#pragma unroll
+    for (int u = 0; u < TRI_U; ++u) {
+      const int k = k0 - u;
+      if (k >= 0) {
+        const double xk = rdl(b * linv, k);
+        if (l == k) b = xk;
+        if (l < k) b -= Lv[u] * xk;
+      }
+    }
+  }
+  return (l < m) ? b : 0.0;
+}
+
+// P^-1 n for the one-sided constraint (row id, sign sg): lane = variable (one value per vehicle)
+template <int NV>
+__device__ __forceinline__ void pinv_row(const QP<NV>& P, int row, double sg, double* out) {
+  const int l = lid(), H = P.H;
+  const int lc = (l < H) ? l : 0;
+  const RowT r = row_terms(P, row);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int i = v * H + lc;
+    double val;
+    if (NV == 2 && r.hk >= 0) {
+      val = (v ? P.g2 : P.g1) * P.Pinv[4 * H * H + r.hk * P.n + i];
+    } else {
+      val = r.c0 * P.Pinv[r.i0 * P.n + i] + r.c1 * P.Pinv[r.i1 * P.n + i];
+    }
+    out[v] = (l < H) ? sg * val : 0.0;
+  }
+}
+
+constexpr int GI_MAX_STEPS = 256;
+constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t, codes
+// Warm start (receding horizon): the previous MPC step's final active set, shifted one time
+// slot (tools/gi_sim.py + the warm-start prototype: 28 -> 3.6 GI steps per bench pair QP),
+// is appended row by row (dependent rows skipped), its equality-constrained minimiser formed
+// and constraints with negative (or beyond-cap) multipliers dropped until the start is dual
+// feasible -- the state GI requires -- before the usual adds.  Any starting set is only a
+// guess: the minimiser and its certificate do not depend on it.
+template <int NV>
+__device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, signed char* lab, double* x, double* y,
+                                         int& nsteps) {
+  constexpr int NR = QP<NV>::NR;
+  const int l = lid(), H = P.H, ld = P.fld, H2 = NV * H;
+  double* vb_ax = P.vb + 192;      // [192, 192 + NR*H): (A v) by row id
+  int* wc = P.ib;                  // active constraint codes 2*row + side, insertion order
+  double* L = P.fac;
+  double* Y = P.Y;
+  const int cap = min(P.mmax - 1, P.ycap);
+  if (P.y_in_k) P.kready = false;  // Y overwrites the K_s^-1 region
+  if (l == 0) P.fstate[0] = -1;    // and L the cached PDAS factor
+  P.csig = -1;                     // (x-step: the factor scratch the parametric tables were built in)
+  double x0[NV], xc[NV];
+  gemv_sym<true>(P, P.Pinv, P.q, x0);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xc[v] = x0[v] = -x0[v];
+  int m = 0, wbits = 0;
+  double ua = 0.0, linv = 0.0;     // lane a < m: multiplier and 1/L_aa of active constraint a
+
+  // y_p = P^-1 n_p (lane = variable), A y_p to vb_ax; returns n_p' P^-1 n_p
+  auto prep = [&](int pc, double* yp) -> double {
+    const int prow = pc >> 1;
+    const double sgp = (pc & 1) ? -1.0 : 1.0;
+    pinv_row(P, prow, sgp, yp);
+    double ay[NR];
+    A_mul(P, yp, ay);
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ay[s];
+    }
+    wsync();
+    return sgp * vb_ax[prow];
+  };
+  // w = L^-1 (N y_p) for the current active set (lane a < m)
+  auto fwd = [&]() -> double {
+    const int myc = (l < m) ? wc[l] : 0;
+    const double va = (l < m) ? ((myc & 1) ? -1.0 : 1.0) * vb_ax[myc >> 1] : 0.0;   // n_a' y_p
+    return tri_fwd(L, ld, linv, va, m);
+  };
+  // append constraint pc: L row m = (w', sqrt(lpp2)), Y column m = y_p
+  auto append = [&](int pc, const double* yp, double w, double lpp2, double u0) {
+    const int prow = pc >> 1, ps = prow / H, pk = prow - ps * H;
+    const double lmm = sqrt(lpp2);
+    if (l < m) L[m * ld + l] = w;
+    if (l == m) {
+      L[m * ld + m] = lmm;
+      linv = 1.0 / lmm;
+      ua = u0;
+      wc[m] = pc;
+    }
+    if (l < H) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) Y[m * H2 + v * H + l] = yp[v];
+    }
+    if (l == pk) wbits |= 1 << (2 * ps + (pc & 1));
+    ++m;
+    if (P.gmem) gsync();
+    else wsync();
+  };
+  // drop active constraint k: delete row/column k of L, rank-one update of the trailing block
+  // with the deleted column, compact L, Y, codes and multipliers
+  auto drop = [&](int k) {
+    const int kc = rdli((l < m) ? wc[l] : 0, k);
+    if (l == (kc >> 1) % H) wbits &= ~(1 << (2 * ((kc >> 1) / H) + (kc & 1)));
+    double xv = (l > k && l < m) ? L[l * ld + k] : 0.0;
+    for (int j = k + 1; j < m; ++j) {
+      const double Ljj = L[j * ld + j];
+      const double xj = rdl(xv, j);
+      const double rr = sqrt(Ljj * Ljj + xj * xj);
+      const double cc = rr / Ljj, sn = xj / Ljj;
+      if (l == j) L[j * ld + j] = rr;
+      if (l > j && l < m) {
+        const double Lij = (L[l * ld + j] + sn * xv) / cc;
+        xv = cc * xv - sn * Lij;
+        L[l * ld + j] = Lij;
+      }
+    }
+    wsync();
+    // compact: row i <- row i+1 (i >= k), column j <- column j+1 (j >= k); lane = column
+    for (int i = k; i < m - 1; ++i) {
+      const double v = (l < m - 1) ? L[(i + 1) * ld + l + (l >= k ? 1 : 0)] : 0.0;
+      wsync();
+      if (l <= i) L[i * ld + l] = v;
+      wsync();
+    }
+    const int cnext = (l + 1 < m) ? wc[l + 1] : 0;
+    wsync();
+    if (l >= k && l < m - 1) wc[l] = cnext;
+    const double un = shdn(ua, 1);
+    if (l >= k) ua = (l < m - 1) ? un : 0.0;
+    for (int a = k; a < m - 1; ++a) {
+      if (l < H) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) Y[a * H2 + v * H + l] = Y[(a + 1) * H2 + v * H + l];
+      }
+    }
+    --m;
+    if (P.gmem) gsync();
+    else wsync();
+    linv = (l < m) ? 1.0 / L[l * ld + l] : 0.0;
+  };
+  // multipliers of the equality-constrained minimiser on the active set (signed normals):
+  // lam = S^-1 (N x0 - b); kernel multiplier of row a = sign_a * lam_a, GI multiplier -lam_a
+  auto eqp_lam = [&]() -> double {
+    double ax0[NR];
+    A_mul(P, x0, ax0);
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ax0[s] - P.lo(s);   // lower-side residual
+    }
+    wsync();
+    double rhs = 0.0;
+    if (l < m) {
+      const int myc = wc[l], rw = myc >> 1, rs = rw / H;
+      // upper side (box / rate rows only, uniform bounds): -(a'x0 - hi)
+      const double blo = (rs & 1) ? -P.dumax : -P.umax;
+      rhs = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
+    }
+    return tri_bwd(L, ld, linv, tri_fwd(L, ld, linv, rhs, m), m);
+  };
+  auto x_of = [&](double lam) {
+    const int lc = (l < H) ? l : 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xc[v] = x0[v];
+    for (int a = 0; a < m; ++a) {
+      const double la = rdl(lam, a);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) xc[v] -= la * Y[a * H2 + v * H + lc];
+    }
+  };
+
+  // warm row: append unless linearly dependent on the rows already in (multiplier set later)
+  auto warm_add = [&](int pc) {
+    if (m >= cap) return;
+    double yp[NV];
+    const double spp = prep(pc, yp);
+    const double w = fwd();
+    const double lpp2 = spp - wsum(w * w);
+    if (lpp2 > DEP_TOL * spp) append(pc, yp, w, lpp2, 0.0);
+  };
+  bool warm = false;
+  unsigned long long t_wb = STAMP_T();
+  if (P.gws) {
+    // ---- pair: the stored active set (this step's, or the previous step's shifted)
+    const int gm = P.gws[0], gt = P.gws[1];
+    const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
+    if ((same || prev) && gm > 0 && gm <= WAVE) {
+      int code = (l < gm) ? P.gws[2 + l] : -1;
+      if (prev && code >= 0) {
+        const int row = code >> 1, s0 = row / H, k = row - s0 * H;
+        const bool keep = P.hinge(s0) ? (k >= 2) : (k >= 1);
+        code = keep ? 2 * (row - 1) + (code & 1) : -1;
+      }
+      if (NV == 2 && P.g1 == 0.0 && P.g2 == 0.0 && code >= 0 && P.hinge((code >> 1) / H)) code = -1;
+      for (int i = 0; i < gm; ++i) {
+        const int pc = rdli(code, i);
+        if (pc >= 0) warm_add(pc);
+      }
+      warm = true;
+    }
+  } else if (wlab) {
+    // ---- x-step: the rows the current labels hold at a bound
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      const bool in = P.valid(s) && wlab[s] != 0;
+      unsigned long long bm = __ballot(in);
+      const int side = (!P.hinge(s) && wlab[s] == UPPER) ? 1 : 0;
+      while (bm) {
+        const int k = __ffsll(bm) - 1;
+        bm &= bm - 1;
+        warm_add(2 * (s * H + k) + rdli(side, k));
+      }
+    }
+    warm = true;
+  }
+  STAMP_ADD(NV == 2 ? ST_ZR_GEMV : ST_ZR_X, t_wb);
+  unsigned long long t_wf = STAMP_T();
+  if (warm) {
+    {
+      // dual feasibility: drop the most negative (or beyond-cap hinge) multiplier until none
+      double lam = 0.0;
+      while (m > 0) {
+        lam = eqp_lam();
+        const int myc = (l < m) ? wc[l] : 0;
+        const double u = -lam;
+        double sc = 0.0;
+        if (l < m) {
+          if (u < 0.0) sc = u;
+          else if (P.hinge((myc >> 1) / H) && u > P.beta) sc = P.beta - u;
+        }
+        const double smin = wmin(sc);
+        if (!(smin < 0.0)) break;
+        const int k = __ffsll((unsigned long long)__ballot(l < m && sc == smin)) - 1;
+        drop(k);
+      }
+      ua = (l < m) ? -lam : 0.0;
+      x_of(lam);
+    }
+  }
+  STAMP_ADD(NV == 2 ? ST_ZR_S : ST_ZR_CHOL, t_wf);
+
+  while (true) {
+    unsigned long long t_gs = STAMP_T();
+    // ---- most violated constraint outside the active set
+    double ax[NR];
+    A_mul(P, xc, ax);
+    double best = 0.0;
+    int code = -1;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      if (!P.valid(s)) continue;
+      const double tp = P.tol * (1.0 + fabs(P.lo(s)));
+      if (!((wbits >> (2 * s)) & 1)) {
+        const double sv = ax[s] - P.lo(s);
+        if (sv < -tp && sv < best) { best = sv; code = 2 * (s * H + l); }
+      }
+      if (!P.hinge(s) && !((wbits >> (2 * s + 1)) & 1)) {
+        const double sv = P.hi(s) - ax[s];
+        if (sv < -tp && sv < best) { best = sv; code = 2 * (s * H + l) + 1; }
+      }
+    }
+    const double bmin = wmin(best);
+    if (!(bmin < 0.0)) break;
+    const int pl = __ffsll((unsigned long long)__ballot(code >= 0 && best == bmin)) - 1;
+    const int pc = rdli(code, pl);
+    const int prow = pc >> 1, pside = pc & 1, ps = prow / H, pk = prow - ps * H;
+    const bool phinge = P.hinge(ps);
+    double sp = rdl(pside ? P.hi(ps) - ax[ps] : ax[ps] - P.lo(ps), pk);   // slack of p (< 0)
+    double yp[NV];
+    const double spp = prep(pc, yp);       // n_p' P^-1 n_p
+    double up = 0.0;
+    STAMP_ADD(ST_GI_SEARCH, t_gs);
+    while (true) {
+      if (++nsteps > GI_MAX_STEPS) return false;
+      unsigned long long t_gv = STAMP_T();
+      const double w = fwd();
+      const double r = tri_bwd(L, ld, linv, w, m);
+      // z = y_p - Y r
+      double z[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) z[v] = yp[v];
+      {
+        const int lc = (l < H) ? l : 0;
+        for (int a0 = 0; a0 < m; a0 += GEMV_U) {
+          double yv[GEMV_U][NV], rv[GEMV_U];
+#pragma unroll
+          for (int u = 0; u < GEMV_U; ++u) {
+            const int a = min(a0 + u, m - 1);
+            rv[u] = (a0 + u < m) ? rdl(r, a) : 0.0;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) yv[u][v] = Y[a * H2 + v * H + lc];
+          }
+#pragma unroll
+          for (int u = 0; u < GEMV_U; ++u)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) z[v] -= rv[u] * yv[u][v];
+        }
+      }
+      const double lpp2 = spp - wsum(w * w);                   // n_p' z
+      STAMP_ADD(ST_GI_SOLVE, t_gv);
+      unsigned long long t_gu = STAMP_T();
+      const double t2 = (lpp2 > DEP_TOL * spp) ? -sp / lpp2 : INFINITY;
+      // dual step limits: an active multiplier reaching 0 (drop) or a hinge one reaching beta
+      const int myc = (l < m) ? wc[l] : 0;
+      const bool hin_a = (l < m) && P.hinge((myc >> 1) / H);
+      const double tdrop = (l < m && r > 0.0) ? ua / r : INFINITY;
+      const double tcap = (hin_a && r < 0.0) ? (P.beta - ua) / (-r) : INFINITY;
+      const double t1 = wmin(tdrop);
+      const double tc = fmin(wmin(tcap), phinge ? P.beta - up : INFINITY);
+      const double t = fmin(t1, t2);
+      if (!(t < INFINITY) || tc <= t) return false;   // unbounded dual step / hinge saturates
+      if (t2 < INFINITY) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xc[v] += t * z[v];
+        sp += t * lpp2;
+      }
+      if (l < m) ua -= t * r;
+      up += t;
+      if (t2 <= t1) {
+        if (m >= cap) return false;
+        append(pc, yp, w, lpp2, up);
+        STAMP_ADD(ST_GI_UPD, t_gu);
+        break;
+      }
+      drop(__ffsll((unsigned long long)__ballot(l < m && tdrop == t1)) - 1);
+      STAMP_ADD(ST_GI_UPD, t_gu);
+    }
+  }
+  // ---- exact solution of the final active set (the reduced solve with this factor):
+  // lam = S^-1 (N x0 - b), x = x0 - Y lam;  kernel multipliers y_a = sign_a * lam_a
+  {
+    const double lam = eqp_lam();
+    x_of(lam);
+    const int myc = (l < m) ? wc[l] : 0;
+    const int rw = myc >> 1;
+    wsync();
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = 0.0;
+    }
+    wsync();
+    if (l < m) vb_ax[rw] = (myc & 1) ? -lam : lam;
+    wsync();
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = (l < H) ? xc[v] : 0.0;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      const bool lo_in = (wbits >> (2 * s)) & 1, hi_in = (wbits >> (2 * s + 1)) & 1;
+      y[s] = (P.valid(s) && l < H && (lo_in || hi_in)) ? vb_ax[s * H + l] : 0.0;
+      if (P.hinge(s)) lab[s] = lo_in ? HKINK : HZERO;
+      else lab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
+      if (!P.valid(s)) lab[s] = 0;
+    }
+    // this step's active set: the next solve's warm start
+    if (P.gws) {
+      if (l < m) P.gws[2 + l] = myc;
+      if (l == 0) {
+        P.gws[0] = m;
+        P.gws[1] = P.tstep;
+      }
+    }
+    wsync();
+  }
+  return true;
+}
+
+// OSQP-style adaptive rho (in the scaled space): rho *= sqrt((|r_prim|/|Ax,z|) / (|r_dual|/|Px,A'y,q|)).
+// Returns the proposed factor (1 when inside [0.2, 5]).
+template <int NV>
+__device__ __forceinline__ double rho_ratio(const QP<NV>& P, const double* xs, const double* zs, const double* ys) {
+  constexpr int NR = QP<NV>::NR;
+  double xu[NV], ax[NR], px[NV], w[NR], aty[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xu[v] = P.D[v] * xs[v];
+  A_mul(P, xu, ax);
+  P_mul(P, xu, px);
+#pragma unroll
+  for (int s = 0; s < NR; ++s) w[s] = P.valid(s) ? P.E[s] * ys[s] : 0.0;
+  At_mul(P, w, aty);
+  double rp = 0.0, na = 0.0, rd = 0.0, nd = 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    if (!P.valid(s)) continue;
+    const double a = P.E[s] * ax[s];
+    rp = fmax(rp, fabs(a - zs[s]));
+    na = fmax(na, fmax(fabs(a), fabs(zs[s])));
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    if (lid() >= P.H) continue;
+    const double ps = P.D[v] * px[v], qs = P.D[v] * P.q[v], as = P.D[v] * aty[v];
+    rd = fmax(rd, fabs(ps + qs + as));
+    nd = fmax(nd, fmax(fabs(ps), fmax(fabs(qs), fabs(as))));
+  }
+  rp = wmax(rp);
+  na = wmax(na);
+  rd = wmax(rd);
+  nd = wmax(nd);
+  const double num = rp / fmax(na, 1e-30), den = rd / fmax(nd, 1e-30);
+  const double ratio = sqrt(num / fmax(den, 1e-30));
+  return (ratio > 5.0 || ratio < 0.2) ? ratio : 1.0;
+}
+
+// x-step: the linear term q = T'-apply(w') is formed only when a path other than the fused
+// parametric pass needs it (dual active set, ADMM)
+template <int NV>
+__device__ __forceinline__ void ensure_q(QP<NV>& P) {
+  if constexpr (NV == 1) {
+    if (!P.qvalid) {
+      const double qv = Tt_apply(P.wq);
+      P.q[0] = (lid() < P.H) ? qv : 0.0;
+      P.qvalid = true;
+    }
+  }
+}
+
+// Raw warm state (x, y of the last certified solve, unscaled) -> scaled ADMM state.
+template <int NV>
+__device__ __forceinline__ void warm_to_scaled(QP<NV>& P, double* xs, double* zs, double* ys) {
+  constexpr int NR = QP<NV>::NR;
+  double ax[NR];
+  A_mul(P, xs, ax);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) xs[v] = (P.D[v] != 0.0) ? xs[v] / P.D[v] : 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    zs[s] = P.valid(s) ? P.E[s] * ax[s] : 0.0;
+    ys[s] = P.valid(s) ? ys[s] / P.E[s] : 0.0;
+  }
+  P.wraw = false;
+}
+
+// Solve one QP.  (xs, zs, ys) is the warm ADMM state (scaled), lab the warm labels.
+// P.rho may be adapted (K^-1 rebuilt in the scratch kscr, stride kld) and persists.
+// Returns PIADMM_QP_* flags; x_out = unscaled minimiser.
+#ifndef PIADMM_ADAPT_EVERY
+#define PIADMM_ADAPT_EVERY 25
+#endif
+constexpr int ADAPT_EVERY = PIADMM_ADAPT_EVERY;
+template <int NV, bool TWO, int XU = XGEMV_U>
+__device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
+                                        bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
+                                        double* x_out, int& n_admm, int& n_pdas, int& n_gi) {
+  constexpr int NR = QP<NV>::NR;
+  double x[NV], y[NR];
+  bool ok = false;
+  signed char flab[NR];   // labels a PDAS attempt already failed from
+#pragma unroll
+  for (int s = 0; s < NR; ++s) flab[s] = -1;
+  if (warm_lab) {
+#pragma unroll
+    for (int s = 0; s < NR; ++s) flab[s] = lab[s];
+    if (NV == 1 && P.ycap > 0) {
+      // x-step: the warm labels' reduced solve (a cached-table hit in the steady state); when
+      // its certificate fails, the dual active set warm-started from those labels finds the
+      // new working set in a few steps, and one reduced solve on it certifies (instead of a
+      // table rebuild per one-step PDAS label move, then ADMM)
+      ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
+      if (__builtin_expect(!ok, 0)) {
+        int ngi = 0;
+        signed char glab[NR];
+        ensure_q(P);
+        if (gi_solve(P, flab, glab, x, y, ngi)) {
+#pragma unroll
+          for (int s = 0; s < NR; ++s) lab[s] = glab[s];
+          ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+        }
+        n_gi += ngi;
+        if (!ok) {
+#pragma unroll
+          for (int s = 0; s < NR; ++s) lab[s] = flab[s];
+          ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+        }
+      }
+    } else {
+      ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+    }
+  }
+  if constexpr (NV == 2) {
+    // pair QP: dual active set first (no K_s^-1, no ADMM); certified by the KKT test, and
+    // when that fails, polished from its labels before the ADMM fallback
+    if (!ok && P.ycap > 0) {
+      int ngi = 0;
+      signed char glab[NR];
+      if (gi_solve(P, nullptr, glab, x, y, ngi)) {
+        signed char nl[NR];
+        ok = kkt_check(P, glab, x, y, nl);
+#pragma unroll
+        for (int s = 0; s < NR; ++s) lab[s] = glab[s];
+        if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+      }
+      n_gi += ngi;
+    }
+  }
+  signed char plab[NR];
+#pragma unroll
+  for (int s = 0; s < NR; ++s) plab[s] = -1;
+  if (__builtin_expect(!ok && !P.kready, 0)) {
+    if (!P.scaled) {
+      // the warm ADMM state is in identity scaling (x, A x, y): move it to the Ruiz space
+      if (P.wraw) warm_to_scaled(P, xs, zs, ys);     // identity D, E: (x, A x, y)
+      unsigned long long t_r = STAMP_T();
+      ruiz(P);
+      STAMP_ADD(ST_SZ_RUIZ, t_r);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) xs[v] = (P.D[v] != 0.0) ? xs[v] / P.D[v] : 0.0;
+#pragma unroll
+      for (int s = 0; s < NR; ++s) {
+        zs[s] = P.valid(s) ? P.E[s] * zs[s] : 0.0;
+        ys[s] = P.valid(s) ? ys[s] / P.E[s] : 0.0;
+      }
+      P.scaled = true;
+    }
+    if (NV == 1 && P.Kcache) {
+      // the per-scenario HBM copy (same penalty): batched loads, then the LDS stores
+      const int l = lid(), n = P.n;
+      for (int i0 = 0; i0 < n; i0 += 8) {
+        double kv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kv[u] = (l < n) ? P.Kcache[min(i0 + u, n - 1) * n + l] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (l < n && i0 + u < n) {
+            if (P.kf32) P.Kf[(i0 + u) * n + l] = (float)kv[u];
+            else P.K[(i0 + u) * n + l] = kv[u];
+          }
+        }
+      }
+    } else {
+      build_K<NV, TWO>(P, kscr, kld);
+    }
+    P.kready = true;
+    if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
+    wsync();
+  }
+  if (__builtin_expect(!ok, 0)) ensure_q(P);
+  if (!ok && P.wraw) warm_to_scaled(P, xs, zs, ys);
+  for (int it = 1; __builtin_expect(!ok, 0) && it <= max_inner; ++it) {
+    unsigned long long t_a = STAMP_T();
+    admm_iter(P, xs, zs, ys);
+    STAMP_ADD(ST_ADMM, t_a);
+    ++n_admm;
+    // adaptive rho for the x-step only: on the pair QPs with long runs of hinge kinks the
+    // OSQP rule stalls ADMM (tools/pair_policy.py: 3 of 15 hard pair QPs uncertified after
+    // 4000 iterations with it, all 15 certified within 530 without it)
+    if (NV == 1 && it % ADAPT_EVERY == 0) {
+      const double f = rho_ratio(P, xs, zs, ys);
+      if (f != 1.0) {
+        P.rho = fmin(fmax(P.rho * f, 1e-6), 1e6);
+        build_K<NV, TWO>(P, kscr, kld);
+        P.Kcache = nullptr;      // the cached copy is for the old penalty
+        if (NV == 2 && lid() == 0) P.fstate[0] = -1;   // the scratch held the pair's cached factor
+        wsync();
+      }
+    }
+    if (it % polish_every == 0) {
+      // polish when the ADMM active-set estimate has not moved since the last check
+      // (or every 8 periods), and never twice from the same labels
+      bool same = true, tried = true;
+#pragma unroll
+      for (int s = 0; s < NR; ++s) {
+        lab[s] = label_scaled(P, s, zs[s] + ys[s] / rrow(P, s));
+        same &= (lab[s] == plab[s]);
+        tried &= (lab[s] == flab[s]);
+        plab[s] = lab[s];
+      }
+      if ((wall(same) || it % (8 * polish_every) == 0) && !wall(tried)) {
+#pragma unroll
+        for (int s = 0; s < NR; ++s) flab[s] = lab[s];
+        ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+      }
+    }
+  }
+  unsigned long long t_ep = STAMP_T();
+  int st = PIADMM_QP_OK;
+  if (ok) {
+    // warm ADMM state at the exact optimum, kept raw until an ADMM iteration needs it
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xs[v] = x[v];
+#pragma unroll
+    for (int s = 0; s < NR; ++s) ys[s] = P.valid(s) ? y[s] : 0.0;
+    P.wraw = true;
+  } else {
+    st |= PIADMM_QP_INEXACT;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = P.D[v] * xs[v];
+#pragma unroll
+    for (int s = 0; s < NR; ++s) lab[s] = label_scaled(P, s, zs[s] + ys[s] / rrow(P, s));
+  }
+  bool fin = true;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    x_out[v] = (lid() < P.H) ? x[v] : 0.0;
+    fin &= isfinite(x_out[v]);
+  }
+  if (!wall(fin)) st |= PIADMM_QP_NAN;
+  if (NV == 1) STAMP_ADD(ST_QEPI, t_ep);
+  return st;
+}
+
+}  // namespace pd

@@ -35,6 +35,7 @@ struct piadmm_ctx {
   int giters = 0;
   int step_cap = 1;              // MPC steps per persistent launch (resid slots)
   bool coop = false;             // term_global natural termination decided in-kernel (one rank)
+  std::vector<double> rho_init;  // host staging of the initial ADMM penalties (outlives the async copy)
 };
 
 namespace {
@@ -89,6 +90,17 @@ int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
   if (pd::lds_bytes(c.H, c.precision) + pd::STATIC_LDS > pd::MAX_LDS)
     return fail(h, PIADMM_E_ARG, "the workgroup's LDS exceeds 160 KB (precision 1 keeps the pair's fp32 "
                                   "K_s^-1 in LDS: H <= 55 in big mode)");
+  return 0;
+}
+
+// Initial ADMM penalties (x-step: adapted by the OSQP rule and carried across steps; pair QPs
+// keep this penalty: no adaptation, and on the GPU smaller fixed penalties cost more ADMM
+// iterations on the bench's pair QPs -- 0.5x: +0%, 0.2x: +39%, 0.1x: +114% time).
+int reset_penalties(piadmm_ctx* h) {
+  const size_t N = h->N, E = h->E;
+  h->rho_init.assign(std::max<size_t>(N, E) + 1, h->cfg.admm_rho);
+  HIPCHK(h, hipMemcpyAsync(h->a.rho_x, h->rho_init.data(), N * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  if (E) HIPCHK(h, hipMemcpyAsync(h->a.rho_e, h->rho_init.data(), E * sizeof(double), hipMemcpyHostToDevice, h->stream));
   return 0;
 }
 
@@ -288,16 +300,8 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   HIPCHK(h, hipMemcpyAsync(d_nb, nbr.data(), N * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(A.xt, xt0, (size_t)N * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
   {
-    std::vector<double> r0((size_t)std::max<size_t>(N, E), h->cfg.admm_rho);
-    HIPCHK(h, hipMemcpyAsync(A.rho_x, r0.data(), (size_t)N * sizeof(double), hipMemcpyHostToDevice, h->stream));
-    // (pair QPs keep this penalty: no adaptation, and on the GPU smaller fixed penalties cost
-    // more ADMM iterations on the bench's pair QPs -- 0.5x: +0%, 0.2x: +39%, 0.1x: +114% time)
-#ifndef PIADMM_PAIR_RHO_SCALE
-#define PIADMM_PAIR_RHO_SCALE 1.0
-#endif
-    std::vector<double> r1((size_t)std::max<size_t>(E, 1), h->cfg.admm_rho * PIADMM_PAIR_RHO_SCALE);
-    if (E) HIPCHK(h, hipMemcpyAsync(A.rho_e, r1.data(), E * sizeof(double), hipMemcpyHostToDevice, h->stream));
   }
+  if (int rc2 = reset_penalties(h)) return rc2;
   HIPCHK(h, hipMemsetAsync(A.xcache_rho, 0xff, (size_t)N * sizeof(double), h->stream));   // NaN: no cache
   HIPCHK(h, hipStreamSynchronize(h->stream));
   A.spd = d_spd;
@@ -327,6 +331,9 @@ int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
   // a new state breaks the receding-horizon sequence: no label warm start for the next step
   HIPCHK(h, hipMemsetAsync(h->a.warm_ok, 0, (size_t)h->N * sizeof(int), h->stream));
   if (h->E) HIPCHK(h, hipMemsetAsync(h->a.gi_ws, 0, (size_t)h->E * (2 + pd::WAVE) * sizeof(int), h->stream));
+  // and no carried ADMM penalties: a run from a new state starts from the configured penalty
+  // (the per-scenario caches stay: they are keyed by the penalty they were built for)
+  if (int rc = reset_penalties(h)) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PIADMM_OK;
 }
@@ -558,7 +565,9 @@ int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n) {
   if (!h || !out) return fail(h, PIADMM_E_ARG, "null argument");
   if (!h->a.stamps) return fail(h, PIADMM_E_STATE, "library built without PIADMM_STAMPS");
   if (n < h->C * 64) return fail(h, PIADMM_E_ARG, "buffer too small");
-  HIPCHK(h, hipMemcpy(out, h->a.stamps, (size_t)h->C * 64 * 8, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  HIPCHK(h, hipMemcpyAsync(out, h->a.stamps, (size_t)h->C * 64 * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
   return PIADMM_OK;
 }
 

@@ -87,6 +87,12 @@ constexpr int xrows(int H) { return H + 2 < 64 ? H + 2 : 64; }
 constexpr size_t STATIC_LDS = NW * 272 * 4 + NW * 8 * 4 + 16;
 constexpr size_t MAX_LDS = 160 * 1024;
 
+// fp32 agent K_s^-1 images in LDS mode: per wave H*H floats rounded up to an even count, so
+// that the next wave's region (which also holds its fp64 dual active-set columns) is 8-byte
+// aligned for odd H; kxf_words = the two waves' regions in doubles.
+constexpr size_t kxf_stride(int H) { return ((size_t)H * H + 1) & ~(size_t)1; }
+constexpr size_t kxf_words(int H) { return kxf_stride(H); }
+
 // LDS bytes needed by one workgroup for horizon H (must match the carve in k_mpc_step).
 // LDS mode (H <= HMAX): every matrix of the component in LDS.  Big mode: agent K_s^-1, G and
 // X' and the pair K_s^-1 in HBM / L2; LDS keeps the factor scratches and the vectors.
@@ -94,7 +100,7 @@ inline size_t lds_bytes(int H, int precision = 0) {
   size_t d = 0;
   const bool f32 = precision == 1;
   if (H <= HMAX) {
-    d += (f32 ? 1 : 2) * (size_t)H * H;   // agent K_s^-1 (2 agents; fp32: half)
+    d += f32 ? kxf_words(H) : 2 * (size_t)H * H;   // agent K_s^-1 (2 agents; fp32: half)
     d += 2 * ((size_t)H * H + H);    // agent polish G | g (2 agents)
     d += (f32 ? 2 : 4) * (size_t)H * H;   // pair K_s^-1 (2H x 2H)
     d += 64 * LD;                    // pair matrix scratch (wave 0)

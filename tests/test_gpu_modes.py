@@ -118,9 +118,10 @@ def test_rccl_single_rank_communicator(Solver):
             scenario.tiled(2, 12, n_steps=10, seed=1), 3, setup=lambda s: s.comm_init(comm_unique_id(), 1, 0))
 
 
-@pytest.mark.parametrize("H,n", [(10, 12), (30, 6), (50, 3)])
+@pytest.mark.parametrize("H,n", [(10, 12), (15, 8), (25, 6), (30, 6), (50, 3)])
 def test_fp32_admm_matrices_keep_answers(Solver, H, n):
     """precision 1 (configs[4] study): the ADMM iterations read fp32 K_s^-1 images, the polish
-    and its KKT certificate stay fp64 -- every QP certified, answers equal the oracle's."""
+    and its KKT certificate stay fp64 -- every QP certified, answers equal the oracle's.  Odd H
+    (15, 25) checks the 8-byte alignment of the second wave's fp32 region in LDS mode."""
     compare(Solver, config.matlab_pi(H=H, precision=1, tighten=int(H == 50)),
             scenario.tiled(2, H, n_steps=12, seed=H + 1), n)

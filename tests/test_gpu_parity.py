@@ -8,6 +8,7 @@ At BASELINE sizes (256 and 1024 agents) parity is checked on sampled tiles
 against the live oracle plus size-independent properties (tile independence,
 permutation equivariance, certified solves).
 """
+import ast
 import os
 
 import numpy as np
@@ -37,7 +38,7 @@ def close(a, b, rtol=RTOL, atol=ATOL):
 
 def fixture_run(name):
     d = np.load(os.path.join(GOLD, f"run_{name}.npz"), allow_pickle=False)
-    cfg = config.PRESETS[str(d["preset"])](**eval(str(d["cfg_kw"])))   # written by oracle/gen_golden.py
+    cfg = config.PRESETS[str(d["preset"])](**ast.literal_eval(str(d["cfg_kw"])))   # written by oracle/gen_golden.py
     scn = scenario.Scenario(spd=d["spd"], xt0=d["xt0"], ref=d["ref"], edges=d["edges"], n_steps=d["xt"].shape[0])
     return d, cfg, scn
 

@@ -9,6 +9,7 @@ Pinning chain ("Oracle and parity"):
   * loop semantics: regression against committed oracle runs + structural
     invariants (tiling, aliasing quirk B4, rounding B6, collision threshold B2).
 """
+import ast
 import os
 
 import numpy as np
@@ -111,7 +112,7 @@ def test_qp_rejects_infeasible_start():
 @pytest.mark.parametrize("name", ["casadi_default_H10", "casadi_default_H15", "matlab_pi_H10", "matlab_pi_H8"])
 def test_oracle_runs_reproduce_fixtures(name):
     d = load(f"run_{name}.npz")
-    cfg = config.PRESETS[str(d["preset"])](**eval(str(d["cfg_kw"])))   # fixture written by oracle/gen_golden.py
+    cfg = config.PRESETS[str(d["preset"])](**ast.literal_eval(str(d["cfg_kw"])))   # fixture written by oracle/gen_golden.py
     scn = scenario.Scenario(spd=d["spd"], xt0=d["xt0"], ref=d["ref"], edges=d["edges"], n_steps=d["xt"].shape[0])
     orc = O.Oracle(cfg, scn)
     for s in range(d["xt"].shape[0]):

@@ -1,8 +1,8 @@
 """Development tool (not shipped, not the oracle): Goldfarb-Idnani dual active set on the pair QP (hinge form), Schur/Cholesky form.
 Constraint ids: 2*r (lower side of row r: a'x >= l), 2*r+1 (upper side: -a'x >= -u); hinge rows
 only lower side with multiplier cap beta."""
-import sys, numpy as np
-sys.path.insert(0,'/root/repo/tools')
+import os, sys, numpy as np
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import qp_sim as Q
 
 def gi(gq, Pinv, max_steps=300, tol=1e-9, stats=None):
