@@ -1111,9 +1111,14 @@ constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t
 // and constraints with negative (or beyond-cap) multipliers dropped until the start is dual
 // feasible -- the state GI requires -- before the usual adds.  Any starting set is only a
 // guess: the minimiser and its certificate do not depend on it.
+#ifdef PIADMM_GI_DEBUG
+#define GI_DBG(...) do { if (lid() == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define GI_DBG(...) ((void)0)
+#endif
 template <int NV>
 __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, signed char* lab, double* x, double* y,
-                                         int& nsteps) {
+                                         int& nsteps, signed char* flab = nullptr) {
   constexpr int NR = QP<NV>::NR;
   const int l = lid(), H = P.H, ld = P.fld, H2 = NV * H;
   double* vb_ax = P.vb + 192;      // [192, 192 + NR*H): (A v) by row id
@@ -1125,11 +1130,34 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   if (l == 0) P.fstate[0] = -1;    // and L the cached PDAS factor
   P.csig = -1;                     // (x-step: the factor scratch the parametric tables were built in)
   double x0[NV], xc[NV];
-  gemv_sym<true>(P, P.Pinv, P.q, x0);
-#pragma unroll
-  for (int v = 0; v < NV; ++v) xc[v] = x0[v] = -x0[v];
   int m = 0, wbits = 0;
   double ua = 0.0, linv = 0.0;     // lane a < m: multiplier and 1/L_aa of active constraint a
+  // Pair: hinge rows fixed in their linear regime (this lane's hinge row).  A hinge whose
+  // multiplier saturates at its cap beta is linear at the optimum, which the dual active set
+  // does not model: GI restarts with that row linear -- its term beta (h - a'x) moves into q
+  // (as in reduced_solve) and the row leaves the constraint search -- warm-started from the
+  // active set it had reached.  The final KKT test checks the linear rows (a'x <= h).
+  bool lin = false;
+  int rcode = -1, rm = 0;
+  auto start = [&]() {
+    double qt[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) qt[v] = P.q[v];
+    if constexpr (NV == 2) {
+      const double tt = Tt_apply((P.valid(4) && lin) ? 1.0 : 0.0);
+      if (l < H) {
+        qt[0] -= P.beta * P.g1 * tt;
+        qt[1] -= P.beta * P.g2 * tt;
+      }
+    }
+    gemv_sym<true>(P, P.Pinv, qt, x0);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xc[v] = x0[v] = -x0[v];
+    m = 0;
+    wbits = 0;
+    ua = 0.0;
+    linv = 0.0;
+  };
 
   // y_p = P^-1 n_p (lane = variable), A y_p to vb_ax; returns n_p' P^-1 n_p
   auto prep = [&](int pc, double* yp) -> double {
@@ -1243,6 +1271,21 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     }
   };
 
+  // On failure (flab != nullptr): the current working set as PDAS labels -- a start for the
+  // polish instead of ADMM.  A hinge row whose multiplier reached the cap beta (row id hrow,
+  // lane-uniform; -1: none) is in its linear regime there: label HLINEAR.
+  auto fail_labels = [&](int hrow) {
+    if (!flab) return;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      const bool lo_in = (wbits >> (2 * s)) & 1, hi_in = (wbits >> (2 * s + 1)) & 1;
+      if (P.hinge(s)) flab[s] = lo_in ? HKINK : HZERO;
+      else flab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
+      if (P.hinge(s) && (lin || hrow == s * H + l)) flab[s] = HLINEAR;
+      if (!P.valid(s)) flab[s] = 0;
+    }
+  };
+
   // warm row: append unless linearly dependent on the rows already in (multiplier set later)
   auto warm_add = [&](int pc) {
     if (m >= cap) return;
@@ -1252,9 +1295,20 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     const double lpp2 = spp - wsum(w * w);
     if (lpp2 > DEP_TOL * spp) append(pc, yp, w, lpp2, 0.0);
   };
+  constexpr int GI_LIN_ROUNDS = WAVE;   // every hinge row may end linear
+  for (int round = 0;; ++round) {
+  start();
   bool warm = false;
+  bool again = false;
   unsigned long long t_wb = STAMP_T();
-  if (P.gws) {
+  if (round > 0) {
+    // ---- restart: the previous round's active set without the saturated hinge row
+    for (int i = 0; i < rm; ++i) {
+      const int pc = rdli(rcode, i);
+      if (pc >= 0) warm_add(pc);
+    }
+    warm = true;
+  } else if (P.gws) {
     // ---- pair: the stored active set (this step's, or the previous step's shifted)
     const int gm = P.gws[0], gt = P.gws[1];
     const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
@@ -1323,6 +1377,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
 #pragma unroll
     for (int s = 0; s < NR; ++s) {
       if (!P.valid(s)) continue;
+      if (P.hinge(s) && lin) continue;          // fixed linear (see start)
       const double tp = P.tol * (1.0 + fabs(P.lo(s)));
       if (!((wbits >> (2 * s)) & 1)) {
         const double sv = ax[s] - P.lo(s);
@@ -1345,7 +1400,11 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     double up = 0.0;
     STAMP_ADD(ST_GI_SEARCH, t_gs);
     while (true) {
-      if (++nsteps > GI_MAX_STEPS) return false;
+      if (++nsteps > GI_MAX_STEPS) {
+        GI_DBG("GI fail: step limit m=%d round=%d\n", m, round);
+        fail_labels(-1);
+        return false;
+      }
       unsigned long long t_gv = STAMP_T();
       const double w = fwd();
       const double r = tri_bwd(L, ld, linv, w, m);
@@ -1382,7 +1441,31 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       const double t1 = wmin(tdrop);
       const double tc = fmin(wmin(tcap), phinge ? P.beta - up : INFINITY);
       const double t = fmin(t1, t2);
-      if (!(t < INFINITY) || tc <= t) return false;   // unbounded dual step / hinge saturates
+      if (tc <= t) {                                 // a hinge multiplier saturates at beta
+        const double tca = wmin(tcap);
+        int hrow;
+        if (phinge && P.beta - up <= tca) {
+          hrow = prow;                               // the entering hinge row
+        } else {
+          const int k = __ffsll((unsigned long long)__ballot(l < m && hin_a && tcap == tca)) - 1;
+          hrow = rdli(myc, k) >> 1;
+        }
+        if (NV == 2 && round < GI_LIN_ROUNDS && hrow / H == 4) {
+          if (l == hrow - 4 * H) lin = true;
+          rcode = (l < m && (wc[l] >> 1) != hrow) ? wc[l] : -1;
+          rm = m;
+          again = true;
+          break;
+        }
+        GI_DBG("GI fail: hinge cap hrow=%d m=%d round=%d\n", hrow, m, round);
+        fail_labels(hrow);
+        return false;
+      }
+      if (!(t < INFINITY)) {                         // unbounded dual step
+        GI_DBG("GI fail: unbounded dual step m=%d round=%d lpp2=%g spp=%g sp=%g\n", m, round, lpp2, spp, sp);
+        fail_labels(-1);
+        return false;
+      }
       if (t2 < INFINITY) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) xc[v] += t * z[v];
@@ -1391,7 +1474,11 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       if (l < m) ua -= t * r;
       up += t;
       if (t2 <= t1) {
-        if (m >= cap) return false;
+        if (m >= cap) {
+          GI_DBG("GI fail: full m=%d cap=%d round=%d\n", m, cap, round);
+          fail_labels(-1);
+          return false;
+        }
         append(pc, yp, w, lpp2, up);
         STAMP_ADD(ST_GI_UPD, t_gu);
         break;
@@ -1399,7 +1486,10 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       drop(__ffsll((unsigned long long)__ballot(l < m && tdrop == t1)) - 1);
       STAMP_ADD(ST_GI_UPD, t_gu);
     }
+    if (again) break;
   }
+  if (!again) break;
+  }   // rounds
   // ---- exact solution of the final active set (the reduced solve with this factor):
   // lam = S^-1 (N x0 - b), x = x0 - Y lam;  kernel multipliers y_a = sign_a * lam_a
   {
@@ -1421,7 +1511,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     for (int s = 0; s < NR; ++s) {
       const bool lo_in = (wbits >> (2 * s)) & 1, hi_in = (wbits >> (2 * s + 1)) & 1;
       y[s] = (P.valid(s) && l < H && (lo_in || hi_in)) ? vb_ax[s * H + l] : 0.0;
-      if (P.hinge(s)) lab[s] = lo_in ? HKINK : HZERO;
+      if (P.hinge(s) && lin && P.valid(s)) y[s] = -P.beta;
+      if (P.hinge(s)) lab[s] = lin ? HLINEAR : (lo_in ? HKINK : HZERO);
       else lab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
       if (!P.valid(s)) lab[s] = 0;
     }
@@ -1556,12 +1647,20 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
     if (!ok && P.ycap > 0) {
       int ngi = 0;
       signed char glab[NR];
-      if (gi_solve(P, nullptr, glab, x, y, ngi)) {
+      signed char clab[NR];
+      if (gi_solve(P, nullptr, glab, x, y, ngi, clab)) {
         signed char nl[NR];
         ok = kkt_check(P, glab, x, y, nl);
 #pragma unroll
         for (int s = 0; s < NR; ++s) lab[s] = glab[s];
         if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+      } else {
+        // GI stopped (typically a hinge multiplier at its cap beta: that hinge is linear at the
+        // optimum, which the dual active set does not model): polish from its working set with
+        // the saturated row linear before falling back to ADMM
+#pragma unroll
+        for (int s = 0; s < NR; ++s) lab[s] = clab[s];
+        ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 4 * PDAS_STEPS);
       }
       n_gi += ngi;
     }

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -36,6 +37,7 @@ struct piadmm_ctx {
   int step_cap = 1;              // MPC steps per persistent launch (resid slots)
   bool coop = false;             // term_global natural termination decided in-kernel (one rank)
   std::vector<double> rho_init;  // host staging of the initial ADMM penalties (outlives the async copy)
+  std::vector<std::vector<int>> graph_host;   // graph-mode index arrays (host staging)
 };
 
 namespace {
@@ -179,17 +181,23 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   const int N = h->cfg.n_agents, H = h->cfg.H;
   if (T < H + 1) return fail(h, PIADMM_E_ARG, "reference too short: T < H+1");
   if (n_edges < 0) return fail(h, PIADMM_E_ARG, "n_edges < 0");
-  // components: consecutive pairs (v, v+1) joined by an edge, or single agents
-  std::vector<int> pair_of(N, -1);
   for (int e = 0; e < n_edges; ++e) {
     const int v1 = edges[2 * e], v2 = edges[2 * e + 1];
     if (v1 < 0 || v2 >= N || v1 >= v2) return fail(h, PIADMM_E_ARG, "edge must satisfy 0 <= v1 < v2 < N");
-    if (v2 != v1 + 1)
-      return fail(h, PIADMM_E_ARG, "this version needs every candidate pair to be (v, v+1) (components of <= 2 agents)");
-    if (pair_of[v1] >= 0 || pair_of[v2] >= 0)
-      return fail(h, PIADMM_E_ARG, "an agent belongs to two pairs: components of <= 2 agents only in this version");
-    pair_of[v1] = e;
-    pair_of[v2] = e;
+  }
+  // The fused kernel (piadmm_device.hip) takes components of one agent or one pair (v, v+1);
+  // any other candidate graph -- components of more agents, agents in several pairs -- runs
+  // on the graph kernel (piadmm_graph.hip).  PIADMM_GRAPH=1 forces graph mode (tests).
+  std::vector<int> pair_of(N, -1);
+  bool simple = true;
+  for (int e = 0; e < n_edges && simple; ++e) {
+    const int v1 = edges[2 * e], v2 = edges[2 * e + 1];
+    if (v2 != v1 + 1 || pair_of[v1] >= 0 || pair_of[v2] >= 0) simple = false;
+    else pair_of[v1] = pair_of[v2] = e;
+  }
+  {
+    const char* g = std::getenv("PIADMM_GRAPH");
+    if (g && g[0] == '1') simple = false;
   }
   for (int i = 0; i < N; ++i)
     if (!std::isfinite(spd[i]) || !std::isfinite(xt0[3 * i]) || !std::isfinite(xt0[3 * i + 1]) ||
@@ -201,17 +209,74 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   h->comp_ptr.assign(1, 0);
   h->comp_edge.clear();
   std::vector<int> nbr(N, 0);
-  for (int a = 0; a < N;) {
-    const int e = pair_of[a];
-    if (e >= 0) {
-      h->comp_edge.push_back(e);
-      nbr[a] = nbr[a + 1] = 1;
-      a += 2;
-    } else {
-      h->comp_edge.push_back(-1);
-      a += 1;
+  // graph mode: connected components labelled in order of their first agent (the oracle's
+  // Scenario.components()), agent / pair lists per component, neighbour CSR sorted by
+  // neighbour id (the order of the x-step's consensus sum)
+  std::vector<int> g_aptr, g_alist, g_eptr, g_elist, g_nptr, g_nedge, g_ndir;
+  if (simple) {
+    for (int a = 0; a < N;) {
+      const int e = pair_of[a];
+      if (e >= 0) {
+        h->comp_edge.push_back(e);
+        nbr[a] = nbr[a + 1] = 1;
+        a += 2;
+      } else {
+        h->comp_edge.push_back(-1);
+        a += 1;
+      }
+      h->comp_ptr.push_back(a);
     }
-    h->comp_ptr.push_back(a);
+  } else {
+    std::vector<int> parent(N);
+    for (int a = 0; a < N; ++a) parent[a] = a;
+    auto find = [&](int a) {
+      while (parent[a] != a) a = parent[a] = parent[parent[a]];
+      return a;
+    };
+    for (int e = 0; e < n_edges; ++e) {
+      const int ra = find(edges[2 * e]), rb = find(edges[2 * e + 1]);
+      if (ra != rb) parent[std::max(ra, rb)] = std::min(ra, rb);
+    }
+    std::vector<int> comp(N), id_of(N, -1);
+    int C = 0;
+    for (int a = 0; a < N; ++a) {
+      const int r = find(a);
+      if (id_of[r] < 0) id_of[r] = C++;
+      comp[a] = id_of[r];
+    }
+    g_aptr.assign(C + 1, 0);
+    g_eptr.assign(C + 1, 0);
+    for (int a = 0; a < N; ++a) ++g_aptr[comp[a] + 1];
+    for (int e = 0; e < n_edges; ++e) ++g_eptr[comp[edges[2 * e]] + 1];
+    for (int k = 0; k < C; ++k) {
+      g_aptr[k + 1] += g_aptr[k];
+      g_eptr[k + 1] += g_eptr[k];
+    }
+    g_alist.resize(N);
+    g_elist.resize(n_edges);
+    {
+      std::vector<int> fa(g_aptr.begin(), g_aptr.end() - 1), fe(g_eptr.begin(), g_eptr.end() - 1);
+      for (int a = 0; a < N; ++a) g_alist[fa[comp[a]]++] = a;
+      for (int e = 0; e < n_edges; ++e) g_elist[fe[comp[edges[2 * e]]]++] = e;
+    }
+    std::vector<std::vector<std::array<int, 3>>> adj(N);
+    for (int e = 0; e < n_edges; ++e) {
+      const int v1 = edges[2 * e], v2 = edges[2 * e + 1];
+      adj[v1].push_back({v2, e, 0});
+      adj[v2].push_back({v1, e, 1});
+    }
+    g_nptr.assign(N + 1, 0);
+    for (int a = 0; a < N; ++a) {
+      std::sort(adj[a].begin(), adj[a].end());
+      nbr[a] = (int)adj[a].size();
+      g_nptr[a + 1] = g_nptr[a] + nbr[a];
+      for (const auto& x : adj[a]) {
+        g_nedge.push_back(x[1]);
+        g_ndir.push_back(x[2]);
+      }
+    }
+    h->comp_ptr = g_aptr;                  // (sizes only: agents of a component need not be contiguous)
+    h->comp_edge.assign(C, -1);
   }
   h->N = N;
   h->E = n_edges;
@@ -260,10 +325,12 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.Pinv_x, (size_t)N * H * H);
   rc |= dalloc(h, &A.sc_x, (size_t)N * 4 * pd::HCAP);
   rc |= dalloc(h, &A.lab_x, (size_t)N * 2 * pd::HCAP);
-  const bool big = H > pd::HMAX;
+  A.graph = simple ? 0 : 1;
+  const bool big = H > pd::HMAX || A.graph;   // graph mode: the big-mode HBM layout at every H
   rc |= dalloc(h, &A.Gx_g, big ? (size_t)N * (H * H + H) : 1);
   rc |= dalloc(h, &A.XT_g, big ? (size_t)N * H1 * pd::XLDG : 1);
-  rc |= dalloc(h, &A.Ke_g, big ? E * 4 * H * H : 1);
+  A.ke_stride = A.graph ? std::max(4 * H * H, 2 * H * pd::WAVE) : 4 * H * H;
+  rc |= dalloc(h, &A.Ke_g, big ? E * A.ke_stride : 1);
   rc |= dalloc(h, &A.Yx_g, big ? (size_t)N * pd::WAVE * H : 1);
   rc |= dalloc(h, &A.tab_e, E * 8 * H * H);
   rc |= dalloc(h, &A.warm_ok, (size_t)N);
@@ -288,6 +355,23 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   rc |= dalloc(h, &A.gpart, (size_t)2 * C * 5);
   rc |= dalloc(h, &A.ghist, (size_t)h->step_cap * std::max(h->cfg.max_outer, 1) * 2);
   rc |= dalloc(h, &A.giters, (size_t)h->step_cap);
+  int *d_gap = nullptr, *d_gal = nullptr, *d_gep = nullptr, *d_gel = nullptr, *d_gnp = nullptr, *d_gne = nullptr,
+      *d_gnd = nullptr;
+  if (A.graph) {
+    rc |= dalloc(h, &d_gap, C + 1);
+    rc |= dalloc(h, &d_gal, (size_t)N);
+    rc |= dalloc(h, &d_gep, C + 1);
+    rc |= dalloc(h, &d_gel, E);
+    rc |= dalloc(h, &d_gnp, (size_t)N + 1);
+    rc |= dalloc(h, &d_gne, 2 * E);
+    rc |= dalloc(h, &d_gnd, 2 * E);
+    rc |= dalloc(h, &A.seed_g, (size_t)N * 2);
+    rc |= dalloc(h, &A.eres, E * 2);
+    rc |= dalloc(h, &A.cpart, C * 5);
+    rc |= dalloc(h, &A.csig_x, (size_t)N * pd::WAVE);
+    rc |= dalloc(h, &A.xflags, (size_t)N);
+    rc |= dalloc(h, &A.eflags, E);
+  }
 #ifdef PIADMM_STAMPS
   rc |= dalloc(h, &A.stamps, C * 64);
 #endif
@@ -299,7 +383,20 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   if (E) HIPCHK(h, hipMemcpyAsync(d_ed, edges, 2 * E * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(d_nb, nbr.data(), N * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(A.xt, xt0, (size_t)N * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
-  {
+  if (A.graph) {
+    h->graph_host = {g_aptr, g_alist, g_eptr, g_elist, g_nptr, g_nedge, g_ndir};   // outlive the copies
+    int* dst[7] = {d_gap, d_gal, d_gep, d_gel, d_gnp, d_gne, d_gnd};
+    for (int k = 0; k < 7; ++k)
+      if (!h->graph_host[k].empty())
+        HIPCHK(h, hipMemcpyAsync(dst[k], h->graph_host[k].data(), h->graph_host[k].size() * sizeof(int),
+                                 hipMemcpyHostToDevice, h->stream));
+    A.comp_aptr = d_gap;
+    A.comp_alist = d_gal;
+    A.comp_eptr = d_gep;
+    A.comp_elist = d_gel;
+    A.nbr_ptr = d_gnp;
+    A.nbr_edge = d_gne;
+    A.nbr_dir = d_gnd;
   }
   if (int rc2 = reset_penalties(h)) return rc2;
   HIPCHK(h, hipMemsetAsync(A.xcache_rho, 0xff, (size_t)N * sizeof(double), h->stream));   // NaN: no cache
@@ -317,7 +414,7 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   {
     const char* nc = std::getenv("PIADMM_NO_COOP");
     h->coop = h->cfg.term_global && !h->cfg.fixed_iters && !(nc && nc[0] == '1') &&
-              pd::coop_fits(A, h->cfg.device);
+              (A.graph ? pd::graph_coop_fits(A, h->cfg.device) : pd::coop_fits(A, h->cfg.device));
   }
   h->have_scn = true;
   return PIADMM_OK;
@@ -349,6 +446,11 @@ int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
     if (_r != ncclSuccess) return fail((h), PIADMM_E_HIP, std::string(#expr ": ") + ncclGetErrorString(_r)); \
   } while (0)
 
+// One launch of the step kernel of the scenario's mode (fused components / general graph).
+static int launch_step(const pd::DevArgs& a, int t, int n, int it0, int it1, int flags, hipStream_t s) {
+  return a.graph ? pd::launch_graph_step(a, t, n, it0, it1, flags, s) : pd::launch_mpc_step(a, t, n, it0, it1, flags, s);
+}
+
 // MPC steps t .. t+n-1 (n <= step_cap).  Per-component termination, or fixed iterations
 // under term_global: ONE persistent launch for all n steps (each workgroup runs its
 // component's steps back to back), plus, under term_global, the component-summed residual
@@ -362,11 +464,11 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
   hipStream_t s = h->stream;
   const int M = c.max_outer;
   if (!c.term_global) {
-    LAUNCH(h, pd::launch_mpc_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST, s));
+    LAUNCH(h, launch_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST, s));
     return PIADMM_OK;
   }
   if (c.fixed_iters) {
-    LAUNCH(h, pd::launch_mpc_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL, s));
+    LAUNCH(h, launch_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL, s));
     LAUNCH(h, pd::launch_resid_history(h->a, n, h->d_part, s));
     if (h->comm)
       NCCLCHK(h, ncclAllReduce(h->d_part, h->d_part, (size_t)n * 2 * M, ncclDouble, ncclSum, h->comm, s));
@@ -380,7 +482,7 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
     return PIADMM_OK;
   }
   if (h->coop && !h->comm &&
-      pd::launch_mpc_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL | pd::F_COOP, s) != 0) {
+      launch_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL | pd::F_COOP, s) != 0) {
     (void)hipGetLastError();       // the cooperative launch was refused: host-decided path from now on
     h->coop = false;
   }
@@ -402,9 +504,9 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
     h->ghist.assign((size_t)2 * M, NAN);
     int flag = 0, nit = 0, nanlast = 0;
     for (int it = 0; it < M; ++it) {
-      LAUNCH(h, pd::launch_mpc_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
+      LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
       double* part = h->d_part + (size_t)5 * it;
-      LAUNCH(h, pd::launch_term_partials(h->a, it, part, s));
+      LAUNCH(h, h->a.graph ? pd::launch_graph_partials(h->a, part, s) : pd::launch_term_partials(h->a, it, part, s));
       if (h->comm) NCCLCHK(h, ncclAllReduce(part, part, 5, ncclDouble, ncclSum, h->comm, s));
       HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
       HIPCHK(h, hipStreamSynchronize(s));
@@ -422,7 +524,7 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
       if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok)) break;
     }
     h->giters = nit;
-    LAUNCH(h, pd::launch_mpc_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
+    LAUNCH(h, launch_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
   }
   return PIADMM_OK;
 }

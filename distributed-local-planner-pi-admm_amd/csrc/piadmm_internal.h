@@ -78,6 +78,28 @@ struct DevArgs {
   double* gpart;            // 2*C*5 coop: per-component termination partials (iteration parity)
   double* ghist;            // step_cap*max_outer*2 coop: global (rk, sk) history per step
   int* giters;              // step_cap coop: global outer iterations per step
+  // ---- graph mode (k_graph_step): any static candidate graph (components of any size, agents
+  // in several pairs).  All per-QP state lives in HBM between the phases of an outer iteration.
+  int graph;                // 1: the scenario runs on k_graph_step
+  const int* nbr_ptr;       // N+1 CSR: incident candidate pairs of agent a, sorted by neighbour id
+  const int* nbr_edge;      // 2E  pair index
+  const int* nbr_dir;       // 2E  0: a is v1 of the pair (owns hat_{v1 v2}), 1: a is v2
+  const int* comp_aptr;     // C+1 agents of component c: comp_alist[comp_aptr[c] .. comp_aptr[c+1])
+  const int* comp_alist;    // N   (increasing agent index)
+  const int* comp_eptr;     // C+1 pairs of component c: comp_elist[comp_eptr[c] .. comp_eptr[c+1])
+  const int* comp_elist;    // E   (increasing pair index: the residual sum order, casadi/main.py:165-173)
+  const unsigned char* owned;   // N   1: this rank solves the agent's x-step (0: ghost of another rank)
+  const unsigned char* counted; // E   1: this rank counts the pair's residual (cross-rank pairs: one rank)
+  const int* xslot;         // N   slot of a boundary agent in the exchange buffer (-1: none)
+  double* xbuf;             // n_slots * (2(H+1) + H): owner-written positions | controls (all-reduced)
+  int n_slots;
+  double* seed_g;           // N*2 seeds of the current MPC step (casadi/main.py:48-49)
+  double* eres;             // E*2 (rk_e, sk_e) of the pair's last z-step
+  double* cpart;            // C*5 termination partials of the component's last iteration
+  int* csig_x;              // N*WAVE per-lane signature of the agent's cached x-step tables (-1: none)
+  int* xflags;              // N   bit 0: the x-step QP holds a warm state
+  int* eflags;              // E   bit 0: the pair QP holds a warm state
+  int ke_stride;            // doubles per pair in Ke_g (graph mode: room for 64 dual active-set columns)
 };
 
 // Big mode: rows of the per-wave x-step factor scratch (working sets of up to H + 2 rows:
@@ -128,6 +150,22 @@ constexpr int F_GLOBAL = 4;   // termination decided outside (term_global): no p
 constexpr int F_NANLAST = 8;  // the global loop stopped at the collision test of iteration it0-1
 constexpr int F_COOP = 16;    // global termination decided in-kernel (cooperative launch, one rank)
 
+// Graph mode: LDS per workgroup of k_graph_step (GW waves, one component per workgroup).
+constexpr int GW = 2;
+inline size_t graph_lds_bytes(int H) {
+  size_t fac = 64 * LD;                                   // pair factor scratch (largest)
+  const size_t xr = (size_t)xrows(H) * (xrows(H) + 1);    // x-step factor scratch (same region)
+  if (xr > fac) fac = xr;
+  return (GW * (fac + 512 + 256) + 64) * sizeof(double);  // + vectors, factor diagonals; scalars
+}
+// Graph launches also use these flags: F_XPHASE / F_ZPHASE restrict an iteration launch to
+// its x-step or its z-step + termination half (the exchange of a sharded job sits between).
+constexpr int F_XONLY = 32;
+constexpr int F_ZONLY = 64;
+
+int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
+bool graph_coop_fits(const DevArgs& a, int device);
+int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s);
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s);
 int launch_resid_history(const DevArgs& a, int nsteps, double* out, hipStream_t s);

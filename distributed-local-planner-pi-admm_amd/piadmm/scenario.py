@@ -133,8 +133,66 @@ def tiled(n_tiles: int, H: int, n_steps: int | None = None, perturb: bool = True
     return Scenario(spd=spd, xt0=xt0, ref=ref, edges=edges, n_steps=base.n_steps)
 
 
+# Approach lanes of the N-vehicle crossing: (x0, y0, theta0, speed, x_end, y_end) over Nt = 5 s.
+# Lanes 0 and 1 are the reference's two vehicles (casadi/PI_ADMM_class.py:21,31-37); lanes 2
+# and 3 enter from the east and the south, offset so that the four paths cross pairwise.
+_LANES = (
+    (-10.0, 0.0, 0.0, 4.0, 10.0, 0.0),
+    (0.0, 20.0, -np.pi / 2, 8.0, 0.0, -20.0),
+    (12.0, 1.5, np.pi, 5.0, -13.0, 1.5),
+    (-1.5, -14.0, np.pi / 2, 6.0, -1.5, 16.0),
+)
+
+
+def crossing(n_vehicles: int, H: int, n_steps: int | None = None, pairs: str = "all",
+             Nt: float = 5.0, dt: float = 0.1, seed: int | None = None) -> Scenario:
+    """An ``n_vehicles`` crossing: the reference's ``num_veh`` loop beyond two vehicles
+    (``casadi/main.py:81,110-113``: every agent's AL sum and collision test over the others).
+
+    Vehicle k drives lane k % 4 of :data:`_LANES` (lanes 0, 1 = the reference's A and B), shifted
+    3 m sideways per full round of lanes.  ``pairs``: ``"all"`` -- every pair i < j is a
+    candidate (the reference's all-pairs semantics, quirk B8); ``"chain"`` -- pairs (k, k+1) only.
+    ``seed`` perturbs the start states like :func:`tiled`."""
+    n_ref = int(Nt / dt)
+    if n_steps is None:
+        n_steps = max(int(Nt / dt - H), 0)
+    T = max(n_ref, n_steps + H)
+    spd = np.empty(n_vehicles)
+    xt0 = np.empty((n_vehicles, 3))
+    ref = np.zeros((n_vehicles, 2, T))
+    for k in range(n_vehicles):
+        x0, y0, th, v, x1, y1 = _LANES[k % 4]
+        off = 3.0 * (k // 4)
+        sx, sy = (0.0, off) if abs(np.cos(th)) > 0.5 else (off, 0.0)
+        spd[k] = v
+        xt0[k] = (x0 + sx, y0 + sy, th)
+        ref[k, 0] = _ref_line(x0 + sx, x1 + sx, n_ref, T)
+        ref[k, 1] = _ref_line(y0 + sy, y1 + sy, n_ref, T)
+    if seed is not None:
+        rng = np.random.default_rng(seed)
+        xt0 += rng.uniform(-1.0, 1.0, size=xt0.shape) * np.array([0.5, 0.5, 0.05])
+    if pairs == "all":
+        edges = [(i, j) for i in range(n_vehicles) for j in range(i + 1, n_vehicles)]
+    elif pairs == "chain":
+        edges = [(i, i + 1) for i in range(n_vehicles - 1)]
+    else:
+        raise ValueError("pairs must be 'all' or 'chain'")
+    return Scenario(spd=spd, xt0=xt0, ref=ref, edges=np.asarray(edges, np.int32).reshape(-1, 2), n_steps=n_steps)
+
+
+def concat(scenarios) -> Scenario:
+    """Independent copies side by side (agents renumbered, candidate pairs kept per copy)."""
+    offs = np.cumsum([0] + [s.n_agents for s in scenarios])
+    T = min(s.ref.shape[2] for s in scenarios)
+    return Scenario(spd=np.concatenate([s.spd for s in scenarios]),
+                    xt0=np.concatenate([s.xt0 for s in scenarios]),
+                    ref=np.concatenate([s.ref[:, :, :T] for s in scenarios]),
+                    edges=np.concatenate([s.edges + o for s, o in zip(scenarios, offs)]).astype(np.int32),
+                    n_steps=min(s.n_steps for s in scenarios))
+
+
 def n_steps_for(H: int, Nt: float = 5.0, dt: float = 0.1) -> int:
     return max(int(Nt / dt - H), 0)
 
 
-__all__ = ["Scenario", "intersection", "tiled", "n_steps_for"]
+__all__ = ["Scenario", "intersection", "tiled", "crossing", "concat", "n_steps_for"]

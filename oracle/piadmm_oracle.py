@@ -20,14 +20,20 @@ What it restates (all paths relative to the reference root):
   * residuals       ``casadi/main.py:164-181`` (MATLAB ``:191-210``)
   * MPC propagation ``casadi/main.py:185-192``, seeds ``:48-49``
 
+Pinned bit for bit to the reference's own statements, executed (tests/test_oracle.py):
+the rollouts (``oracle/gen_ref_rollouts.py`` -> ``tests/golden/ref_rollouts.npz``) and the
+loop's NumPy statements -- seeds, collision test, pair hat rollout, plain dual update, residual
+sums, propagation (``oracle/gen_ref_mainloop.py`` -> ``tests/golden/ref_mainloop.npz``).
+
 Parity pinning: the reference cannot run here (casadi, bunch and OSQP are
 absent) and its repository holds no tests, fixtures or outputs for
-this path.  The oracle is pinned (a) by executing the reference's own numeric
-rollout functions on seeded inputs (fixtures in tests/golden/, generated by
-oracle/gen_ref_rollouts.py from the reference source), and (b) by KKT
-certificates of every QP it solves (the reference's solver output is not
-available anywhere).  The QP assembly and the outer-loop logic are therefore
-"parity unpinned" against reference *outputs*; see DESIGN.md.
+this path.  The oracle is pinned (a) by executing the reference's own NumPy code
+on seeded inputs -- the numeric rollouts (oracle/gen_ref_rollouts.py) and every
+non-solver statement of the casadi/main.py loop (oracle/gen_ref_mainloop.py), bit
+for bit -- and (b) by KKT certificates of every QP it solves (the reference's
+solver output is not available anywhere).  What stays "parity unpinned" against
+reference outputs: the QP assembly (cost_function_primal / _edge need CasADi) and
+the MATLAB PI update (MATLAB is absent); see DESIGN.md section 3.
 
 Generalisation from the reference's two vehicles to N agents:
 static candidate pairs (the AL sum runs over candidate neighbours, B8),
@@ -239,6 +245,31 @@ def safety_distance(cfg, xt, spd, v1, v2):
     return cfg.dis_thres + np.hypot(*delay_offset(cfg, xt[v1], spd[v1])) + np.hypot(*delay_offset(cfg, xt[v2], spd[v2]))
 
 
+def collides(cfg, p1, p2, d_eff):
+    """Collision test of one candidate pair (``casadi/main.py:110-113``): any horizon point with
+    d^2 below the threshold (Python compares d^2 with the unsquared dis_thres, quirk B2)."""
+    d2 = np.square(p1[0] - p2[0]) + np.square(p1[1] - p2[1])
+    return bool(np.max(d2 < cfg.collide_thr(d_eff)))
+
+
+def pair_residuals(cfg, p_v1, hat_v1v2, last_v1v2):
+    """One pair's terms of ``casadi/main.py:170-173`` (the v1 side only, times 2, quirk B5):
+    (primal, dual) = (2 |p_v1 - hat_v1v2|_F, 2 |rho (last_hat_v1v2 - hat_v1v2)|_F)."""
+    sk = 2 * np.sqrt(np.sum((cfg.rho * (last_v1v2 - hat_v1v2)) ** 2))
+    rk = 2 * np.sqrt(np.sum((p_v1 - hat_v1v2) ** 2))
+    return rk, sk
+
+
+def propagate(cfg, xt, u, spd):
+    """MPC propagation (``casadi/main.py:185-192``): every agent's state one step along the
+    nonlinear rollout of its plan."""
+    new_xt = np.array(xt, np.float64, copy=True)
+    for i in range(new_xt.shape[0]):
+        x, y, th = rollout_nonlinear(xt[i], u[i], spd[i], cfg.dt, cfg.L)
+        new_xt[i] = (x[1], y[1], th[1])
+    return new_xt
+
+
 def shift_horizon(a):
     """Receding-horizon shift along the last axis: drop slot 0, duplicate the last slot
     (``iterate_next_state``, ``decentralized/optimizer.py:337-344``)."""
@@ -347,8 +378,7 @@ class Oracle:
                 # ---- collision graph, casadi/main.py:110-118
                 for e in edges:
                     v1, v2 = self.scn.edges[e]
-                    d2 = np.square(pos_old[v1, 0] - pos_old[v2, 0]) + np.square(pos_old[v1, 1] - pos_old[v2, 1])
-                    active[e] = bool(np.max(d2 < cfg.collide_thr(d_eff[e])))
+                    active[e] = collides(cfg, pos_old[v1], pos_old[v2], d_eff[e])
                 act = [e for e in edges if active[e]]
                 # ---- z-step + dual update, casadi/main.py:121-162 (none when no pair is active)
                 for e in act:
@@ -371,10 +401,10 @@ class Oracle:
                     for e in self.comp_edges[c]:
                         if not active[e]:
                             continue
-                        v1 = int(self.scn.edges[e, 0])
+                        rk_e, sk_e = pair_residuals(cfg, pos_old[int(self.scn.edges[e, 0])], hat[e, 0], last_hat[e, 0])
                         if not g_alias[g]:
-                            sk += 2 * np.sqrt(np.sum((cfg.rho * (last_hat[e, 0] - hat[e, 0])) ** 2))
-                        rk += 2 * np.sqrt(np.sum((pos_old[v1] - hat[e, 0]) ** 2))
+                            sk += sk_e
+                        rk += rk_e
                     comp_r.append((rk, sk))
                 seen = [e for e in edges if np.isfinite(dis_chk[e])]
                 part = np.array([sum(r for r, _ in comp_r), sum(q for _, q in comp_r), float(len(act)),
@@ -403,10 +433,8 @@ class Oracle:
         self.edge_state = (hat.copy(), lam.copy(), S.copy(), D.copy(), last_hat.copy())
         # ---- propagation, casadi/main.py:185-192 (of the components that ran)
         new_xt = self.xt.copy()
-        prop = range(N) if components is None else np.concatenate([self.comp_agents[ci] for ci in comps])
-        for i in prop:
-            x, y, th = rollout_nonlinear(self.xt[i], self.primal_u[i], self.scn.spd[i], cfg.dt, cfg.L)
-            new_xt[i] = (x[1], y[1], th[1])
+        prop = np.arange(N) if components is None else np.concatenate([self.comp_agents[ci] for ci in comps])
+        new_xt[prop] = propagate(cfg, self.xt[prop], self.primal_u[prop], self.scn.spd[prop])
         self.xt = new_xt
         self.t += 1
         return StepRecord(xt=new_xt.copy(), u=self.primal_u.copy(), iters=iters, resid=resid,

@@ -1,0 +1,142 @@
+"""GPU parity of graph mode (csrc/piadmm_graph.hip) through the C-ABI: candidate graphs beyond
+disjoint two-vehicle pairs -- the reference's ``num_veh`` loop with every pair a candidate
+(casadi/main.py:81,110-113; PI_ADMM_class.py:126-129), chains, several components of
+different shapes, and the tiled benchmark forced onto the graph kernel (PIADMM_GRAPH=1),
+which must agree with the fused kernel.  Tolerance as in test_gpu_parity.py (held 1e-8,
+contract 1e-5), identical outer-iteration counts and residual histories."""
+import numpy as np
+import pytest
+
+from oracle import piadmm_oracle as O
+from piadmm import config, scenario
+
+pytestmark = pytest.mark.gpu
+RTOL = ATOL = 1e-8
+
+
+@pytest.fixture(scope="module")
+def Solver():
+    from piadmm.solver import PI_ADMM_MI355X, device_count
+    if device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests need an MI355X")
+    return PI_ADMM_MI355X
+
+
+def close(a, b, rtol=RTOL, atol=ATOL):
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol)
+
+
+def compare(Solver, cfg, scn, n_steps, setup=None):
+    orc = O.Oracle(cfg, scn)
+    with Solver(cfg, scn) as s:
+        if setup:
+            setup(s)
+        assert s.C == orc.n_comp
+        for k in range(n_steps):
+            ro, rg = orc.mpc_step(), s.mpc_step()
+            np.testing.assert_array_equal(rg.status, 0)
+            np.testing.assert_array_equal(rg.iters, ro.iters, err_msg=f"step {k}")
+            close(rg.xt, ro.xt)
+            close(rg.u, ro.u)
+            for c in range(s.C):
+                n = len(ro.resid[c])
+                if n:
+                    close(rg.resid[c, :n], np.array(ro.resid[c]), rtol=1e-7, atol=1e-7)
+                assert np.all(np.isnan(rg.resid[c, n:]))
+            if cfg.term_global:
+                n = len(ro.global_resid)
+                assert rg.global_iters == int(ro.iters[0])
+                if n:
+                    close(rg.global_resid[:n], np.array(ro.global_resid), rtol=1e-7, atol=1e-7)
+        st = s.state()
+    close(st["pos_old"], ro.pos_old)
+    close(st["hat"], ro.hat)
+    close(st["lam"], ro.lam)
+    np.testing.assert_array_equal(st["edge_active"].astype(bool), ro.edge_active)
+
+
+@pytest.mark.parametrize("preset", ["matlab_pi", "casadi_default"])
+@pytest.mark.parametrize("n", [3, 4])
+def test_all_pairs_crossing(Solver, preset, n):
+    """n vehicles, every pair a candidate: each agent's AL sum has n-1 terms, up to
+    n(n-1)/2 pair QPs per outer iteration (matlab_pi at n = 4 includes a step that runs all
+    100 outer iterations)."""
+    compare(Solver, config.PRESETS[preset](H=15), scenario.crossing(n, 15, n_steps=30), 24)
+
+
+def test_chain_graph(Solver):
+    """Six vehicles, candidate pairs (k, k+1): interior agents in two pairs."""
+    compare(Solver, config.matlab_pi(H=15), scenario.crossing(6, 15, n_steps=30, pairs="chain"), 24)
+
+
+@pytest.mark.parametrize("H", [10, 30, 40])
+def test_mixed_components_and_horizons(Solver, H):
+    """Components of 4 (all pairs), 3 (chain), 2 and 1 agents side by side, per-component
+    termination; H = 40 takes the two-columns-per-lane pair K path (big mode)."""
+    scn = scenario.concat([scenario.crossing(4, H, n_steps=14, seed=1), scenario.crossing(3, H, n_steps=14, pairs="chain"),
+                           scenario.intersection(H, n_steps=14), scenario.crossing(1, H, n_steps=14)])
+    compare(Solver, config.matlab_pi(H=H), scn, 8 if H > 32 else 12)
+
+
+@pytest.mark.parametrize("coop", [True, False])
+def test_graph_global_termination(Solver, coop, monkeypatch):
+    """The reference's global flag / stop over all agents (term_global): in-kernel behind a grid
+    barrier (cooperative launch) or host-decided (PIADMM_NO_COOP=1, one launch per iteration)."""
+    scn = scenario.concat([scenario.crossing(4, 15, n_steps=20, seed=2), scenario.crossing(3, 15, n_steps=20, seed=3)])
+    if not coop:
+        monkeypatch.setenv("PIADMM_NO_COOP", "1")
+    compare(Solver, config.matlab_pi(H=15, term_global=1), scn, 14)
+
+
+def test_graph_warm_duals_tightening_fixed(Solver):
+    """a12 (receding-horizon dual shift) and a13 (delay tightening) on a 4-vehicle all-pairs
+    crossing, and fixed iterations under the global scope."""
+    compare(Solver, config.matlab_pi(H=15, warm_duals=1, tighten=1), scenario.crossing(4, 15, n_steps=24, seed=4), 16)
+    compare(Solver, config.matlab_pi(H=12, fixed_iters=1, max_outer=8, term_global=1),
+            scenario.crossing(4, 12, n_steps=12, seed=5), 6)
+
+
+@pytest.mark.parametrize("H,fixed", [(12, 0), (30, 1), (40, 0)])
+def test_graph_kernel_equals_fused_kernel_on_tiles(Solver, H, fixed, monkeypatch):
+    """The tiled benchmark scenario forced onto the graph kernel gives the fused kernel's
+    states, iteration counts and residual histories (to rounding: the two kernels contract
+    multiply-adds differently)."""
+    cfg = config.matlab_pi(H=H, fixed_iters=fixed, max_outer=30 if fixed else 100)
+    scn = scenario.tiled(16, H, n_steps=10, seed=7)
+    with Solver(cfg, scn) as s1:
+        monkeypatch.setenv("PIADMM_GRAPH", "1")
+        s2 = Solver(cfg, scn)
+        monkeypatch.delenv("PIADMM_GRAPH")
+        try:
+            for _ in range(6):
+                r1, r2 = s1.mpc_step(), s2.mpc_step()
+                np.testing.assert_array_equal(r1.iters, r2.iters)
+                close(r2.xt, r1.xt, rtol=1e-10, atol=1e-10)
+                close(r2.u, r1.u, rtol=1e-10, atol=1e-10)
+                np.testing.assert_allclose(r2.resid, r1.resid, rtol=1e-9, atol=1e-9)
+                assert np.all(r2.status == 0)
+            c1, c2 = s1.counters(), s2.counters()
+            assert c1["x_qps"] == c2["x_qps"] and c1["z_qps"] == c2["z_qps"]
+        finally:
+            s2.close()
+
+
+def test_all_pairs_tiles_at_256_agents(Solver):
+    """64 copies of the 4-vehicle all-pairs crossing (256 agents, 384 candidate pairs, H = 30):
+    sampled components against the oracle, every QP certified."""
+    H = 30
+    tiles = [scenario.crossing(4, H, n_steps=6, seed=k) for k in range(64)]
+    scn = scenario.concat(tiles)
+    cfg = config.matlab_pi(H=H)
+    comps = [0, 31, 63]
+    orc = O.Oracle(cfg, scn)
+    with Solver(cfg, scn) as s:
+        assert s.N == 256 and s.C == 64
+        for _ in range(3):
+            ro, rg = orc.mpc_step(components=comps), s.mpc_step()
+            np.testing.assert_array_equal(rg.status, 0)
+            for c in comps:
+                sl = slice(4 * c, 4 * c + 4)
+                assert rg.iters[c] == ro.iters[c]
+                close(rg.xt[sl], ro.xt[sl])
+                close(rg.u[sl], ro.u[sl])

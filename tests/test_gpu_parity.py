@@ -295,8 +295,8 @@ def test_errors_are_loud(Solver):
     with pytest.raises(_lib.PiadmmError, match="H must be"):
         Solver(config.matlab_pi(H=64), scenario.tiled(1, 64, n_steps=1))
     bad = scenario.tiled(2, 10)
-    bad.edges = np.array([[0, 2]], np.int32)
-    with pytest.raises(_lib.PiadmmError, match="pair"):
+    bad.edges = np.array([[2, 0]], np.int32)
+    with pytest.raises(_lib.PiadmmError, match="edge must satisfy"):
         Solver(config.matlab_pi(H=10), bad)
     with Solver(config.matlab_pi(H=10), scenario.intersection(10)) as s:
         with pytest.raises(_lib.PiadmmError, match="time index"):

@@ -195,3 +195,55 @@ def test_empty_candidate_graph_terminates_after_one_iteration():
     scn.edges = np.zeros((0, 2), np.int32)
     r = O.Oracle(config.casadi_default(H=10), scn).mpc_step()
     assert list(r.iters) == [1, 1]
+
+
+# ---------------------------------------------------------------------------------------------
+# The casadi/main.py loop's own NumPy statements, executed (oracle/gen_ref_mainloop.py):
+# the oracle's seeds, collision test, pair hat rollout, plain dual update, residual sums and
+# propagation must reproduce them bit for bit.
+def _mainloop_cases():
+    d = np.load(os.path.join(GOLD, "ref_mainloop.npz"), allow_pickle=False)
+    for k in range(int(d["n_cases"])):
+        yield {name[len(f"c{k}_"):]: d[name] for name in d.files if name.startswith(f"c{k}_")}
+
+
+def test_mainloop_statements_bit_exact():
+    n = 0
+    for c in _mainloop_cases():
+        N, H = int(c["N"]), int(c["H"])
+        cfg = config.casadi_default(H=H, rho=2.0)
+        spd = c["spd"]
+        # seeds, casadi/main.py:48-49
+        scn = scenario.Scenario(spd=spd, xt0=c["xt"], ref=np.zeros((N, 2, H + 1)),
+                                edges=np.zeros((0, 2), np.int32), n_steps=1)
+        np.testing.assert_array_equal(O.Oracle(cfg, scn).seeds(), c["seeds"])
+        # collision test over all pairs i < j, :110-113 (edge list in np.where order, :121)
+        pos = c["pos_old"].reshape(N, 2, H + 1)
+        hits = [(i, j) for i in range(N) for j in range(i + 1, N) if O.collides(cfg, pos[i], pos[j], cfg.dis_thres)]
+        assert hits == list(zip(c["edge_row"].tolist(), c["edge_col"].tolist()))
+        for i in range(N):
+            for j in range(i + 1, N):
+                assert float(O.collides(cfg, pos[i], pos[j], cfg.dis_thres)) == c["edge_mat"][i, j]
+        # hat rollouts (:156-158) and plain dual updates (:161-162), edge by edge
+        hat, lam, last = c["hat_in"].copy(), c["dual_in"].copy(), c["last_in"]
+        for k, (v1, v2) in enumerate(hits):
+            for d, v in enumerate((v1, v2)):
+                hx, hy, _ = O.rollout_nonlinear(c["xt"][v], c["uh"][k][d], spd[v], cfg.dt, cfg.L)
+                (hat[v1, v2] if d == 0 else hat[v2, v1])[:] = (hx, hy)
+            hat_e = np.stack([hat[v1, v2], hat[v2, v1]])
+            lam_e = np.stack([lam[v1, v2], lam[v2, v1]])
+            O.dual_update(cfg, pos[v1], pos[v2], hat_e, lam_e, np.zeros_like(lam_e), np.zeros_like(lam_e), None)
+            lam[v1, v2], lam[v2, v1] = lam_e
+        np.testing.assert_array_equal(hat, c["hat_out"])
+        np.testing.assert_array_equal(lam, c["dual_out"])
+        # residual sums, :165-173 (edge-list order)
+        rk = sk = 0.0
+        for v1, v2 in hits:
+            r, q = O.pair_residuals(cfg, pos[v1], hat[v1, v2], last[v1, v2])
+            sk += q
+            rk += r
+        assert rk == c["error_rk"] and sk == c["error_sk"]
+        # propagation, :185-192
+        np.testing.assert_array_equal(O.propagate(cfg, c["xt"], c["primal_u"], spd), c["xt_next"])
+        n += 1
+    assert n == 20
