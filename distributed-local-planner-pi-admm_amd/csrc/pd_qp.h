@@ -1103,7 +1103,7 @@ __device__ __forceinline__ void pinv_row(const QP<NV>& P, int row, double sg, do
   }
 }
 
-constexpr int GI_MAX_STEPS = 256;
+constexpr int GI_MAX_STEPS = 1024;   // a cold pair QP at H = 30 with most rows active takes ~300 adds + drops
 constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t, codes
 // Warm start (receding horizon): the previous MPC step's final active set, shifted one time
 // slot (tools/gi_sim.py + the warm-start prototype: 28 -> 3.6 GI steps per bench pair QP),
@@ -1132,13 +1132,15 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   double x0[NV], xc[NV];
   int m = 0, wbits = 0;
   double ua = 0.0, linv = 0.0;     // lane a < m: multiplier and 1/L_aa of active constraint a
-  // Pair: hinge rows fixed in their linear regime (this lane's hinge row).  A hinge whose
-  // multiplier saturates at its cap beta is linear at the optimum, which the dual active set
-  // does not model: GI restarts with that row linear -- its term beta (h - a'x) moves into q
-  // (as in reduced_solve) and the row leaves the constraint search -- warm-started from the
-  // active set it had reached.  The final KKT test checks the linear rows (a'x <= h).
+  // Pair: hinge rows in their linear regime (this lane's hinge row).  A hinge row's multiplier
+  // is bounded, u in [0, beta] (dual of beta max(0, h - a'x)): when a step takes it to beta the
+  // row turns linear -- its term beta (h - a'x) moves into q, i.e. x0 += beta P^-1 n, and the
+  // row leaves the active set -- and the search then watches the other side of the kink
+  // (a'x <= h, normal -a, multiplier v = beta - u): an active upper side whose v reaches beta
+  // turns the row back to its zero regime (x0 += beta P^-1 n again).  Both events keep the
+  // iterate stationary and dual feasible, so the dual active set continues in place (a bounded
+  // dual method): no restart, no cycling between the regimes.
   bool lin = false;
-  int rcode = -1, rm = 0;
   auto start = [&]() {
     double qt[NV];
 #pragma unroll
@@ -1255,7 +1257,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     if (l < m) {
       const int myc = wc[l], rw = myc >> 1, rs = rw / H;
       // upper side (box / rate rows only, uniform bounds): -(a'x0 - hi)
-      const double blo = (rs & 1) ? -P.dumax : -P.umax;
+      const double blo = P.hinge(rs) ? 0.0 : ((rs & 1) ? -P.dumax : -P.umax);   // hinge: hi = lo = h
       rhs = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
     }
     return tri_bwd(L, ld, linv, tri_fwd(L, ld, linv, rhs, m), m);
@@ -1272,16 +1274,14 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   };
 
   // On failure (flab != nullptr): the current working set as PDAS labels -- a start for the
-  // polish instead of ADMM.  A hinge row whose multiplier reached the cap beta (row id hrow,
-  // lane-uniform; -1: none) is in its linear regime there: label HLINEAR.
-  auto fail_labels = [&](int hrow) {
+  // polish instead of ADMM (a linear hinge row: HLINEAR, or HKINK with its upper side active).
+  auto fail_labels = [&]() {
     if (!flab) return;
 #pragma unroll
     for (int s = 0; s < NR; ++s) {
       const bool lo_in = (wbits >> (2 * s)) & 1, hi_in = (wbits >> (2 * s + 1)) & 1;
-      if (P.hinge(s)) flab[s] = lo_in ? HKINK : HZERO;
+      if (P.hinge(s)) flab[s] = (lo_in || hi_in) ? HKINK : (lin ? HLINEAR : HZERO);
       else flab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
-      if (P.hinge(s) && (lin || hrow == s * H + l)) flab[s] = HLINEAR;
       if (!P.valid(s)) flab[s] = 0;
     }
   };
@@ -1295,20 +1295,10 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     const double lpp2 = spp - wsum(w * w);
     if (lpp2 > DEP_TOL * spp) append(pc, yp, w, lpp2, 0.0);
   };
-  constexpr int GI_LIN_ROUNDS = WAVE;   // every hinge row may end linear
-  for (int round = 0;; ++round) {
   start();
   bool warm = false;
-  bool again = false;
   unsigned long long t_wb = STAMP_T();
-  if (round > 0) {
-    // ---- restart: the previous round's active set without the saturated hinge row
-    for (int i = 0; i < rm; ++i) {
-      const int pc = rdli(rcode, i);
-      if (pc >= 0) warm_add(pc);
-    }
-    warm = true;
-  } else if (P.gws) {
+  if (P.gws) {
     // ---- pair: the stored active set (this step's, or the previous step's shifted)
     const int gm = P.gws[0], gt = P.gws[1];
     const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
@@ -1319,6 +1309,9 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
         const bool keep = P.hinge(s0) ? (k >= 2) : (k >= 1);
         code = keep ? 2 * (row - 1) + (code & 1) : -1;
       }
+      // a kink held from its upper side (a linear row) restarts as the lower side (regimes
+      // start at zero; both sides are the same equality a'x = h)
+      if (code >= 0 && P.hinge((code >> 1) / H)) code &= ~1;
       if (NV == 2 && P.g1 == 0.0 && P.g2 == 0.0 && code >= 0 && P.hinge((code >> 1) / H)) code = -1;
       for (int i = 0; i < gm; ++i) {
         const int pc = rdli(code, i);
@@ -1377,14 +1370,14 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
 #pragma unroll
     for (int s = 0; s < NR; ++s) {
       if (!P.valid(s)) continue;
-      if (P.hinge(s) && lin) continue;          // fixed linear (see start)
+      const bool hl = P.hinge(s) && lin;        // linear hinge row: only its upper side a'x <= h
       const double tp = P.tol * (1.0 + fabs(P.lo(s)));
-      if (!((wbits >> (2 * s)) & 1)) {
+      if (!hl && !((wbits >> (2 * s)) & 1)) {
         const double sv = ax[s] - P.lo(s);
         if (sv < -tp && sv < best) { best = sv; code = 2 * (s * H + l); }
       }
-      if (!P.hinge(s) && !((wbits >> (2 * s + 1)) & 1)) {
-        const double sv = P.hi(s) - ax[s];
+      if ((hl || !P.hinge(s)) && !((wbits >> (2 * s + 1)) & 1)) {
+        const double sv = (hl ? P.lo(s) : P.hi(s)) - ax[s];
         if (sv < -tp && sv < best) { best = sv; code = 2 * (s * H + l) + 1; }
       }
     }
@@ -1394,15 +1387,15 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     const int pc = rdli(code, pl);
     const int prow = pc >> 1, pside = pc & 1, ps = prow / H, pk = prow - ps * H;
     const bool phinge = P.hinge(ps);
-    double sp = rdl(pside ? P.hi(ps) - ax[ps] : ax[ps] - P.lo(ps), pk);   // slack of p (< 0)
+    double sp = rdl(pside ? (phinge ? P.lo(ps) : P.hi(ps)) - ax[ps] : ax[ps] - P.lo(ps), pk);   // slack of p (< 0)
     double yp[NV];
     const double spp = prep(pc, yp);       // n_p' P^-1 n_p
     double up = 0.0;
     STAMP_ADD(ST_GI_SEARCH, t_gs);
     while (true) {
       if (++nsteps > GI_MAX_STEPS) {
-        GI_DBG("GI fail: step limit m=%d round=%d\n", m, round);
-        fail_labels(-1);
+        GI_DBG("GI fail: step limit m=%d\n", m);
+        fail_labels();
         return false;
       }
       unsigned long long t_gv = STAMP_T();
@@ -1441,29 +1434,40 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       const double t1 = wmin(tdrop);
       const double tc = fmin(wmin(tcap), phinge ? P.beta - up : INFINITY);
       const double t = fmin(t1, t2);
-      if (tc <= t) {                                 // a hinge multiplier saturates at beta
+      if (tc <= t) {
+        // a hinge multiplier reaches its bound beta: step there, then the row changes regime
+        // (lower side -> linear, upper side -> zero) and its constraint leaves the active set
         const double tca = wmin(tcap);
-        int hrow;
-        if (phinge && P.beta - up <= tca) {
-          hrow = prow;                               // the entering hinge row
-        } else {
-          const int k = __ffsll((unsigned long long)__ballot(l < m && hin_a && tcap == tca)) - 1;
-          hrow = rdli(myc, k) >> 1;
+        const bool entering = phinge && P.beta - up <= tca;
+        if (t2 < INFINITY) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) xc[v] += tc * z[v];
+          sp += tc * lpp2;
         }
-        if (NV == 2 && round < GI_LIN_ROUNDS && hrow / H == 4) {
-          if (l == hrow - 4 * H) lin = true;
-          rcode = (l < m && (wc[l] >> 1) != hrow) ? wc[l] : -1;
-          rm = m;
-          again = true;
-          break;
+        if (l < m) ua -= tc * r;
+        up += tc;
+        if (entering) {
+          if (l == pk) lin = pside == 0;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) x0[v] += P.beta * yp[v];
+          STAMP_ADD(ST_GI_UPD, t_gu);
+          break;                                     // p never enters: next search
         }
-        GI_DBG("GI fail: hinge cap hrow=%d m=%d round=%d\n", hrow, m, round);
-        fail_labels(hrow);
-        return false;
+        const int k = __ffsll((unsigned long long)__ballot(l < m && hin_a && tcap == tca)) - 1;
+        const int kc = rdli(myc, k), krow = kc >> 1;
+        if (l == krow - (NV == 2 ? 4 : 0) * H) lin = (kc & 1) == 0;
+        {
+          const int lc = (l < H) ? l : 0;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) x0[v] += P.beta * Y[k * H2 + v * H + lc];
+        }
+        drop(k);
+        STAMP_ADD(ST_GI_UPD, t_gu);
+        continue;                                    // the same p, a new step direction
       }
       if (!(t < INFINITY)) {                         // unbounded dual step
-        GI_DBG("GI fail: unbounded dual step m=%d round=%d lpp2=%g spp=%g sp=%g\n", m, round, lpp2, spp, sp);
-        fail_labels(-1);
+        GI_DBG("GI fail: unbounded dual step m=%d lpp2=%g spp=%g sp=%g\n", m, lpp2, spp, sp);
+        fail_labels();
         return false;
       }
       if (t2 < INFINITY) {
@@ -1475,8 +1479,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       up += t;
       if (t2 <= t1) {
         if (m >= cap) {
-          GI_DBG("GI fail: full m=%d cap=%d round=%d\n", m, cap, round);
-          fail_labels(-1);
+          GI_DBG("GI fail: full m=%d cap=%d\n", m, cap);
+          fail_labels();
           return false;
         }
         append(pc, yp, w, lpp2, up);
@@ -1486,10 +1490,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       drop(__ffsll((unsigned long long)__ballot(l < m && tdrop == t1)) - 1);
       STAMP_ADD(ST_GI_UPD, t_gu);
     }
-    if (again) break;
   }
-  if (!again) break;
-  }   // rounds
   // ---- exact solution of the final active set (the reduced solve with this factor):
   // lam = S^-1 (N x0 - b), x = x0 - Y lam;  kernel multipliers y_a = sign_a * lam_a
   {
@@ -1511,8 +1512,9 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     for (int s = 0; s < NR; ++s) {
       const bool lo_in = (wbits >> (2 * s)) & 1, hi_in = (wbits >> (2 * s + 1)) & 1;
       y[s] = (P.valid(s) && l < H && (lo_in || hi_in)) ? vb_ax[s * H + l] : 0.0;
-      if (P.hinge(s) && lin && P.valid(s)) y[s] = -P.beta;
-      if (P.hinge(s)) lab[s] = lin ? HLINEAR : (lo_in ? HKINK : HZERO);
+      // linear hinge row: multiplier -beta, or -(beta - v) at a kink held from the upper side
+      if (P.hinge(s) && lin && P.valid(s)) y[s] = hi_in ? y[s] - P.beta : -P.beta;
+      if (P.hinge(s)) lab[s] = (lo_in || hi_in) ? HKINK : (lin ? HLINEAR : HZERO);
       else lab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
       if (!P.valid(s)) lab[s] = 0;
     }
@@ -1651,6 +1653,18 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       if (gi_solve(P, nullptr, glab, x, y, ngi, clab)) {
         signed char nl[NR];
         ok = kkt_check(P, glab, x, y, nl);
+#ifdef PIADMM_GI_DEBUG
+        GI_DBG("GI done steps=%d kkt=%d\n", ngi, (int)ok);
+        if (!ok) {
+          double axd[NR];
+          A_mul(P, x, axd);
+#pragma unroll
+          for (int s = 0; s < NR; ++s)
+            if (P.valid(s) && nl[s] != glab[s])
+              printf("  kkt viol slot %d lane %d lab %d -> %d ax %.12g lo %.12g hi %.12g y %.12g\n", s, lid(),
+                     (int)glab[s], (int)nl[s], axd[s], P.lo(s), P.hi(s), y[s]);
+        }
+#endif
 #pragma unroll
         for (int s = 0; s < NR; ++s) lab[s] = glab[s];
         if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);

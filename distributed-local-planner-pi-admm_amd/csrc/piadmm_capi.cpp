@@ -38,6 +38,17 @@ struct piadmm_ctx {
   bool coop = false;             // term_global natural termination decided in-kernel (one rank)
   std::vector<double> rho_init;  // host staging of the initial ADMM penalties (outlives the async copy)
   std::vector<std::vector<int>> graph_host;   // graph-mode index arrays (host staging)
+  std::vector<unsigned char> shard_host;      // owned | counted (host staging)
+  // sharded graph (piadmm_set_scenario_shard): ghost agents fed by one all-reduce of the
+  // boundary exchange buffer per outer iteration
+  bool xchg = false;
+  int n_slots = 0;
+  double* d_xrecv = nullptr;
+  // host all-reduce transport (piadmm_set_allreduce): used when there is no RCCL communicator
+  piadmm_allreduce_fn xfn = nullptr;
+  void* xctx = nullptr;
+  double* h_x = nullptr;         // pinned staging of the host transport
+  size_t h_x_n = 0;
 };
 
 namespace {
@@ -106,6 +117,35 @@ int reset_penalties(piadmm_ctx* h) {
   return 0;
 }
 
+// Sum over the job's ranks of n doubles at send into recv (may alias), on the handle's stream:
+// ncclAllReduce over the RCCL communicator, else the host transport callback (through pinned
+// memory; the callback returns when every rank has contributed), else one rank: a copy.
+int allreduce(piadmm_ctx* h, const double* send, double* recv, size_t n) {
+  if (n == 0) return 0;
+  if (h->comm) {
+    ncclResult_t r = ncclAllReduce(send, recv, n, ncclDouble, ncclSum, h->comm, h->stream);
+    if (r != ncclSuccess) return fail(h, PIADMM_E_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    return 0;
+  }
+  if (h->xfn) {
+    if (n > h->h_x_n) {
+      if (h->h_x) (void)hipHostFree(h->h_x);
+      h->h_x = nullptr;
+      h->h_x_n = 0;
+      HIPCHK(h, hipHostMalloc((void**)&h->h_x, n * sizeof(double)));
+      h->h_x_n = n;
+    }
+    HIPCHK(h, hipMemcpyAsync(h->h_x, send, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (int rc = h->xfn(h->xctx, h->h_x, (int64_t)n))
+      return fail(h, PIADMM_E_STATE, "all-reduce callback failed with " + std::to_string(rc));
+    HIPCHK(h, hipMemcpyAsync(recv, h->h_x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    return 0;
+  }
+  if (send != recv) HIPCHK(h, hipMemcpyAsync(recv, send, n * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -167,6 +207,7 @@ int32_t piadmm_destroy(piadmm_handle_t h) {
   free_all(h);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   if (h->h_part) (void)hipHostFree(h->h_part);
+  if (h->h_x) (void)hipHostFree(h->h_x);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -174,8 +215,9 @@ int32_t piadmm_destroy(piadmm_handle_t h) {
   return PIADMM_OK;
 }
 
-int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* xt0, const double* ref,
-                            int32_t T, const int32_t* edges, int32_t n_edges) {
+static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const double* xt0, const double* ref,
+                                 int32_t T, const int32_t* edges, int32_t n_edges, const uint8_t* owned,
+                                 const int32_t* slot, int32_t n_slots, const uint8_t* counted) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!spd || !xt0 || !ref || (n_edges > 0 && !edges)) return fail(h, PIADMM_E_ARG, "null array");
   const int N = h->cfg.n_agents, H = h->cfg.H;
@@ -198,6 +240,28 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   {
     const char* g = std::getenv("PIADMM_GRAPH");
     if (g && g[0] == '1') simple = false;
+  }
+  // a sharded job with a boundary exchange runs on the graph kernel (its X / Z phases are
+  // split launches around the all-reduce)
+  const bool sharded = owned != nullptr;
+  if (sharded) {
+    if (!slot || !counted || n_slots < 0) return fail(h, PIADMM_E_ARG, "shard: null array or n_slots < 0");
+    bool ghosts = false;
+    for (int i = 0; i < N; ++i) {
+      if (owned[i] > 1 || slot[i] < -1 || slot[i] >= n_slots)
+        return fail(h, PIADMM_E_ARG, "shard: owned must be 0/1 and slot in [-1, n_slots)");
+      if (!owned[i] && slot[i] < 0) return fail(h, PIADMM_E_ARG, "shard: a ghost agent needs an exchange slot");
+      ghosts |= !owned[i];
+    }
+    for (int e = 0; e < n_edges; ++e) {
+      if (counted[e] > 1) return fail(h, PIADMM_E_ARG, "shard: counted must be 0/1");
+      if (!owned[edges[2 * e]] && !owned[edges[2 * e + 1]])
+        return fail(h, PIADMM_E_ARG, "shard: a pair of two ghost agents (it belongs to another rank)");
+    }
+    if (ghosts && n_slots == 0) return fail(h, PIADMM_E_ARG, "shard: ghost agents without an exchange buffer");
+    if (n_slots > 0 && !h->cfg.term_global)
+      return fail(h, PIADMM_E_ARG, "shard: pairs across ranks need term_global (one stop for the whole job)");
+    if (n_slots > 0) simple = false;
   }
   for (int i = 0; i < N; ++i)
     if (!std::isfinite(spd[i]) || !std::isfinite(xt0[3 * i]) || !std::isfinite(xt0[3 * i + 1]) ||
@@ -372,6 +436,20 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
     rc |= dalloc(h, &A.xflags, (size_t)N);
     rc |= dalloc(h, &A.eflags, E);
   }
+  unsigned char *d_owned = nullptr, *d_counted = nullptr;
+  int* d_xslot = nullptr;
+  h->xchg = sharded && n_slots > 0;
+  h->n_slots = h->xchg ? n_slots : 0;
+  h->d_xrecv = nullptr;
+  if (sharded) {
+    rc |= dalloc(h, &d_owned, (size_t)N);
+    rc |= dalloc(h, &d_counted, E);
+    rc |= dalloc(h, &d_xslot, (size_t)N);
+  }
+  if (h->xchg) {
+    rc |= dalloc(h, &A.xbuf, (size_t)n_slots * 3 * H1);
+    rc |= dalloc(h, &h->d_xrecv, (size_t)n_slots * 3 * H1);
+  }
 #ifdef PIADMM_STAMPS
   rc |= dalloc(h, &A.stamps, C * 64);
 #endif
@@ -398,6 +476,20 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
     A.nbr_edge = d_gne;
     A.nbr_dir = d_gnd;
   }
+  if (sharded) {
+    h->shard_host.assign(owned, owned + N);
+    h->shard_host.insert(h->shard_host.end(), counted, counted + E);
+    h->graph_host.push_back(std::vector<int>(slot, slot + N));
+    HIPCHK(h, hipMemcpyAsync(d_owned, h->shard_host.data(), N, hipMemcpyHostToDevice, h->stream));
+    if (E) HIPCHK(h, hipMemcpyAsync(d_counted, h->shard_host.data() + N, E, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(d_xslot, h->graph_host.back().data(), (size_t)N * sizeof(int), hipMemcpyHostToDevice,
+                             h->stream));
+    A.owned = d_owned;
+    A.counted = d_counted;
+    A.xslot = d_xslot;
+    A.xrecv = h->d_xrecv;
+    A.n_slots = h->n_slots;
+  }
   if (int rc2 = reset_penalties(h)) return rc2;
   HIPCHK(h, hipMemsetAsync(A.xcache_rho, 0xff, (size_t)N * sizeof(double), h->stream));   // NaN: no cache
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -413,10 +505,30 @@ int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* 
   // every rank of a sharded job takes, with the RCCL all-reduce) for tests and comparisons
   {
     const char* nc = std::getenv("PIADMM_NO_COOP");
-    h->coop = h->cfg.term_global && !h->cfg.fixed_iters && !(nc && nc[0] == '1') &&
+    h->coop = h->cfg.term_global && !h->cfg.fixed_iters && !(nc && nc[0] == '1') && !h->xchg &&
               (A.graph ? pd::graph_coop_fits(A, h->cfg.device) : pd::coop_fits(A, h->cfg.device));
   }
   h->have_scn = true;
+  return PIADMM_OK;
+}
+
+int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* xt0, const double* ref,
+                            int32_t T, const int32_t* edges, int32_t n_edges) {
+  return set_scenario_impl(h, spd, xt0, ref, T, edges, n_edges, nullptr, nullptr, 0, nullptr);
+}
+
+int32_t piadmm_set_scenario_shard(piadmm_handle_t h, const double* spd, const double* xt0, const double* ref,
+                                  int32_t T, const int32_t* edges, int32_t n_edges, const uint8_t* owned,
+                                  const int32_t* slot, int32_t n_slots, const uint8_t* counted) {
+  if (!owned) return fail(h, PIADMM_E_ARG, "shard: null owned");
+  return set_scenario_impl(h, spd, xt0, ref, T, edges, n_edges, owned, slot, n_slots, counted);
+}
+
+int32_t piadmm_set_allreduce(piadmm_handle_t h, piadmm_allreduce_fn fn, void* ctx) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (h->comm && fn) return fail(h, PIADMM_E_STATE, "the handle already has an RCCL communicator");
+  h->xfn = fn;
+  h->xctx = ctx;
   return PIADMM_OK;
 }
 
@@ -459,10 +571,65 @@ static int launch_step(const pd::DevArgs& a, int t, int n, int it0, int it1, int
 // partials all-reduced over RCCL and read back, the stop decided on the host exactly as
 // casadi/main.py:115-118,174-178 (MATLAB :191-210) do over all agents, then a final launch
 // for outputs and propagation.
+// Sharded graph with pairs across ranks: every outer iteration is an X launch
+// (x-steps of the rank's own agents; boundary agents write px | py | u to their exchange slot),
+// ONE all-reduce of the exchange buffer (the ranks' slots are disjoint and zero elsewhere, so
+// the sum is an all-gather), and a Z launch (ghost agents read their owner's values; every
+// pair with an own agent -- a cross-rank pair on both of its ranks, bit-identically -- does its
+// collision test, pair QP and dual update; a cross-rank pair counts its residual on the rank
+// of its first agent only).  Natural termination adds the 5-double all-reduce of the
+// termination partials and the host decision of the unsharded host-decided path.
+static int32_t run_steps_xchg(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outputs) {
+  const piadmm_config_t& c = h->cfg;
+  hipStream_t s = h->stream;
+  const int M = c.max_outer;
+  const size_t nx = (size_t)h->n_slots * 3 * (c.H + 1);
+  for (int k = 0; k < n; ++k) {
+    const int tk = t + k;
+    h->ghist.assign((size_t)2 * M, NAN);
+    int flag = 0, nit = 0, nanlast = 0;
+    for (int it = 0; it < M; ++it) {
+      LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | pd::F_XONLY, s));
+      if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
+      LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, pd::F_GLOBAL | pd::F_ZONLY, s));
+      nit = it + 1;
+      if (c.fixed_iters) continue;
+      double* part = h->d_part + (size_t)5 * it;
+      LAUNCH(h, pd::launch_graph_partials(h->a, part, s));
+      if (int rc = allreduce(h, part, part, 5)) return rc;
+      HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
+      const double n_seen = h->h_part[3], n_bad = h->h_part[4];
+      if (n_act == 0.0 && flag == 0) {      // no pair collides anywhere: stop (casadi/main.py:115-116)
+        nanlast = 1;
+        break;
+      }
+      flag = 1;
+      h->ghist[2 * it + 0] = rk;
+      h->ghist[2 * it + 1] = sk;
+      if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || (n_seen > 0.0 && n_bad == 0.0))) break;
+    }
+    h->giters = nit;
+    LAUNCH(h, launch_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
+    if (c.fixed_iters) {
+      LAUNCH(h, pd::launch_resid_history(h->a, 1, h->d_part, s));
+      if (int rc = allreduce(h, h->d_part, h->d_part, (size_t)2 * M)) return rc;
+      if (sync_outputs && k == n - 1) {
+        HIPCHK(h, hipMemcpyAsync(h->h_part, h->d_part, (size_t)2 * M * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        h->ghist.assign(h->h_part, h->h_part + 2 * M);
+      }
+    }
+  }
+  return PIADMM_OK;
+}
+
 static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outputs) {
   const piadmm_config_t& c = h->cfg;
   hipStream_t s = h->stream;
   const int M = c.max_outer;
+  if (h->xchg) return run_steps_xchg(h, t, n, sync_outputs);
   if (!c.term_global) {
     LAUNCH(h, launch_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST, s));
     return PIADMM_OK;
@@ -470,8 +637,7 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
   if (c.fixed_iters) {
     LAUNCH(h, launch_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL, s));
     LAUNCH(h, pd::launch_resid_history(h->a, n, h->d_part, s));
-    if (h->comm)
-      NCCLCHK(h, ncclAllReduce(h->d_part, h->d_part, (size_t)n * 2 * M, ncclDouble, ncclSum, h->comm, s));
+    if (int rc = allreduce(h, h->d_part, h->d_part, (size_t)n * 2 * M)) return rc;
     h->giters = M;
     if (sync_outputs) {
       const double* last = h->d_part + (size_t)(n - 1) * 2 * M;
@@ -481,12 +647,12 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
     }
     return PIADMM_OK;
   }
-  if (h->coop && !h->comm &&
+  if (h->coop && !h->comm && !h->xfn &&
       launch_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST | pd::F_GLOBAL | pd::F_COOP, s) != 0) {
     (void)hipGetLastError();       // the cooperative launch was refused: host-decided path from now on
     h->coop = false;
   }
-  if (h->coop && !h->comm) {
+  if (h->coop && !h->comm && !h->xfn) {
     if (sync_outputs) {
       int gi = 0;
       HIPCHK(h, hipMemcpyAsync(h->h_part, h->a.ghist + (size_t)(n - 1) * 2 * M, (size_t)2 * M * sizeof(double),
@@ -507,7 +673,7 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
       LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
       double* part = h->d_part + (size_t)5 * it;
       LAUNCH(h, h->a.graph ? pd::launch_graph_partials(h->a, part, s) : pd::launch_term_partials(h->a, it, part, s));
-      if (h->comm) NCCLCHK(h, ncclAllReduce(part, part, 5, ncclDouble, ncclSum, h->comm, s));
+      if (int rc = allreduce(h, part, part, 5)) return rc;
       HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
       HIPCHK(h, hipStreamSynchronize(s));
       const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
@@ -601,7 +767,8 @@ int32_t piadmm_n_components(piadmm_handle_t h) { return h && h->have_scn ? h->C 
 
 int32_t piadmm_steps_per_launch(piadmm_handle_t h) {
   if (!h || !h->have_scn) return 0;
-  if (h->cfg.term_global && !h->cfg.fixed_iters) return (h->coop && !h->comm) ? h->step_cap : 1;
+  if (h->xchg) return 1;
+  if (h->cfg.term_global && !h->cfg.fixed_iters) return (h->coop && !h->comm && !h->xfn) ? h->step_cap : 1;
   return h->step_cap;
 }
 
@@ -641,6 +808,7 @@ int32_t piadmm_comm_init(piadmm_handle_t h, const uint8_t* id_in, int32_t nranks
   if (!h || !id_in) return fail(h, PIADMM_E_ARG, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(h, PIADMM_E_ARG, "bad rank / nranks");
   if (h->comm) return fail(h, PIADMM_E_STATE, "communicator already initialised");
+  if (h->xfn) return fail(h, PIADMM_E_STATE, "the handle already has a host all-reduce transport");
   HIPCHK(h, hipSetDevice(h->cfg.device));
   ncclUniqueId id;
   std::memcpy(id.internal, id_in, NCCL_UNIQUE_ID_BYTES);

@@ -495,6 +495,19 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       __syncthreads();
     }
     if (xonly) break;
+    // -------- ghosts (sharded job): the positions and controls their owner rank computed in this
+    // iteration's X phase, from the all-reduced exchange buffer (piadmm_capi.cpp run_steps)
+    if (A.xrecv) {
+      for (int i = a0 + w; i < a1; i += GW) {
+        const int a = A.comp_alist[i];
+        if (A.owned[a]) continue;
+        const double* xb = A.xrecv + (size_t)A.xslot[a] * (3 * H1);
+        double* po = A.pos_old + (size_t)a * 2 * H1;
+        for (int k = l; k < 2 * H1; k += WAVE) po[k] = xb[k];
+        if (l < H) A.u[(size_t)a * H + l] = xb[2 * H1 + l];
+      }
+      __syncthreads();
+    }
     // -------- Z: collision test + pair QPs + dual updates (casadi/main.py:110-162)
     for (int j = e0 + w; j < e1; j += GW) g_zstep<BIG>(A, A.comp_elist[j], t, W, n);
     __syncthreads();
@@ -503,12 +516,13 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       double rk = 0.0, sk = 0.0, nact = 0.0, nseen = 0.0, nbad = 0.0;
       for (int j = e0; j < e1; ++j) {
         const int e = A.comp_elist[j];
+        if (A.counted && !A.counted[e]) continue;    // a cross-rank pair counts on one rank only
         const double d = A.dischk[e];
         if (d == d) {
           nseen += 1.0;
           nbad += (d > A.deff[e]) ? 0.0 : 1.0;
         }
-        if (!A.edge_active[e] || (A.counted && !A.counted[e])) continue;
+        if (!A.edge_active[e]) continue;
         nact += 1.0;
         if (!aliased) sk += A.eres[2 * e + 1];
         rk += A.eres[2 * e];
@@ -580,7 +594,9 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
     }
     if (stop) break;
     // last_iter_hat_pos = hat_pos_old (casadi/main.py:180; MATLAB copies): after the decision
-    if (!c.alias_dual_residual) {
+    // (host-decided global termination: at the start of the next launch, once the host has
+    // decided to continue)
+    if (!c.alias_dual_residual && !(global && !coop && !c.fixed_iters)) {
       for (int j = e0 + w; j < e1; j += GW) {
         const int e = A.comp_elist[j];
         if (A.edge_active[e])

@@ -91,7 +91,9 @@ struct DevArgs {
   const unsigned char* owned;   // N   1: this rank solves the agent's x-step (0: ghost of another rank)
   const unsigned char* counted; // E   1: this rank counts the pair's residual (cross-rank pairs: one rank)
   const int* xslot;         // N   slot of a boundary agent in the exchange buffer (-1: none)
-  double* xbuf;             // n_slots * (2(H+1) + H): owner-written positions | controls (all-reduced)
+  double* xbuf;             // n_slots * 3(H+1): send buffer, px | py | u of the rank's own boundary
+                            //   agents (other slots stay 0, so the all-reduce sum is an all-gather)
+  const double* xrecv;      // n_slots * 3(H+1): the all-reduced buffer (ghost agents read theirs)
   int n_slots;
   double* seed_g;           // N*2 seeds of the current MPC step (casadi/main.py:48-49)
   double* eres;             // E*2 (rk_e, sk_e) of the pair's last z-step

@@ -77,7 +77,13 @@ SYMBOLS = [
     ("piadmm_comm_unique_id", c_i32, [_P(ctypes.c_uint8)]),
     ("piadmm_comm_init", c_i32, [_H, _P(ctypes.c_uint8), c_i32, c_i32]),
     ("piadmm_global_resid", c_i32, [_H, _dp, _ip]),
+    ("piadmm_set_scenario_shard", c_i32, [_H, _dp, _dp, _dp, c_i32, _ip, c_i32, _P(ctypes.c_uint8), _ip, c_i32,
+                                          _P(ctypes.c_uint8)]),
+    ("piadmm_set_allreduce", c_i32, [_H, ctypes.c_void_p, ctypes.c_void_p]),
 ]
+
+# piadmm_allreduce_fn: int32_t (*)(void* ctx, double* buf, int64_t n)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(c_i32, ctypes.c_void_p, _dp, ctypes.c_int64)
 
 _lib = None
 

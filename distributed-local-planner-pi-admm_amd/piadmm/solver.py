@@ -36,9 +36,17 @@ class StepResult:
 class PI_ADMM_MI355X:
     """Batched PI-ADMM planner on one GPU (one handle, one HIP stream)."""
 
-    def __init__(self, cfg: PIADMMConfig, scenario: Scenario, device: int = 0):
+    def __init__(self, cfg: PIADMMConfig, scenario: Scenario | None = None, device: int = 0, shard=None):
+        """``shard`` (a :class:`piadmm.dist.Shard`): this rank's part of a job whose candidate
+        pairs may cross ranks; ``scenario`` is then ``shard.scn`` (own agents + ghosts)."""
+        if shard is not None:
+            scenario = shard.scn if scenario is None else scenario
+        if scenario is None:
+            raise ValueError("a scenario (or a shard) is required")
         self.cfg = cfg
         self.scn = scenario
+        self.shard = shard
+        self._xfn = None
         self.N = scenario.n_agents
         self.E = scenario.n_edges
         self.lib = _lib.load()
@@ -56,9 +64,19 @@ class PI_ADMM_MI355X:
         xt0 = np.ascontiguousarray(scenario.xt0, np.float64)
         ref = np.ascontiguousarray(scenario.ref, np.float64)
         edges = np.ascontiguousarray(scenario.edges, np.int32).reshape(-1)
-        self._check(self.lib.piadmm_set_scenario(self._h, _lib.dptr(spd), _lib.dptr(xt0), _lib.dptr(ref),
-                                                 ref.shape[2], _lib.iptr(edges) if edges.size else None,
-                                                 self.E))
+        if shard is None:
+            self._check(self.lib.piadmm_set_scenario(self._h, _lib.dptr(spd), _lib.dptr(xt0), _lib.dptr(ref),
+                                                     ref.shape[2], _lib.iptr(edges) if edges.size else None,
+                                                     self.E))
+        else:
+            u8 = ctypes.POINTER(ctypes.c_uint8)
+            owned = np.ascontiguousarray(shard.owned, np.uint8)
+            counted = np.ascontiguousarray(shard.counted, np.uint8)
+            slot = np.ascontiguousarray(shard.slot, np.int32)
+            self._check(self.lib.piadmm_set_scenario_shard(
+                self._h, _lib.dptr(spd), _lib.dptr(xt0), _lib.dptr(ref), ref.shape[2],
+                _lib.iptr(edges) if edges.size else None, self.E, owned.ctypes.data_as(u8), _lib.iptr(slot),
+                int(shard.n_slots), counted.ctypes.data_as(u8) if counted.size else None))
         self.C = self.lib.piadmm_n_components(self._h)
         self.t = 0
         self.xt = xt0.copy()
@@ -105,6 +123,24 @@ class PI_ADMM_MI355X:
             raise ValueError("an RCCL unique id has 128 bytes")
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
         self._check(self.lib.piadmm_comm_init(self._h, buf, int(nranks), int(rank)))
+
+    def set_allreduce(self, fn):
+        """Host all-reduce transport (piadmm_set_allreduce): ``fn(buf)`` gets a float64 array view
+        and must replace it in place by its sum over the job's ranks (e.g. a gloo all-reduce).
+        ``None`` removes it."""
+        if fn is None:
+            self._xfn = None
+            self._check(self.lib.piadmm_set_allreduce(self._h, None, None))
+            return
+
+        def cb(ctx, buf, n):
+            try:
+                fn(np.ctypeslib.as_array(buf, shape=(int(n),)))
+                return 0
+            except Exception:       # an exception cannot cross the C boundary: fail the step
+                return 1
+        self._xfn = _lib.ALLREDUCE_FN(cb)      # kept alive as long as the handle
+        self._check(self.lib.piadmm_set_allreduce(self._h, ctypes.cast(self._xfn, ctypes.c_void_p), None))
 
     def run(self, n_steps: int | None = None) -> list[StepResult]:
         n = self.scn.n_steps if n_steps is None else n_steps

@@ -22,8 +22,11 @@
  *   - all arrays are row-major fp64 (int32 for indices); the caller owns host
  *     arrays, the library copies them; the library owns all device memory.
  *   - a handle is bound to one HIP device and is not thread-safe.
- *   - multi-GPU = one process per GPU, each with its own handle over its own
- *     shard of components (no data-path collective: see DESIGN.md).
+ *   - multi-GPU = one process per GPU, each with its own handle over its shard of
+ *     agents.  Whole components per rank need no data-path collective (global
+ *     termination all-reduces 5 scalars per outer iteration); pairs across ranks add
+ *     one all-reduce of the boundary exchange buffer per outer iteration
+ *     (piadmm_set_scenario_shard).
  */
 #ifndef PIADMM_H
 #define PIADMM_H
@@ -34,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PIADMM_ABI_VERSION 2
+#define PIADMM_ABI_VERSION 3
 
 enum {
   PIADMM_OK = 0,
@@ -58,7 +61,7 @@ enum {
  * ABI: the Python dataclass piadmm.config.PIADMMConfig has the same fields. */
 typedef struct piadmm_config {
   int32_t n_agents;
-  int32_t H;                 /* num_ho (<= 32 in this version) */
+  int32_t H;                 /* num_ho, 3 <= H <= 63 (H > 32: matrices in HBM / L2) */
   int32_t max_outer;         /* iter_num */
   int32_t dual_mode;
   double dt, L, dis_thres, beta, Pnorm, Pcost, rho, eps_pri, eps_dual, u_max, du_max;
@@ -102,10 +105,38 @@ const char* piadmm_last_error(piadmm_handle_t h);
 
 /* Scenario: speeds (N), initial states (N x 3: x, y, theta), reference positions
  * (N x 2 x T, ref[i][0][t] = x, ref[i][1][t] = y; casadi/PI_ADMM_class.py:33-37)
- * and candidate pairs (E x 2, v1 < v2).  Components of the pair graph must
- * have at most 2 agents in this version.  Resets xt to xt0. */
+ * and candidate pairs (E x 2, v1 < v2; any static graph: an agent's x-step sums the
+ * consensus term over all its candidate neighbours, PI_ADMM_class.py:126-129, and every
+ * candidate pair is collision-tested, casadi/main.py:110-113).  Resets xt to xt0. */
 int32_t piadmm_set_scenario(piadmm_handle_t h, const double* spd, const double* xt0,
                             const double* ref, int32_t T, const int32_t* edges, int32_t n_edges);
+
+/* One rank's part of a sharded job whose candidate pairs may cross ranks.
+ * The arrays describe the rank's LOCAL scenario: its own agents plus a ghost copy of every
+ * neighbour owned by another rank, and every pair with at least one own agent (the host
+ * side, piadmm.dist.shard_graph, builds it).
+ *   owned   N   1: this rank solves the agent's x-step; 0: ghost (another rank's agent)
+ *   slot    N   the agent's slot in the job-wide boundary exchange buffer, -1 if none; every
+ *               ghost has one, and so has every own agent with a neighbour on another rank
+ *   n_slots     slots in the job (the same on every rank; 0: nothing crosses ranks)
+ *   counted E   1: this rank counts the pair's residuals and termination terms (a cross-rank
+ *               pair on exactly one of its ranks, e.g. the owner of v1)
+ * With n_slots > 0 every outer iteration all-reduces n_slots x 3(H+1) doubles (positions and
+ * controls of the boundary agents, each slot written by its owner and 0 elsewhere) between
+ * the x-steps and the pair step; a cross-rank pair is solved on both of its ranks, bit-
+ * identically.  Requires term_global (the job stops as one).  Transport: the RCCL
+ * communicator (piadmm_comm_init) or the host callback (piadmm_set_allreduce). */
+int32_t piadmm_set_scenario_shard(piadmm_handle_t h, const double* spd, const double* xt0,
+                                  const double* ref, int32_t T, const int32_t* edges, int32_t n_edges,
+                                  const uint8_t* owned, const int32_t* slot, int32_t n_slots,
+                                  const uint8_t* counted);
+
+/* Host all-reduce transport for jobs without RCCL (e.g. ranks sharing one GPU, or a gloo /
+ * MPI host fabric): fn(ctx, buf, n) must replace buf[0..n) by its sum over all ranks of the
+ * job and return 0 (non-zero aborts the step).  Used for the exchange buffer, termination
+ * partials and residual histories; fn = NULL removes it. */
+typedef int32_t (*piadmm_allreduce_fn)(void* ctx, double* buf, int64_t n);
+int32_t piadmm_set_allreduce(piadmm_handle_t h, piadmm_allreduce_fn fn, void* ctx);
 
 /* Overwrite the current agent states (N x 3). */
 int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt);
@@ -158,8 +189,9 @@ int32_t piadmm_get_component_counters(piadmm_handle_t h, uint64_t* out, int32_t 
  * the other ranks (any out-of-band channel); every rank then calls piadmm_comm_init.
  * mpc_step then all-reduces the termination partials (rk, sk, active pairs, distance
  * checks) once per outer iteration, or, with fixed_iters, the residual history once per
- * MPC step.  Components never straddle ranks.  Without a communicator the handle is a
- * single-rank job. */
+ * MPC step, and, for a sharded graph (piadmm_set_scenario_shard), the boundary exchange
+ * buffer once per outer iteration.  Without a communicator (or host transport) the
+ * handle is a single-rank job. */
 int32_t piadmm_comm_unique_id(uint8_t* id_out /* 128 bytes */);
 int32_t piadmm_comm_init(piadmm_handle_t h, const uint8_t* id /* 128 bytes */, int32_t nranks, int32_t rank);
 

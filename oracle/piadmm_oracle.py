@@ -293,9 +293,14 @@ class StepRecord:
 class Oracle:
     """Runs the reference loop (``casadi/main.py:43-201``) on a :class:`Scenario`."""
 
-    def __init__(self, cfg, scn):
+    def __init__(self, cfg, scn, owned=None, counted=None):
+        """``owned`` / ``counted`` (one rank of a job whose pairs cross ranks, piadmm.dist.Shard):
+        only owned agents solve their x-step (the others are ghosts filled by the ``exchange``
+        hook of :meth:`mpc_step`), and only counted pairs enter the residual sums."""
         self.cfg = cfg
         self.scn = scn
+        self.owned = None if owned is None else np.asarray(owned, bool)
+        self.counted = None if counted is None else np.asarray(counted, bool)
         self.N, self.E, self.H = scn.n_agents, scn.n_edges, cfg.H
         self.comp, self.n_comp = scn.components()
         self.xt = scn.xt0.astype(np.float64).copy()
@@ -319,7 +324,7 @@ class Oracle:
         sy = around(xt[:, 1] + c.dt * self.scn.spd * np.sin(xt[:, 2]), c.round_decimals)
         return np.stack([sx, sy], axis=1)
 
-    def mpc_step(self, components=None, reduce=None) -> StepRecord:
+    def mpc_step(self, components=None, reduce=None, exchange=None) -> StepRecord:
         """One ``num_step`` body of ``casadi/main.py:43-201``.
 
         Iteration-major: every outer iteration runs the x-steps of all agents, the
@@ -332,8 +337,14 @@ class Oracle:
         ``reduce`` (term_global only) maps this process's termination partials
         [rk, sk, active pairs, pairs with a distance check, pairs failing it] to the sums over
         all processes: the all-reduce of the sharded path (tests/test_dist.py runs it on gloo).
+        ``exchange(pos_old, primal_u)`` (a rank of a job whose pairs cross ranks) fills the ghost
+        agents' rows in place after the x-steps: the boundary all-reduce of the sharded path.
         """
         cfg, H, N, E = self.cfg, self.H, self.N, self.E
+        if exchange is not None and not cfg.term_global:
+            raise ValueError("pairs across ranks need term_global")
+        own = (lambda i: True) if self.owned is None else (lambda i: bool(self.owned[i]))
+        cnt = (lambda e: True) if self.counted is None else (lambda e: bool(self.counted[e]))
         t = self.t
         seeds = self.seeds()
         pos_old = np.zeros((N, 2, H + 1))
@@ -367,6 +378,8 @@ class Oracle:
                     iters[c] = it + 1
                 # ---- x-step, casadi/main.py:81-106
                 for i in agents:
+                    if not own(i):
+                        continue          # a ghost: its owner rank solves it (exchange below)
                     terms = [(hat[e, d], lam[e, d]) for (_, e, d) in self.nbrs[i]]
                     u_star, _ = solve_xstep(cfg, self.xt[i], self.scn.spd[i],
                                             self.scn.ref[i, :, t:t + H + 1], terms)
@@ -375,6 +388,8 @@ class Oracle:
                     px, py, _ = roll(self.xt[i], u, self.scn.spd[i], cfg.dt, cfg.L)
                     pos_old[i, 0], pos_old[i, 1] = px, py
                     self.primal_u[i] = u
+                if exchange is not None:
+                    exchange(pos_old, self.primal_u)
                 # ---- collision graph, casadi/main.py:110-118
                 for e in edges:
                     v1, v2 = self.scn.edges[e]
@@ -399,15 +414,16 @@ class Oracle:
                 for c in gcomps:
                     rk = sk = 0.0
                     for e in self.comp_edges[c]:
-                        if not active[e]:
+                        if not active[e] or not cnt(e):
                             continue
                         rk_e, sk_e = pair_residuals(cfg, pos_old[int(self.scn.edges[e, 0])], hat[e, 0], last_hat[e, 0])
                         if not g_alias[g]:
                             sk += sk_e
                         rk += rk_e
                     comp_r.append((rk, sk))
-                seen = [e for e in edges if np.isfinite(dis_chk[e])]
-                part = np.array([sum(r for r, _ in comp_r), sum(q for _, q in comp_r), float(len(act)),
+                seen = [e for e in edges if np.isfinite(dis_chk[e]) and cnt(e)]
+                part = np.array([sum(r for r, _ in comp_r), sum(q for _, q in comp_r),
+                                 float(sum(1 for e in act if cnt(e))),
                                  float(len(seen)), float(sum(1 for e in seen if not dis_chk[e] > d_eff[e]))])
                 if cfg.term_global and reduce is not None:
                     part = np.asarray(reduce(part), np.float64)     # the all-reduce of the sharded path

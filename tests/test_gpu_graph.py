@@ -78,14 +78,16 @@ def test_mixed_components_and_horizons(Solver, H):
     compare(Solver, config.matlab_pi(H=H), scn, 8 if H > 32 else 12)
 
 
+@pytest.mark.parametrize("warm", [0, 1])
 @pytest.mark.parametrize("coop", [True, False])
-def test_graph_global_termination(Solver, coop, monkeypatch):
+def test_graph_global_termination(Solver, coop, warm, monkeypatch):
     """The reference's global flag / stop over all agents (term_global): in-kernel behind a grid
-    barrier (cooperative launch) or host-decided (PIADMM_NO_COOP=1, one launch per iteration)."""
+    barrier (cooperative launch) or host-decided (PIADMM_NO_COOP=1, one launch per iteration);
+    with warm duals the step's final last_iter_hat carries over (copied only when continuing)."""
     scn = scenario.concat([scenario.crossing(4, 15, n_steps=20, seed=2), scenario.crossing(3, 15, n_steps=20, seed=3)])
     if not coop:
         monkeypatch.setenv("PIADMM_NO_COOP", "1")
-    compare(Solver, config.matlab_pi(H=15, term_global=1), scn, 14)
+    compare(Solver, config.matlab_pi(H=15, term_global=1, warm_duals=warm), scn, 14)
 
 
 def test_graph_warm_duals_tightening_fixed(Solver):

@@ -101,7 +101,13 @@ def test_tightening_matches_oracle(Solver):
             scenario.tiled(2, 15, n_steps=30, seed=6), 20)
 
 
-def test_all_modes_together_at_bench_horizon(Solver):
+@pytest.mark.parametrize("coop", [True, False])
+def test_all_modes_together_at_bench_horizon(Solver, coop, monkeypatch):
+    """Global scope, warm duals and tightening at H = 30, the stop decided in-kernel (coop) or
+    on the host (one launch per outer iteration): last_iter_hat is copied only when the job
+    continues (casadi/main.py:180 after the stop test), which the warm duals carry over."""
+    if not coop:
+        monkeypatch.setenv("PIADMM_NO_COOP", "1")
     cfg = config.matlab_pi(H=30, term_global=1, warm_duals=1, tighten=1)
     compare(Solver, cfg, scenario.tiled(2, 30, n_steps=10, seed=8), 6)
 
