@@ -607,7 +607,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
   double xv[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) xv[v] = x0[v];
-  {
+  auto sub_Y = [&](double lamv) {
     constexpr int XB = 4;
     const int lc = (l < H) ? l : 0;
     for (int a0 = 0; a0 < m; a0 += XB) {
@@ -643,6 +643,26 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
 #pragma unroll
         for (int v = 0; v < NV; ++v) xv[v] -= (cf[u][v][0] * tv[u][v][0] + cf[u][v][1] * tv[u][v][1]) * la[u];
     }
+  };
+  sub_Y(lamv);
+  // one step of primal refinement: at a vertex held by large multipliers (a saturated pair
+  // pushed by linear hinge rows: |lam| ~ 1e6 at beta = 1000) x0 - Y lam cancels to ~1e-9, above
+  // the certificate's feasibility tolerance; the correction of the active rows' residual
+  // e = A_W x - b is small, so its own cancellation is not
+  {
+    double axr[NR];
+    A_mul(P, xv, axr);
+    wsync();
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = axr[s];
+    }
+    wsync();
+    const double e = (l < m) ? vb_ax[myid] - vb_b[l] : 0.0;
+    const double dl = chol_solve(P.fac, ld, linv, e, m);
+    if (!isfinite(dl)) return false;
+    lamv += dl;
+    sub_Y(dl);
   }
   STAMP_ADD(NV == 1 ? ST_RED_X : ST_ZR_X, t_x);
   if (l < m) vb_lam[l] = lamv;
@@ -1245,9 +1265,9 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   };
   // multipliers of the equality-constrained minimiser on the active set (signed normals):
   // lam = S^-1 (N x0 - b); kernel multiplier of row a = sign_a * lam_a, GI multiplier -lam_a
-  auto eqp_lam = [&]() -> double {
+  auto eqp_lam = [&](const double* xv) -> double {
     double ax0[NR];
-    A_mul(P, x0, ax0);
+    A_mul(P, xv, ax0);
     if (l < H) {
 #pragma unroll
       for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ax0[s] - P.lo(s);   // lower-side residual
@@ -1341,7 +1361,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       // dual feasibility: drop the most negative (or beyond-cap hinge) multiplier until none
       double lam = 0.0;
       while (m > 0) {
-        lam = eqp_lam();
+        lam = eqp_lam(x0);
         const int myc = (l < m) ? wc[l] : 0;
         const double u = -lam;
         double sc = 0.0;
@@ -1492,10 +1512,21 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     }
   }
   // ---- exact solution of the final active set (the reduced solve with this factor):
-  // lam = S^-1 (N x0 - b), x = x0 - Y lam;  kernel multipliers y_a = sign_a * lam_a
+  // lam = S^-1 (N x0 - b), x = x0 - Y lam, then one step of primal refinement on the active
+  // rows' residual (see reduced_solve);  kernel multipliers y_a = sign_a * lam_a
   {
-    const double lam = eqp_lam();
-    x_of(lam);
+    const double lam0 = eqp_lam(x0);
+    x_of(lam0);
+    const double dl = eqp_lam(xc);
+    {
+      const int lc = (l < H) ? l : 0;
+      for (int a = 0; a < m; ++a) {
+        const double da = rdl(dl, a);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xc[v] -= da * Y[a * H2 + v * H + lc];
+      }
+    }
+    const double lam = lam0 + dl;
     const int myc = (l < m) ? wc[l] : 0;
     const int rw = myc >> 1;
     wsync();
@@ -1660,14 +1691,20 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
           A_mul(P, x, axd);
 #pragma unroll
           for (int s = 0; s < NR; ++s)
-            if (P.valid(s) && nl[s] != glab[s])
-              printf("  kkt viol slot %d lane %d lab %d -> %d ax %.12g lo %.12g hi %.12g y %.12g\n", s, lid(),
-                     (int)glab[s], (int)nl[s], axd[s], P.lo(s), P.hi(s), y[s]);
+            if (P.valid(s)) {
+              const double bd = (glab[s] == UPPER && !P.hinge(s)) ? P.hi(s) : P.lo(s);
+              const bool act = P.hinge(s) ? glab[s] == HKINK : glab[s] != FREE;
+              const double tp = P.tol * (1.0 + fabs(P.lo(s)));
+              if (nl[s] != glab[s] || (act && fabs(axd[s] - bd) > tp) || !isfinite(y[s]))
+                printf("  kkt viol slot %d lane %d lab %d -> %d ax %.12g bd %.12g y %.12g\n", s, lid(),
+                       (int)glab[s], (int)nl[s], axd[s], bd, y[s]);
+            }
         }
 #endif
 #pragma unroll
         for (int s = 0; s < NR; ++s) lab[s] = glab[s];
         if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+        GI_DBG("  after pdas ok=%d\n", (int)ok);
       } else {
         // GI stopped (typically a hinge multiplier at its cap beta: that hinge is linear at the
         // optimum, which the dual active set does not model): polish from its working set with
