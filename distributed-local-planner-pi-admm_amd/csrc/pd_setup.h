@@ -87,11 +87,14 @@ __device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, doubl
 
 // x-step QP of agent a (cost_function_primal, PI_ADMM_class.py:114-135, constraints :172-192):
 // scaling, K_s^-1 (LDS) and P^-1 (LDS) for the whole MPC step.
-__device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, const Geo& g, double* xfac) {
+// coef >= 0: the P coefficient of M'M (global PI: 2 Pnorm + sum of the pairs' penalties), part of
+// the cache key.  Returns true when the caches were rebuilt (the parametric tables are stale).
+__device__ __forceinline__ bool setup_agent(const DevArgs& A, int a, QP<1>& P, const Geo& g, double* xfac,
+                                            double coef = -1.0) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, l = lid();
   const bool in = l < H;
-  P.coefP = 2.0 * c.Pnorm + c.rho * (double)A.nbr_cnt[a];
+  P.coefP = coef >= 0.0 ? coef : 2.0 * c.Pnorm + c.rho * (double)A.nbr_cnt[a];
   P.mm[0] = g.mm;
   double* Kc = A.Kx_cache + (size_t)a * H * H;
   double* Pc = A.Pinv_x + (size_t)a * H * H;
@@ -99,7 +102,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
   const int li = l < HCAP ? l : 0;
   // P depends on the agent's speed only (make_geo): K_s^-1, P^-1 and the scaling are
   // cached in HBM per scenario and rebuilt only when the ADMM penalty differs.
-  if (__builtin_expect(A.xcache_rho[a] == P.rho, 1)) {
+  if (__builtin_expect(A.xcache_rho[a] == P.rho && (!A.xcache_coef || A.xcache_coef[a] == P.coefP), 1)) {
     P.D[0] = in ? sc[li] : 0.0;
     P.E[0] = in ? sc[HCAP + li] : 0.0;
     P.E[1] = (l < H - 1) ? sc[2 * HCAP + li] : 0.0;
@@ -108,7 +111,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
       P.kready = false;
     }
     wsync();
-    return;
+    return false;
   }
   ruiz(P);
   build_K<1, false>(P, xfac, P.fld, Kc);
@@ -127,9 +130,13 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
     sc[1 * HCAP + l] = P.E[0];
     sc[2 * HCAP + l] = P.E[1];
   }
-  if (l == 0) A.xcache_rho[a] = P.rho;
+  if (l == 0) {
+    A.xcache_rho[a] = P.rho;
+    if (A.xcache_coef) A.xcache_coef[a] = P.coefP;
+  }
   __threadfence();      // P^-1 (read back through L2 by the polish) is visible to this wave
   wsync();
+  return true;
 }
 
 // Pair (z-step) QP of cost_function_edge (PI_ADMM_class.py:145-169), heading frozen at
@@ -139,7 +146,7 @@ __device__ __forceinline__ void setup_agent(const DevArgs& A, int a, QP<1>& P, c
 // PGt = P^-1 G' (HBM), GPG = G P^-1 G' (HBM) and K_s^-1 (LDS).
 __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, const Geo& g1, const Geo& g2,
                                            double c1x, double c1y, double c2x, double c2y, const double* seeds,
-                                           double* scr, double* Ke_lds, double deff) {
+                                           double* scr, double* Ke_lds, double deff, double rho_pair = -1.0) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, n = 2 * H, l = lid();
   const bool in = l < H;
@@ -152,13 +159,13 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
   const double h_time = Dsq + dd - 2.0 * (dbx * (c2x - c1x) + dby * (c2y - c1y));
   P.h0 = shdn(h_time, 1);                    // hinge lane k <-> time k+1
   if (!P.valid(4)) P.h0 = 0.0;
-  P.coefP = c.rho;
+  P.coefP = rho_pair >= 0.0 ? rho_pair : c.rho;
   P.mm[0] = g1.mm;
   P.mm[1] = g2.mm;
 
   // ---- P_v^-1 blocks (HBM), Y = P_v^-1 T' (PGt, unscaled by g) and Z_v = T P_v^-1 T' (GPG):
   // speed-only, so built once per scenario; g1, g2 scale them on the fly (s_gather, x recovery)
-  if (__builtin_expect(!A.ecache[e], 0)) {
+  if (__builtin_expect(!A.ecache[e] || (A.ecache_rho && A.ecache_rho[e] != P.coefP), 0)) {
     double* Yl = Ke_lds;             // H x n staging (the Ke region is rebuilt below)
     double* Pi = A.tab_e + (size_t)e * 8 * H * H;
     for (int v = 0; v < 2; ++v) {
@@ -195,7 +202,10 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
     }
     for (int k = 0; k < H; ++k)
       for (int col = l; col < n; col += WAVE) Pg[k * n + col] = Yl[k * n + col];
-    if (l == 0) A.ecache[e] = 1;
+    if (l == 0) {
+      A.ecache[e] = 1;
+      if (A.ecache_rho) A.ecache_rho[e] = P.coefP;
+    }
     gsync();                    // the tables are read back through L2 by the polish
   }
   STAMP_ADD(ST_SZ_PRE, t_pre);

@@ -37,6 +37,7 @@ struct piadmm_ctx {
   int step_cap = 1;              // MPC steps per persistent launch (resid slots)
   bool coop = false;             // term_global natural termination decided in-kernel (one rank)
   std::vector<double> rho_init;  // host staging of the initial ADMM penalties (outlives the async copy)
+  std::vector<double> rho_pi_init;   // host staging of the global-PI pair penalties
   std::vector<std::vector<int>> graph_host;   // graph-mode index arrays (host staging)
   std::vector<unsigned char> shard_host;      // owned | counted (host staging)
   // sharded graph (piadmm_set_scenario_shard): ghost agents fed by one all-reduce of the
@@ -92,8 +93,10 @@ int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
   if (c.n_agents <= 0) return fail(h, PIADMM_E_ARG, "n_agents must be > 0");
   if (c.H < 3 || c.H > pd::HBIG) return fail(h, PIADMM_E_ARG, "H must be in [3, 63] in this version");
   if (c.max_outer <= 0) return fail(h, PIADMM_E_ARG, "max_outer must be > 0");
-  if (c.dual_mode != PIADMM_DUAL_PLAIN && c.dual_mode != PIADMM_DUAL_PI)
-    return fail(h, PIADMM_E_ARG, "dual_mode must be 0 (plain) or 1 (PI)");
+  if (c.dual_mode != PIADMM_DUAL_PLAIN && c.dual_mode != PIADMM_DUAL_PI && c.dual_mode != PIADMM_DUAL_PI_GLOBAL)
+    return fail(h, PIADMM_E_ARG, "dual_mode must be 0 (plain), 1 (PI) or 2 (global PI)");
+  if (c.dual_mode == PIADMM_DUAL_PI_GLOBAL && !(c.rho_min > 0 && c.rho_max >= c.rho_min && c.rho_num > 0))
+    return fail(h, PIADMM_E_ARG, "global PI needs 0 < rho_min <= rho_max and rho_num > 0");
   if (!(c.dt > 0) || !(c.L > 0) || !(c.rho > 0) || !(c.Pcost > 0) || c.Pnorm < 0 || c.beta < 0)
     return fail(h, PIADMM_E_ARG, "dt, L, rho, Pcost must be > 0; Pnorm, beta >= 0");
   if (c.max_inner <= 0 || c.polish_every <= 0) return fail(h, PIADMM_E_ARG, "max_inner, polish_every must be > 0");
@@ -112,8 +115,12 @@ int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
 int reset_penalties(piadmm_ctx* h) {
   const size_t N = h->N, E = h->E;
   h->rho_init.assign(std::max<size_t>(N, E) + 1, h->cfg.admm_rho);
+  h->rho_pi_init.assign(E + 1, h->cfg.rho);
   HIPCHK(h, hipMemcpyAsync(h->a.rho_x, h->rho_init.data(), N * sizeof(double), hipMemcpyHostToDevice, h->stream));
   if (E) HIPCHK(h, hipMemcpyAsync(h->a.rho_e, h->rho_init.data(), E * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  // global PI: every pair starts from the configured penalty (PI_ADMM_class.py:26, rho = 1)
+  if (E && h->a.rho_pi)
+    HIPCHK(h, hipMemcpyAsync(h->a.rho_pi, h->rho_pi_init.data(), E * sizeof(double), hipMemcpyHostToDevice, h->stream));
   return 0;
 }
 
@@ -241,6 +248,8 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     const char* g = std::getenv("PIADMM_GRAPH");
     if (g && g[0] == '1') simple = false;
   }
+  // the global PI law (adaptive per-pair penalties) runs on the graph kernel
+  if (h->cfg.dual_mode == PIADMM_DUAL_PI_GLOBAL || h->cfg.no_collision_gate) simple = false;
   // a sharded job with a boundary exchange runs on the graph kernel (its X / Z phases are
   // split launches around the all-reduce)
   const bool sharded = owned != nullptr;
@@ -435,6 +444,11 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     rc |= dalloc(h, &A.csig_x, (size_t)N * pd::WAVE);
     rc |= dalloc(h, &A.xflags, (size_t)N);
     rc |= dalloc(h, &A.eflags, E);
+    if (h->cfg.dual_mode == PIADMM_DUAL_PI_GLOBAL) {
+      rc |= dalloc(h, &A.rho_pi, E);
+      rc |= dalloc(h, &A.xcache_coef, (size_t)N);
+      rc |= dalloc(h, &A.ecache_rho, E);
+    }
   }
   unsigned char *d_owned = nullptr, *d_counted = nullptr;
   int* d_xslot = nullptr;
@@ -492,6 +506,8 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   }
   if (int rc2 = reset_penalties(h)) return rc2;
   HIPCHK(h, hipMemsetAsync(A.xcache_rho, 0xff, (size_t)N * sizeof(double), h->stream));   // NaN: no cache
+  if (A.xcache_coef) HIPCHK(h, hipMemsetAsync(A.xcache_coef, 0xff, (size_t)N * sizeof(double), h->stream));
+  if (A.ecache_rho && E) HIPCHK(h, hipMemsetAsync(A.ecache_rho, 0xff, E * sizeof(double), h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   A.spd = d_spd;
   A.ref = d_ref;

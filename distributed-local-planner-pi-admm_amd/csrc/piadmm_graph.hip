@@ -81,14 +81,24 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GW
   qx.y_in_k = false;
   if (l == 0) W.xfs[0] = -1;                 // the wave's scratch served another QP before
   wsync();
-  setup_agent(A, a, qx, gx, W.fac);
+  // global PI: each neighbour term weighted by its pair's adaptive penalty, so P's coefficient of
+  // M'M is 2 Pnorm + sum_e rho_e (neighbour order) and the caches are keyed by it
+  const bool gpi = c.dual_mode == PIADMM_DUAL_PI_GLOBAL;
+  const int k0 = A.nbr_ptr[a], k1 = A.nbr_ptr[a + 1];
+  double coef = -1.0;
+  if (gpi) {
+    double rs = 0.0;
+    for (int k = k0; k < k1; ++k) rs = rs + A.rho_pi[A.nbr_edge[k]];
+    coef = 2.0 * c.Pnorm + rs;
+  }
+  const bool rebuilt = setup_agent(A, a, qx, gx, W.fac, coef);
   // warm state of this QP (written by the previous x-step of the agent, or the step init)
   const double* qs = A.qs_x + (size_t)a * 5 * WAVE;
   const signed char* ql = A.ql_x + (size_t)a * 2 * WAVE;
   double xs[1] = {qs[l]}, zs[2] = {qs[WAVE + l], qs[2 * WAVE + l]}, ys[2] = {qs[3 * WAVE + l], qs[4 * WAVE + l]};
   signed char lab[2] = {ql[l], ql[WAVE + l]};
   const bool warm = (A.xflags[a] & 1) != 0;
-  qx.csig = A.csig_x[(size_t)a * WAVE + l];
+  qx.csig = rebuilt ? -1 : A.csig_x[(size_t)a * WAVE + l];
   // q of cost_function_primal (PI_ADMM_class.py:114-135): M'(2 Pnorm (c - r) + rho sum_j (c - hat_ij
   // + lam_ij)), the neighbours j in increasing order (the oracle's order)
   double vx = 0.0, vy = 0.0;
@@ -97,14 +107,14 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GW
     vx = 2.0 * c.Pnorm * (cx - rp[t + l]);
     vy = 2.0 * c.Pnorm * (cy - rp[A.T + t + l]);
   }
-  const int k1 = A.nbr_ptr[a + 1];
-  for (int k = A.nbr_ptr[a]; k < k1; ++k) {
+  for (int k = k0; k < k1; ++k) {
     const int e = A.nbr_edge[k], d = A.nbr_dir[k];
     const double* hb = A.hat + (size_t)e * 4 * H1 + d * 2 * H1;
     const double* lb = A.lam + (size_t)e * 4 * H1 + d * 2 * H1;
+    const double rw = gpi ? A.rho_pi[e] : c.rho;
     if (tl) {
-      vx = vx + c.rho * (cx - hb[l] + lb[l]);
-      vy = vy + c.rho * (cy - hb[H1 + l] + lb[H1 + l]);
+      vx = vx + rw * (cx - hb[l] + lb[l]);
+      vy = vy + rw * (cy - hb[H1 + l] + lb[H1 + l]);
     }
   }
   const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
@@ -181,7 +191,8 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
     const double dx = px[0] - px[1], dy = py[0] - py[1];
     hit = (dx * dx + dy * dy) < thr;
   }
-  const bool act = wany(hit);
+  // the global-PI script has no collision test: its edge problem runs every iteration
+  const bool act = c.no_collision_gate ? true : wany(hit);
   if (l == 0) A.edge_active[e] = act ? 1 : 0;
   if (!act) return;
   // pair QP of cost_function_edge (PI_ADMM_class.py:145-169), heading frozen at xt (B3)
@@ -201,6 +212,8 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
   qe.Pcost2 = 2.0 * c.Pcost;
   qe.beta = c.beta;
   qe.rho = A.rho_e[e];
+  const bool gpi = c.dual_mode == PIADMM_DUAL_PI_GLOBAL;
+  const double rw = gpi ? A.rho_pi[e] : c.rho;   // the pair's penalty (global PI: adaptive)
   qe.sigma = c.admm_sigma;
   qe.alpha = c.admm_alpha;
   qe.tol = c.qp_tol;
@@ -228,7 +241,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
   if (l == 0) W.zfs[0] = -1;
   wsync();
   const double sd[4] = {A.seed_g[2 * v1], A.seed_g[2 * v1 + 1], A.seed_g[2 * v2], A.seed_g[2 * v2 + 1]};
-  setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, sd, W.fac, Ke, deff);
+  setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, sd, W.fac, Ke, deff, gpi ? rw : -1.0);
   const double* qs = A.qs_e + (size_t)e * 12 * WAVE;
   const signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
   double xs[2] = {qs[l], qs[WAVE + l]}, zs[5], ys[5];
@@ -254,8 +267,8 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
     const double w1 = tl ? ge1.ax * bx[0] + ge1.ay * by[0] : 0.0;
     const double w2 = tl ? ge2.ax * bx[1] + ge2.ay * by[1] : 0.0;
     const double q1 = Tt_apply(shdn(w1, 1)), q2 = Tt_apply(shdn(w2, 1));
-    qe.q[0] = (l < H) ? -c.rho * q1 : 0.0;
-    qe.q[1] = (l < H) ? -c.rho * q2 : 0.0;
+    qe.q[0] = (l < H) ? -rw * q1 : 0.0;
+    qe.q[1] = (l < H) ? -rw * q2 : 0.0;
     qe.qvalid = true;
   }
   double uh[2];
@@ -269,6 +282,64 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
     const double uv = (l < H) ? around(uh[v], c.round_decimals) : 0.0;
     rollout(v ? xb : xa, A.spd[v ? v2 : v1], uv, c, H, true, hx[v], hy[v], hth);
   }
+  double rr = 0.0, ss = 0.0, dchk;
+  if (gpi) {
+    // global PI with adaptive rho and K_P (casadi_old_PI_ADMM/main.py:133-151; oracle
+    // dual_update_global_pi): distances along the nonlinear rollouts of the x-step plans
+    double nx[2], ny[2], nth;
+    for (int v = 0; v < 2; ++v) {
+      const int av = v ? v2 : v1;
+      const double uv = (l < H) ? A.u[(size_t)av * H + l] : 0.0;
+      rollout(v ? xb : xa, A.spd[av], uv, c, H, true, nx[v], ny[v], nth);
+    }
+    double dn;
+    {
+      const double dx = nx[0] - nx[1], dy = ny[0] - ny[1];
+      dn = sqrt(dx * dx + dy * dy);
+    }
+    const double dmin = wmin(tl ? dn : INFINITY);
+    const double kP = fmin(c.theta1 / dmin, c.theta2);
+    const double rnew = fmax(c.rho_min, fmin(c.rho_max, c.rho_num / dmin));
+    double lraw[2][2], lsat[2][2];
+    bool changed = false;
+    for (int v = 0; v < 2; ++v) {
+      double* Sv = Sa + v * 2 * H1;
+      double* Dv = Da + v * 2 * H1;
+      double* hv = hat + v * 2 * H1;
+      for (int xy = 0; xy < 2; ++xy) {
+        const double p = xy == 0 ? px[v] : py[v];
+        const double h = xy == 0 ? hx[v] : hy[v];
+        const double err = p - h;
+        const double so = tl ? Sv[xy * H1 + l] : 0.0;
+        lraw[v][xy] = so + kP * err;                          // lam = S + K_P e (:143)
+        if (tl) Sv[xy * H1 + l] = (so + c.kI * err) + 2.0 * Dv[xy * H1 + l];   // S += K_I e + 2 D (:144)
+        lsat[v][xy] = c.windup ? fmin(c.windup_sat, fmax(lraw[v][xy], -c.windup_sat)) : lraw[v][xy];
+        changed |= tl && (lsat[v][xy] != lraw[v][xy]);
+        if (tl) hv[xy * H1 + l] = h;
+      }
+    }
+    const bool anyc = wany(changed);                           // over the whole pair (:148)
+    for (int v = 0; v < 2; ++v)
+      for (int xy = 0; xy < 2; ++xy)
+        if (tl) {
+          lam[v * 2 * H1 + xy * H1 + l] = lsat[v][xy];
+          if (c.windup) Da[v * 2 * H1 + xy * H1 + l] = anyc ? lsat[v][xy] - lraw[v][xy] : 0.0;
+        }
+    // residuals (:153-154): both sides, no factor 2, the updated penalty
+    if (tl) {
+      for (int v = 0; v < 2; ++v) {
+        const double ex = px[v] - hx[v], ey = py[v] - hy[v];
+        rr += ex * ex + ey * ey;
+        const double fx = rnew * (last[v * 2 * H1 + l] - hx[v]);
+        const double fy = rnew * (last[v * 2 * H1 + H1 + l] - hy[v]);
+        ss += fx * fx + fy * fy;
+      }
+    }
+    rr = wsum(rr);
+    ss = wsum(ss);
+    dchk = rdl(dn, 1);
+    if (l == 0) A.rho_pi[e] = rnew;
+  } else {
   // dual update (plain casadi/main.py:161-162 / PI + anti-windup ADMM_CVX_...:156-188)
   double dist;
   {
@@ -311,7 +382,6 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
     }
   }
   // residual contributions of this pair (casadi/main.py:167-173): the v1 side only
-  double rr = 0.0, ss = 0.0;
   if (tl) {
     const double ex = px[0] - hx[0], ey = py[0] - hy[0];
     rr = ex * ex + ey * ey;
@@ -321,7 +391,9 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
   }
   rr = wsum(rr);
   ss = wsum(ss);
-  const double dchk = rdl(dist, 1);
+  dchk = rdl(dist, 1);
+  }
+  const double rfac = gpi ? 1.0 : 2.0;   // casadi/main.py:170-173 doubles the v1 side (quirk B5)
   // warm state back to HBM (unscaled: the next z-step restarts in identity scaling, setup_pair)
   if (qe.wraw) warm_to_scaled(qe, xs, zs, ys);
   double* qw = A.qs_e + (size_t)e * 12 * WAVE;
@@ -335,8 +407,8 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
     lw[q * WAVE + l] = lab[q];
   }
   if (l == 0) {
-    A.eres[2 * e] = 2.0 * sqrt(rr);
-    A.eres[2 * e + 1] = 2.0 * sqrt(ss);
+    A.eres[2 * e] = rfac * sqrt(rr);
+    A.eres[2 * e + 1] = rfac * sqrt(ss);
     A.dischk[e] = dchk;
     A.eflags[e] = 1;
     A.status[A.N + e] |= st;

@@ -102,6 +102,11 @@ struct DevArgs {
   int* xflags;              // N   bit 0: the x-step QP holds a warm state
   int* eflags;              // E   bit 0: the pair QP holds a warm state
   int ke_stride;            // doubles per pair in Ke_g (graph mode: room for 64 dual active-set columns)
+  // global PI (PIADMM_DUAL_PI_GLOBAL, graph mode): the pair's adaptive penalty (kept across MPC
+  // steps) and the penalty-dependent caches' keys
+  double* rho_pi;           // E   rho of the pair (casadi_old_PI_ADMM/main.py:139)
+  double* xcache_coef;      // N   x-step P coefficient 2 Pnorm + sum_e rho_e the caches were built for
+  double* ecache_rho;       // E   pair penalty the pair's polish tables were built for
 };
 
 // Big mode: rows of the per-wave x-step factor scratch (working sets of up to H + 2 rows:

@@ -33,6 +33,8 @@ class PiadmmConfigC(ctypes.Structure):
         ("polish_every", c_i32), ("device", c_i32),
         ("term_global", c_i32), ("warm_duals", c_i32), ("tighten", c_i32), ("precision", c_i32),
         ("tight_p", c_dbl), ("avg_delay", c_dbl), ("var_delay", c_dbl),
+        ("rho_num", c_dbl), ("rho_min", c_dbl), ("rho_max", c_dbl), ("no_collision_gate", c_i32),
+        ("reserved0", c_i32),
     ]
 
 

@@ -19,6 +19,7 @@ import math
 # dual-update modes
 DUAL_PLAIN = 0      # lam += rho*(p - hat)            casadi/main.py:161-162
 DUAL_PI = 1         # per-edge PI + back-calculation   ADMM_CVX_..._PI_antiwindup.m:156-188
+DUAL_PI_GLOBAL = 2  # PI with adaptive rho and K_P     casadi_old_PI_ADMM/main.py:133-151
 
 # position model used for pos_old (quirk B15)
 POS_LINEAR = 0      # Python dynamic_update_local (heading frozen)   casadi/PI_ADMM_class.py:59-69
@@ -67,6 +68,13 @@ class PIADMMConfig:
     var_delay: float = 0.025    # VehicleConfig.var_delay  (veh_config.py:26)
     precision: int = 0          # 1: ADMM matrices K_s^-1 in fp32 (mixed precision; the polish and its
                                 #    certificate stay fp64, so answers do not change) -- configs[4] study
+    # --- global PI with adaptive rho and K_P (casadi_old_PI_ADMM/main.py:133-151) ---
+    rho_num: float = 4.0        # rho = max(rho_min, min(rho_max, rho_num / dis_min))   (:139)
+    rho_min: float = 1.0
+    rho_max: float = 5.0
+    no_collision_gate: int = 0  # 1: every candidate pair's QP every iteration (the script has no
+                                #    collision test: its edge problem is solved unconditionally, :96-115)
+    reserved0: int = 0
     # --- inner QP solver (build's own; not in the reference) ---
     admm_rho: float = 0.05      # ADMM penalty in the Ruiz-scaled space (tools/qp_sim.py sweep)
     admm_sigma: float = 1e-6
@@ -105,4 +113,20 @@ def matlab_pi(**kw) -> PIADMMConfig:
     return base.replace(**kw)
 
 
-PRESETS = {"casadi_default": casadi_default, "matlab_pi": matlab_pi}
+def casadi_old_pi(**kw) -> PIADMMConfig:
+    """``casadi_old_PI_ADMM/main.py`` + its ``PI_ADMM_class.py:15-28``: the
+    global PI law with adaptive rho and K_P (:133-151), the reference's QP costs (the script solves
+    them with IPOPT, :78,114 -- convex QPs, so the same minimisers), no collision gate, aliased
+    dual residual (:161), stop with dis_vec[1] > dis_thres (:156).  Build decision:
+    the edge controls are rounded to 4 decimals like casadi/main.py:153 (the script's
+    np.around without decimals, :120, rounds |u| <= pi/6 to 0, which is taken as a typo)."""
+    base = PIADMMConfig(
+        H=5, max_outer=100, dt=0.1, L=1.0, dis_thres=1.5, beta=1e4, Pnorm=5.0, Pcost=1.0,
+        rho=1.0, eps_pri=1.0, eps_dual=1.0, dual_mode=DUAL_PI_GLOBAL, windup=1, kP=0.0, kI=3.0,
+        theta1=5.0, theta2=2.5, windup_sat=20.0, round_decimals=4, collide_sq_thres=0,
+        alias_dual_residual=1, pos_model=POS_LINEAR, term_dist_check=1, rho_num=4.0, rho_min=1.0,
+        rho_max=5.0, no_collision_gate=1)
+    return base.replace(**kw)
+
+
+PRESETS = {"casadi_default": casadi_default, "matlab_pi": matlab_pi, "casadi_old_pi": casadi_old_pi}

@@ -50,6 +50,7 @@ enum {
 /* dual_mode */
 #define PIADMM_DUAL_PLAIN 0  /* lam += rho (p - hat)            casadi/main.py:161-162 */
 #define PIADMM_DUAL_PI 1     /* per-edge PI + back-calculation  ADMM_CVX_..._PI_antiwindup.m:156-188 */
+#define PIADMM_DUAL_PI_GLOBAL 2  /* PI with adaptive rho and K_P   casadi_old_PI_ADMM/main.py:133-151 */
 
 /* status_out codes per agent / pair (bit flags accumulated over one MPC step) */
 #define PIADMM_QP_OK 0
@@ -88,6 +89,14 @@ typedef struct piadmm_config {
   int32_t precision;         /* 0: fp64; 1: ADMM iteration matrices K_s^-1 stored fp32 (half the LDS),
                                 polish and certificate fp64 -- answers unchanged (configs[4] study) */
   double tight_p, avg_delay, var_delay;   /* VehicleConfig prob / avg_delay / var_delay (veh_config.py:25-27) */
+  /* ABI 3: PIADMM_DUAL_PI_GLOBAL (casadi_old_PI_ADMM/main.py:133-151), per pair from the minimum
+   * distance d of the x-step plans (nonlinear rollouts): rho = clamp(rho_num / d, rho_min, rho_max)
+   * (penalty of the next x-steps and pair QPs, kept across MPC steps), K_P = min(theta1 / d,
+   * theta2), lam = S + K_P e, S += kI e + 2 D, saturation +-windup_sat with back-calculation D */
+  double rho_num, rho_min, rho_max;
+  int32_t no_collision_gate; /* 1: every candidate pair runs its pair QP every iteration (the
+                                global-PI script solves the edge problem unconditionally) */
+  int32_t reserved0;
 } piadmm_config_t;
 
 typedef struct piadmm_ctx* piadmm_handle_t;

@@ -135,7 +135,8 @@ def xstep_qp(cfg, xt_i, s_i, ref_i, nbr_terms):
     J(u) = Pnorm||c+Mu-r||^2 + ||D2 u||^2 + rho/2 sum_j ||c+Mu-hat_ij+lam_ij||^2 + Pcost||u||^2
     -> P = (2 Pnorm + rho |N|) M'M + 2 D2'D2 + 2 Pcost I,
        q = M'(2 Pnorm (c - r) + rho sum_j (c - hat_ij + lam_ij)).
-    ``nbr_terms`` is a list of (hat_ij, lam_ij), each (2, H+1).
+    ``nbr_terms`` is a list of (hat_ij, lam_ij), each (2, H+1), or (hat_ij, lam_ij, rho_ij) with a
+    per-pair penalty (global PI, ``casadi_old_PI_ADMM/main.py:139``: rho |N| becomes sum_j rho_ij).
     """
     H = cfg.H
     c, M = rollout_affine(xt_i, s_i, cfg.dt, cfg.L, H)
@@ -145,16 +146,22 @@ def xstep_qp(cfg, xt_i, s_i, ref_i, nbr_terms):
     for k in range(H - 2):
         D2[k, k:k + 3] = (1.0, -2.0, 1.0)
     nN = len(nbr_terms)
-    P = (2.0 * cfg.Pnorm + cfg.rho * nN) * (Mf.T @ Mf) + 2.0 * (D2.T @ D2) + 2.0 * cfg.Pcost * np.eye(H)
+    rhos = [t[2] if len(t) > 2 else cfg.rho for t in nbr_terms]
+    rsum = cfg.rho * nN
+    if any(len(t) > 2 for t in nbr_terms):
+        rsum = 0.0
+        for r in rhos:
+            rsum = rsum + r
+    P = (2.0 * cfg.Pnorm + rsum) * (Mf.T @ Mf) + 2.0 * (D2.T @ D2) + 2.0 * cfg.Pcost * np.eye(H)
     v = 2.0 * cfg.Pnorm * (cf - ref_i.reshape(-1))
-    for hat, lam in nbr_terms:
-        v = v + cfg.rho * (cf - hat.reshape(-1) + lam.reshape(-1))
+    for t, r in zip(nbr_terms, rhos):
+        v = v + r * (cf - t[0].reshape(-1) + t[1].reshape(-1))
     q = Mf.T @ v
     A, lo, hi = box_rate_rows(H, cfg.u_max, cfg.du_max)
     return P, q, A, lo, hi
 
 
-def edge_qp(cfg, xt1, s1, xt2, s2, p1, p2, lam1, lam2, seed1, seed2, d_eff=None):
+def edge_qp(cfg, xt1, s1, xt2, s2, p1, p2, lam1, lam2, seed1, seed2, d_eff=None, rho=None):
     """Pair z-step of ``cost_function_edge`` (``PI_ADMM_class.py:145-169``), slack form.
 
     Heading frozen at xt (MATLAB symbolic branch ``ADMM_CVX_...:378-397``, quirk B3) so
@@ -164,6 +171,7 @@ def edge_qp(cfg, xt1, s1, xt2, s2, p1, p2, lam1, lam2, seed1, seed2, d_eff=None)
     dis_k = 2 dbar'(e_2k - e_1k) - ||dbar||^2, k = 1..H, dbar = seed_2 - seed_1.
     """
     H = cfg.H
+    rho = cfg.rho if rho is None else rho     # the pair's adaptive penalty (global PI)
     c1, M1 = rollout_affine(xt1, s1, cfg.dt, cfg.L, H)
     c2, M2 = rollout_affine(xt2, s2, cfg.dt, cfg.L, H)
     dbar = np.asarray(seed2, np.float64) - np.asarray(seed1, np.float64)
@@ -175,8 +183,8 @@ def edge_qp(cfg, xt1, s1, xt2, s2, p1, p2, lam1, lam2, seed1, seed2, d_eff=None)
         Mf = M.reshape(2 * (H + 1), H)
         b = p.reshape(-1) + lam.reshape(-1) - c.reshape(-1)
         sl = slice(v * H, (v + 1) * H)
-        P[sl, sl] = cfg.rho * (Mf.T @ Mf) + 2.0 * cfg.Pcost * np.eye(H)
-        q[sl] = -cfg.rho * (Mf.T @ b)
+        P[sl, sl] = rho * (Mf.T @ Mf) + 2.0 * cfg.Pcost * np.eye(H)
+        q[sl] = -rho * (Mf.T @ b)
     q[2 * H:] = cfg.beta
     Ab, lob, hib = box_rate_rows(H, cfg.u_max, cfg.du_max)
     m1 = Ab.shape[0]
@@ -215,8 +223,8 @@ def solve_xstep(cfg, xt_i, s_i, ref_i, nbr_terms):
     return x, (P, q, A, lo, hi, y)
 
 
-def solve_edge(cfg, xt1, s1, xt2, s2, p1, p2, lam1, lam2, seed1, seed2, d_eff=None):
-    P, q, A, lo, hi = edge_qp(cfg, xt1, s1, xt2, s2, p1, p2, lam1, lam2, seed1, seed2, d_eff)
+def solve_edge(cfg, xt1, s1, xt2, s2, p1, p2, lam1, lam2, seed1, seed2, d_eff=None, rho=None):
+    P, q, A, lo, hi = edge_qp(cfg, xt1, s1, xt2, s2, p1, p2, lam1, lam2, seed1, seed2, d_eff, rho)
     H = cfg.H
     x0 = np.zeros(3 * H)
     x0[2 * H:] = np.maximum(0.0, lo[-H:])          # feasible: s = max(0, g(0))
@@ -316,6 +324,9 @@ class Oracle:
             self.nbrs[a].sort()
         self.t = 0
         self.edge_state = None      # (hat, lam, S, D, last_hat) after the last step (warm_duals)
+        # global PI: the pair's adaptive penalty, kept across MPC steps like PI_ADMM.param.rho
+        # (casadi_old_PI_ADMM/main.py:139 is never reset)
+        self.rho_pi = np.full(self.E, float(cfg.rho))
 
     def seeds(self):
         """``casadi/main.py:48-49``."""
@@ -377,10 +388,12 @@ class Oracle:
                 for c in gcomps:
                     iters[c] = it + 1
                 # ---- x-step, casadi/main.py:81-106
+                gpi = cfg.dual_mode == 2
                 for i in agents:
                     if not own(i):
                         continue          # a ghost: its owner rank solves it (exchange below)
-                    terms = [(hat[e, d], lam[e, d]) for (_, e, d) in self.nbrs[i]]
+                    terms = [(hat[e, d], lam[e, d], self.rho_pi[e]) if gpi else (hat[e, d], lam[e, d])
+                             for (_, e, d) in self.nbrs[i]]
                     u_star, _ = solve_xstep(cfg, self.xt[i], self.scn.spd[i],
                                             self.scn.ref[i, :, t:t + H + 1], terms)
                     u = around(u_star, cfg.round_decimals)
@@ -393,18 +406,22 @@ class Oracle:
                 # ---- collision graph, casadi/main.py:110-118
                 for e in edges:
                     v1, v2 = self.scn.edges[e]
-                    active[e] = collides(cfg, pos_old[v1], pos_old[v2], d_eff[e])
+                    active[e] = True if cfg.no_collision_gate else collides(cfg, pos_old[v1], pos_old[v2], d_eff[e])
                 act = [e for e in edges if active[e]]
                 # ---- z-step + dual update, casadi/main.py:121-162 (none when no pair is active)
                 for e in act:
                     v1, v2 = (int(a) for a in self.scn.edges[e])
                     uh, _ = solve_edge(cfg, self.xt[v1], self.scn.spd[v1], self.xt[v2], self.scn.spd[v2],
                                        pos_old[v1], pos_old[v2], lam[e, 0], lam[e, 1], seeds[v1], seeds[v2],
-                                       d_eff[e])
+                                       d_eff[e], self.rho_pi[e] if gpi else None)
                     uh = around(uh, cfg.round_decimals)
                     for d, v in enumerate((v1, v2)):
                         hx, hy, _ = rollout_nonlinear(self.xt[v], uh[d], self.scn.spd[v], cfg.dt, cfg.L)
                         hat[e, d, 0], hat[e, d, 1] = hx, hy
+                    if gpi:
+                        dis_chk[e] = dual_update_global_pi(cfg, self.xt, self.scn.spd, self.primal_u, v1, v2,
+                                                           pos_old, hat[e], lam[e], S[e], D[e], self.rho_pi, e)
+                        continue
                     dvec = pos_old[v1] - pos_old[v2]
                     dist = np.sqrt(np.sum(dvec * dvec, axis=0))
                     dual_update(cfg, pos_old[v1], pos_old[v2], hat[e], lam[e], S[e], D[e], dist)
@@ -416,7 +433,12 @@ class Oracle:
                     for e in self.comp_edges[c]:
                         if not active[e] or not cnt(e):
                             continue
-                        rk_e, sk_e = pair_residuals(cfg, pos_old[int(self.scn.edges[e, 0])], hat[e, 0], last_hat[e, 0])
+                        v1, v2 = (int(a) for a in self.scn.edges[e])
+                        if gpi:
+                            rk_e, sk_e = pair_residuals_global_pi(pos_old[v1], pos_old[v2], hat[e], last_hat[e],
+                                                                  self.rho_pi[e])
+                        else:
+                            rk_e, sk_e = pair_residuals(cfg, pos_old[v1], hat[e, 0], last_hat[e, 0])
                         if not g_alias[g]:
                             sk += sk_e
                         rk += rk_e
@@ -487,3 +509,44 @@ def dual_update(cfg, p1, p2, hat_e, lam_e, S_e, D_e, dist):
                 D_e[d] = lam_e[d] - orig
             else:
                 D_e[d] = 0.0
+
+
+def dual_update_global_pi(cfg, xt, spd, primal_u, v1, v2, pos_old, hat_e, lam_e, S_e, D_e, rho_pi, e):
+    """Global PI with adaptive rho and K_P (``casadi_old_PI_ADMM/main.py:133-151``) for one pair,
+    in place.  d = the pair's distances along the nonlinear rollouts of the x-step controls
+    (``x_curr_pred``, :133-137); K_P = min(theta1/d_min, theta2) (:138, 5 and 2.5), the penalty
+    rho = max(rho_min, min(rho_max, rho_num/d_min)) (:139); lam = S + K_P e, S += K_I e + 2 D
+    (:143-144, S before its update); saturation with back-calculation over the pair (:147-153,
+    ``np.sum(orig != sat) > 0`` over the whole dual array).  Returns dis_vec[1] (the stop
+    check, :156)."""
+    x1, y1, _ = rollout_nonlinear(xt[v1], primal_u[v1], spd[v1], cfg.dt, cfg.L)
+    x2, y2, _ = rollout_nonlinear(xt[v2], primal_u[v2], spd[v2], cfg.dt, cfg.L)
+    dx, dy = x1 - x2, y1 - y2
+    dist = np.sqrt(dx * dx + dy * dy)
+    dmin = np.min(dist)
+    kP = min(cfg.theta1 / dmin, cfg.theta2)
+    rho_pi[e] = max(cfg.rho_min, min(cfg.rho_max, cfg.rho_num / dmin))
+    raw = np.empty_like(lam_e)
+    for d, v in enumerate((v1, v2)):
+        err = pos_old[v] - hat_e[d]
+        raw[d] = S_e[d] + kP * err
+        S_e[d] = S_e[d] + cfg.kI * err + 2.0 * D_e[d]
+    if cfg.windup:
+        W = cfg.windup_sat
+        sat = np.minimum(W, np.maximum(raw, -W))
+        D_e[...] = (sat - raw) if np.sum(raw != sat) > 0 else 0.0
+        lam_e[...] = sat
+    else:
+        lam_e[...] = raw
+    return dist[1]
+
+
+def pair_residuals_global_pi(p_v1, p_v2, hat_e, last_e, rho):
+    """One pair's terms of ``casadi_old_PI_ADMM/main.py:153-154``: (primal, dual) =
+    (|[p_1; p_2] - [hat_12; hat_21]|_F, |rho ([last_12; last_21] - [hat_12; hat_21])|_F) -- both
+    sides, no factor 2 (unlike casadi/main.py:170-173), rho the pair's updated penalty."""
+    pos = np.concatenate([p_v1, p_v2])                 # (4, H+1): the script's 2N x (H+1) layout
+    hat = hat_e.reshape(4, -1)
+    sk = np.sqrt(np.sum((rho * (last_e.reshape(4, -1) - hat)) ** 2))
+    rk = np.sqrt(np.sum((pos - hat) ** 2))
+    return rk, sk
