@@ -11,13 +11,18 @@ intersection, inputs resident in HBM before the timed region):
                sees per MPC step)
   --config2    configs[1]: 64 agents x H20, casadi_default, fixed 200 outer iterations (C2)
   --config5    configs[4]: 256 agents x H50 with delay tightening
-  --strong     configs[3]: 1024 agents x H30 in total, sharded over the N ranks (strong scaling)
+  --strong     configs[3]: 1024 agents x H30 in total, sharded over the N ranks (strong scaling);
+               --split interleaved puts the two agents of every tile on different ranks (SURVEY.md
+               8d C4 "adversarial": every pair crosses ranks, one all-reduce of the boundary
+               exchange buffer per outer iteration)
+  --crossing   coupling-heavy: 64 four-vehicle all-pairs crossings (256 agents, 384 candidate
+               pairs, H30) on the graph kernel -- pairs stay active for many outer iterations
 
 One "step" = one MPC step of the full loop (x-step QPs of all agents, collision graph, pair
 z-step QPs, PI + back-calculation dual update, residuals) plus propagation; the library's MPC
 loop never returns to the host inside the timed region.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config2 | --config5 | --strong] [--natural]
+  python bench.py [--gpus N --steps K --warmup W] [--config2 | --config5 | --strong [--split interleaved] | --crossing] [--natural]
 
 N > 1: one process per GPU (torch.distributed.run).  Run directly with --gpus N and no
 WORLD_SIZE in the environment, this script starts ``torch.distributed.run --nproc-per-node N``
@@ -57,6 +62,9 @@ WORKLOADS = {
                desc="256 agents x H50 per GPU (128 tiles), matlab_pi + delay tightening p=0.95"),
     "c4": dict(tiles=512, H=30, preset="matlab_pi", max_outer=100, tighten=0, scaling="strong",
                desc="1024 agents x H30 in total (512 tiles) sharded over the GPUs, matlab_pi preset"),
+    "x4": dict(tiles=64, H=30, preset="matlab_pi", max_outer=100, tighten=0, scaling="weak", kind="crossing",
+               desc="256 agents x H30 per GPU (64 four-vehicle all-pairs crossings, 384 candidate pairs), "
+                    "matlab_pi preset"),
 }
 
 
@@ -109,18 +117,17 @@ def latest_profile(kind: str, workload: str):
 
 
 def cpu_baseline(wl: dict, budget_s: float) -> dict:
-    """The CPU baseline on this host: the B-opt C++ / OpenMP build of the loop when it is built
-    (oracle/cpu_ref, all host cores), else the NumPy oracle on one core (bounded sample)."""
+    """The CPU baseline on this host, timed BEFORE anything touches the GPU: the oracle over a
+    pool of processes on all host cores (oracle/cpu_parallel.py), else on one core."""
     sys.path.insert(0, ROOT)
     from piadmm import config, scenario
     n_tiles, H = wl["tiles"], wl["H"]
     cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=1, max_outer=wl["max_outer"], tighten=wl["tighten"])
     try:
-        from oracle import cpu_ref
-        if cpu_ref.available():
-            return cpu_ref.time_baseline(cfg, n_tiles, budget_s)
-    except ImportError:
-        pass
+        from oracle import cpu_parallel
+        return cpu_parallel.time_baseline(cfg, n_tiles, budget_s)
+    except Exception as e:          # noqa: BLE001 -- fall back to the one-core sample below
+        print(f"bench.py: parallel CPU baseline failed ({e}); one core instead", file=sys.stderr)
     from oracle import piadmm_oracle as O
     try:
         from threadpoolctl import threadpool_limits
@@ -151,7 +158,7 @@ def cpu_baseline(wl: dict, budget_s: float) -> dict:
                       f"host {platform.processor() or platform.machine()}, {os.cpu_count()} cpus visible"}
 
 
-def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_rank: int, dist):
+def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_rank: int, dist, split="components"):
     """Time K MPC steps of workload wl on this rank; returns (metrics, counters, solver info)."""
     from piadmm import config, scenario
     from piadmm import dist as pdist
@@ -160,11 +167,19 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
     cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=0 if natural else 1, max_outer=M, term_global=1,
                                        tighten=wl["tighten"])
     n_steps = max(K, W, 1)
+    shard = None
     if wl["scaling"] == "strong":
-        scn = pdist.shard(scenario.tiled(wl["tiles"], H, n_steps=n_steps, perturb=True, seed=0), rank, world)
+        full = scenario.tiled(wl["tiles"], H, n_steps=n_steps, perturb=True, seed=0)
+        if split == "interleaved":
+            shard = pdist.shard_graph(full, rank, world, pdist.owners_interleaved(full.n_agents, world))
+            scn = shard.scn
+        else:
+            scn = pdist.shard(full, rank, world)
+    elif wl.get("kind") == "crossing":
+        scn = scenario.concat([scenario.crossing(4, H, n_steps=n_steps, seed=1000 * rank + k) for k in range(wl["tiles"])])
     else:
         scn = scenario.tiled(wl["tiles"], H, n_steps=n_steps, perturb=True, seed=1000 * rank)
-    solver = PI_ADMM_MI355X(cfg, scn, device=local_rank)
+    solver = PI_ADMM_MI355X(cfg, scn, device=local_rank, shard=shard)
     try:
         if dist is not None:
             def bcast(b):
@@ -189,7 +204,9 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
         if dist is not None:
             dist.barrier()
         cnt = solver.counters()
-        spl, C, N = solver.steps_per_launch(), max(solver.C, 1), solver.N
+        spl, C = solver.steps_per_launch(), max(solver.C, 1)
+        N = int(shard.owned.sum()) if shard is not None else solver.N
+        xchg = shard is not None and shard.n_slots > 0
     finally:
         solver.close()
     if dist is not None:
@@ -198,10 +215,16 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, ev_ms = float(tt[0]), float(tt[1])
     job_iters = cnt["outer_iters"] / C                  # iterations of the job (every component runs them)
-    # k_mpc_step launches in the timed region: one persistent launch per steps_per_launch() steps,
-    # or (natural termination across ranks) one per outer iteration plus one per step
-    n_launch = -(-K // spl) if spl > 1 else int(job_iters) + K
-    return dict(wall=wall, ev_ms=ev_ms, job_iters=job_iters, n_launch=n_launch, spl=spl, N=N, C=C), cnt
+    # step-kernel launches in the timed region: one persistent launch per steps_per_launch() steps,
+    # or (natural termination across ranks) one per outer iteration plus one per step, or (pairs
+    # across ranks) an X and a Z launch per outer iteration plus one per step
+    if xchg:
+        n_launch = 2 * int(job_iters) + K
+    else:
+        n_launch = -(-K // spl) if spl > 1 else int(job_iters) + K
+    graph = xchg or wl.get("kind") == "crossing"
+    return dict(wall=wall, ev_ms=ev_ms, job_iters=job_iters, n_launch=n_launch, spl=spl, N=N, C=C, xchg=xchg,
+                kernel="pd::k_graph_step" if graph else "pd::k_mpc_step"), cnt
 
 
 def main():
@@ -217,6 +240,9 @@ def main():
     g.add_argument("--config2", action="store_true", help="BASELINE configs[1]: 64 agents x H20")
     g.add_argument("--config5", action="store_true", help="BASELINE configs[4]: H=50 with delay tightening")
     g.add_argument("--strong", action="store_true", help="BASELINE configs[3]: 1024 agents sharded over N GPUs")
+    g.add_argument("--crossing", action="store_true", help="coupling-heavy: 64 four-vehicle all-pairs crossings")
+    ap.add_argument("--split", choices=("components", "interleaved"), default="components",
+                    help="--strong: whole tiles per rank, or every tile across two ranks (boundary exchange)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "0"))
@@ -228,6 +254,13 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    key = "c2" if args.config2 else "c5" if args.config5 else "c4" if args.strong else "x4" if args.crossing else "c3"
+    wl = WORKLOADS[key]
+    # the CPU baseline first, on the host cores, before this process touches the GPU (its worker
+    # pool is started with the spawn method)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and wl.get("kind") != "crossing":
+        cpu = cpu_baseline(wl, args.cpu_budget)
 
     from piadmm import _lib
     lib = _lib.load()                       # HIP runtime loaded before torch (same SONAME)
@@ -236,11 +269,9 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    key = "c2" if args.config2 else "c5" if args.config5 else "c4" if args.strong else "c3"
-    wl = WORKLOADS[key]
     H, M = wl["H"], wl["max_outer"]
     K, W = args.steps, args.warmup
-    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist)
+    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist, args.split)
 
     # value = units all ranks processed / the max-over-ranks wall time.  Weak scaling: one unit =
     # one outer iteration of a rank's (256-agent) block, so all ranks processed world x job
@@ -251,7 +282,8 @@ def main():
     avg_launch_s = (m["ev_ms"] / 1e3) / m["n_launch"]
     bytes_launch = algorithmic_bytes(cnt, H) / m["n_launch"]
     achieved = bytes_launch / avg_launch_s / 1e9
-    wname = f"tiled{wl['tiles']}_H{H}_{wl['preset']}_fixed{M}" + ("_tight" if wl["tighten"] else "")
+    wname = f"{'crossing4x' if wl.get('kind') == 'crossing' else 'tiled'}{wl['tiles']}_H{H}_{wl['preset']}_fixed{M}" + (
+        "_tight" if wl["tighten"] else "")
     traffic = latest_profile("traffic", wname) if not args.natural else None
     traffic_launch = traffic["hbm_bytes_per_step"] * K / m["n_launch"] if traffic else None
     sq = latest_profile("sq", wname) if not args.natural else None
@@ -277,7 +309,9 @@ def main():
             "outer_iters_per_step": m["job_iters"] / K,
             "job_outer_iters_per_s": m["job_iters"] / m["wall"],
             "agent_qps_per_s": cnt["x_qps"] * world / m["wall"],
-            "parallelism": f"components sharded over {world} GPU(s); " + (
+            "parallelism": (f"agents sharded over {world} GPU(s), every tile across two ranks: one all-reduce of "
+                            f"the boundary exchange buffer per outer iteration + " if m["xchg"] else
+                            f"components sharded over {world} GPU(s); ") + (
                 ("one RCCL all-reduce of the termination partials per outer iteration" if world > 1 else
                  "stop test in-kernel behind a grid barrier (cooperative launch)") if args.natural else
                 "one RCCL all-reduce of the residual history per persistent launch") + (
@@ -286,7 +320,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS, "traffic": traffic_launch,
-            "kernel": "pd::k_mpc_step", "avg_launch_ms": avg_launch_s * 1e3,
+            "kernel": m["kernel"], "avg_launch_ms": avg_launch_s * 1e3,
             "steps_per_launch": m["spl"], "launches": m["n_launch"],
             "algorithmic_bytes_per_launch": bytes_launch,
             "traffic_source": traffic["_file"] if traffic else None,
@@ -325,7 +359,7 @@ def main():
     line["latency"] = lat
 
     if not args.natural and not args.no_natural:
-        mn, cn = run(wl, True, K, W, rank, world, local_rank, dist)
+        mn, cn = run(wl, True, K, W, rank, world, local_rank, dist, args.split)
         line["natural"] = {
             "ms_per_step": mn["wall"] / K * 1e3,
             "outer_iters_per_step": mn["job_iters"] / K,
@@ -334,9 +368,9 @@ def main():
             "steps_per_launch": mn["spl"],
             "note": "same workload, the reference's stop test on (casadi/main.py:174-178): the per-step latency",
         }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
-        line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
+        line["speedup_vs_cpu_baseline"] = value / cpu["value"]
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -13,7 +13,7 @@ import shutil
 import sys
 
 out, tag = sys.argv[1], sys.argv[2]
-steps_per_launch = int(sys.argv[3]) if len(sys.argv) > 3 else 10   # bench.py default: 10-step launches
+steps_per_launch = int(sys.argv[3]) if len(sys.argv) > 3 else 20   # bench.py default: the timed 20-step launch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -33,11 +33,14 @@ if stats:
 
 
 def pmc(name):
-    vals = []
+    """The counter summed over the timed launch (the last k_mpc_step dispatch: bench.py
+    --no-natural runs the warmup launch, then the timed one)."""
+    per = {}
     for r in rows(os.path.join(name.lower().split("_")[0], "**", "*counter_collection.csv")):
         if "k_mpc_step" in r.get("Kernel_Name", "") and r.get("Counter_Name") == name:
-            vals.append(float(r["Counter_Value"]))
-    return vals
+            d = int(r["Dispatch_Id"])
+            per[d] = per.get(d, 0.0) + float(r["Counter_Value"])
+    return [per[max(per)]] if per else []
 
 
 fetch = pmc("FETCH_SIZE")
