@@ -38,6 +38,7 @@ struct GWave {
   double* vb;      // LDS vectors (512)
   double* xdiag;   // LDS x factor diagonals (128)
   double* zdiag;   // LDS pair factor diagonals (128)
+  double* ylds;    // LDS dual active-set columns (H <= HMAX), nullptr: HBM (big mode)
   int *xids, *zids, *xfs, *zfs;
 };
 
@@ -76,8 +77,9 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GW
   qx.mmax = xrows(H);
   qx.gws = nullptr;
   qx.tstep = t;
-  qx.Y = A.Yx_g + (size_t)a * WAVE * H;
-  qx.ycap = A.x_gi ? WAVE : 0;
+  // the dual active set's columns: LDS when they fit (H <= HMAX), else the agent's HBM buffer
+  qx.Y = W.ylds ? W.ylds : A.Yx_g + (size_t)a * WAVE * H;
+  qx.ycap = A.x_gi ? (W.ylds ? GYCAP : WAVE) : 0;
   qx.y_in_k = false;
   if (l == 0) W.xfs[0] = -1;                 // the wave's scratch served another QP before
   wsync();
@@ -232,9 +234,10 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
   qe.xld = 0;
   qe.G = nullptr;
   qe.XT = nullptr;
-  qe.Y = Ke;
-  qe.ycap = A.pair_gi ? min(WAVE, A.ke_stride / (2 * H)) : 0;
-  qe.y_in_k = true;
+  // the dual active set's columns in LDS (H <= HMAX); big mode: in the pair's K_s^-1 region
+  qe.Y = W.ylds ? W.ylds : Ke;
+  qe.ycap = A.pair_gi ? (W.ylds ? GYCAP : min(WAVE, A.ke_stride / (2 * H))) : 0;
+  qe.y_in_k = W.ylds == nullptr;
   qe.gws = A.gi_ws + (size_t)e * GI_WS;
   qe.tstep = t;
   qe.csig = -1;
@@ -516,12 +519,14 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   size_t fac_n = 64 * LD;
   const size_t xr = (size_t)xrows(H) * (xrows(H) + 1);
   if (xr > fac_n) fac_n = xr;
-  double* wbase = lds + (size_t)w * (fac_n + 512 + 256);
+  const size_t ylds_n = graph_ylds(H);
+  double* wbase = lds + (size_t)w * (fac_n + 512 + 256 + ylds_n);
   GWave W;
   W.fac = wbase;
   W.vb = wbase + fac_n;
   W.xdiag = W.vb + 512;
   W.zdiag = W.xdiag + 128;
+  W.ylds = ylds_n ? W.zdiag + 128 : nullptr;
   W.xids = s_int + w * 272;
   W.zids = W.xids + 128;
   W.xfs = W.xids + 256;

@@ -159,11 +159,15 @@ constexpr int F_COOP = 16;    // global termination decided in-kernel (cooperati
 
 // Graph mode: LDS per workgroup of k_graph_step (GW waves, one component per workgroup).
 constexpr int GW = 2;
+// Dual active-set columns P^-1 n_a in LDS per wave (H <= HMAX; beyond, in HBM): the pair's
+// 2H-long columns (63 of them) or the x-step's H-long ones, in turn.
+constexpr int GYCAP = 63;
+constexpr size_t graph_ylds(int H) { return H <= HMAX ? (size_t)GYCAP * 2 * H : 0; }
 inline size_t graph_lds_bytes(int H) {
   size_t fac = 64 * LD;                                   // pair factor scratch (largest)
   const size_t xr = (size_t)xrows(H) * (xrows(H) + 1);    // x-step factor scratch (same region)
   if (xr > fac) fac = xr;
-  return (GW * (fac + 512 + 256) + 64) * sizeof(double);  // + vectors, factor diagonals; scalars
+  return (GW * (fac + 512 + 256 + graph_ylds(H)) + 64) * sizeof(double);  // + vectors, diagonals, Y
 }
 // Graph launches also use these flags: F_XPHASE / F_ZPHASE restrict an iteration launch to
 // its x-step or its z-step + termination half (the exchange of a sharded job sits between).

@@ -72,12 +72,12 @@ def test_chain_graph(Solver):
 @pytest.mark.parametrize("H", [10, 30, 40])
 def test_mixed_components_and_horizons(Solver, H):
     """Components of 4 (all pairs), 3 (chain), 2 and 1 agents side by side, per-component
-    termination; H = 40 takes the two-columns-per-lane pair K path (big mode) with a 3-vehicle
-    all-pairs crossing in place of the 4-vehicle one, whose saturated pair QPs need working sets
-    beyond the 63-row capacity (see test_working_set_capacity_is_reported)."""
+    termination; H = 40 takes the two-columns-per-lane pair K path (big mode) with two tiles of
+    the intersection in place of the all-pairs crossing, whose saturated pair QPs at H = 40 need
+    working sets beyond the 63-row capacity (see test_working_set_capacity_is_reported)."""
     big = H > 32
-    scn = scenario.concat([scenario.crossing(3 if big else 4, H, n_steps=14, seed=1),
-                           scenario.crossing(3, H, n_steps=14, pairs="chain"),
+    first = scenario.tiled(2, H, n_steps=14, seed=3) if big else scenario.crossing(4, H, n_steps=14, seed=1)
+    scn = scenario.concat([first, scenario.crossing(3, H, n_steps=14, pairs="chain"),
                            scenario.intersection(H, n_steps=14), scenario.crossing(1, H, n_steps=14)])
     compare(Solver, config.matlab_pi(H=H), scn, 8 if big else 12)
 
