@@ -846,6 +846,100 @@ int32_t piadmm_global_resid(piadmm_handle_t h, double* resid_out, int32_t* iters
   return PIADMM_OK;
 }
 
+// Candidate pairs on a uniform grid hash (piadmm_detect.hip; casadi/main.py:110-113 at O(N)).
+int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double* radius, int32_t n,
+                               int32_t* pairs_out, int32_t max_pairs, int32_t* n_pairs_out, float* ms_out) {
+  if (!h || !n_pairs_out || (n > 0 && (!xy || !radius))) return fail(h, PIADMM_E_ARG, "null argument");
+  if (n < 0 || n > (1 << 25)) return fail(h, PIADMM_E_ARG, "n must be in [0, 2^25]");
+  if (max_pairs < 0 || (max_pairs > 0 && !pairs_out)) return fail(h, PIADMM_E_ARG, "bad pairs_out / max_pairs");
+  *n_pairs_out = 0;
+  if (ms_out) *ms_out = 0.0f;
+  if (n == 0) return PIADMM_OK;
+  double rmax = 0.0;
+  for (int i = 0; i < n; ++i) {
+    if (!std::isfinite(xy[2 * i]) || !std::isfinite(xy[2 * i + 1]) || !std::isfinite(radius[i]) || radius[i] < 0)
+      return fail(h, PIADMM_E_ARG, "positions and radii must be finite, radii >= 0");
+    rmax = std::max(rmax, radius[i]);
+  }
+  // cell size >= 2 max r (a candidate pair is in the same or an adjacent cell), with margin for
+  // the rounding of x / cs; buckets: a power of two >= 2n
+  const double cs = rmax > 0 ? 2.0 * rmax * (1.0 + 1e-9) : 1.0;
+  unsigned T = 1024;
+  while (T < 2u * (unsigned)n) T <<= 1;
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  hipStream_t s = h->stream;
+  std::vector<void*> tmp;
+  auto get = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr;
+    tmp.push_back(p);
+    return p;
+  };
+  auto release = [&]() {
+    (void)hipStreamSynchronize(s);
+    for (void* p : tmp) (void)hipFree(p);
+    tmp.clear();
+  };
+  double* d_xy = (double*)get((size_t)n * 2 * sizeof(double));
+  double* d_r = (double*)get((size_t)n * sizeof(double));
+  unsigned* d_key = (unsigned*)get((size_t)n * sizeof(unsigned));
+  int* d_cnt = (int*)get((size_t)T * sizeof(int));
+  int* d_fill = (int*)get((size_t)T * sizeof(int));
+  int* d_start = (int*)get(((size_t)T + 1) * sizeof(int));
+  int* d_order = (int*)get((size_t)n * sizeof(int));
+  int* d_pcnt = (int*)get((size_t)n * sizeof(int));
+  int* d_off = (int*)get(((size_t)n + 1) * sizeof(int));
+  long long* d_total = (long long*)get(sizeof(long long));
+  if (tmp.size() != 10) {
+    release();
+    return fail(h, PIADMM_E_HIP, "hipMalloc failed (candidate pairs)");
+  }
+  hipEvent_t e[4];
+  for (auto& ev : e) (void)hipEventCreate(&ev);
+  auto cleanup = [&]() {
+    release();
+    for (auto& ev : e) (void)hipEventDestroy(ev);
+  };
+  int rc = 0;
+  long long total = 0;
+  rc |= hipMemcpyAsync(d_xy, xy, (size_t)n * 2 * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess;
+  rc |= hipMemcpyAsync(d_r, radius, (size_t)n * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess;
+  rc |= hipEventRecord(e[0], s) != hipSuccess;
+  rc |= pd::launch_detect_count(d_xy, d_r, n, 1.0 / cs, T, d_key, d_cnt, d_start, d_fill, d_order, d_pcnt, d_off,
+                                d_total, s) != 0;
+  rc |= hipEventRecord(e[1], s) != hipSuccess;
+  rc |= hipMemcpyAsync(&total, d_total, sizeof(long long), hipMemcpyDeviceToHost, s) != hipSuccess;
+  rc |= hipStreamSynchronize(s) != hipSuccess;
+  if (rc) {
+    cleanup();
+    return fail(h, PIADMM_E_HIP, "candidate pairs: count phase failed");
+  }
+  if (total > 0x7fffffffll / 2) {
+    cleanup();
+    return fail(h, PIADMM_E_ARG, "candidate pairs: more than 2^30 pairs");
+  }
+  int* d_out = (int*)get((size_t)total * 2 * sizeof(int));
+  if (!d_out) {
+    cleanup();
+    return fail(h, PIADMM_E_HIP, "hipMalloc failed (candidate pairs output)");
+  }
+  rc |= hipEventRecord(e[2], s) != hipSuccess;
+  rc |= pd::launch_detect_emit(d_xy, d_r, n, 1.0 / cs, T, d_start, d_order, d_off, d_out, s) != 0;
+  rc |= hipEventRecord(e[3], s) != hipSuccess;
+  const long long ncopy = std::min<long long>(total, max_pairs);
+  if (ncopy > 0)
+    rc |= hipMemcpyAsync(pairs_out, d_out, (size_t)ncopy * 2 * sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess;
+  rc |= hipStreamSynchronize(s) != hipSuccess;
+  float m1 = 0.0f, m2 = 0.0f;
+  if (!rc && ms_out && hipEventElapsedTime(&m1, e[0], e[1]) == hipSuccess &&
+      hipEventElapsedTime(&m2, e[2], e[3]) == hipSuccess)
+    *ms_out = m1 + m2;
+  cleanup();
+  if (rc) return fail(h, PIADMM_E_HIP, "candidate pairs: emit phase failed");
+  *n_pairs_out = (int32_t)total;
+  return PIADMM_OK;
+}
+
 // Diagnostic builds only: per-component phase cycle sums (C x 32), reset with the counters.
 int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n) {
   if (!h || !out) return fail(h, PIADMM_E_ARG, "null argument");

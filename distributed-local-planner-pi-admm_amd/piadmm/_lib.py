@@ -82,6 +82,7 @@ SYMBOLS = [
     ("piadmm_set_scenario_shard", c_i32, [_H, _dp, _dp, _dp, c_i32, _ip, c_i32, _P(ctypes.c_uint8), _ip, c_i32,
                                           _P(ctypes.c_uint8)]),
     ("piadmm_set_allreduce", c_i32, [_H, ctypes.c_void_p, ctypes.c_void_p]),
+    ("piadmm_candidate_pairs", c_i32, [_H, _dp, _dp, c_i32, _ip, c_i32, _ip, _P(ctypes.c_float)]),
 ]
 
 # piadmm_allreduce_fn: int32_t (*)(void* ctx, double* buf, int64_t n)

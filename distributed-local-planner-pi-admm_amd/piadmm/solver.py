@@ -142,6 +142,25 @@ class PI_ADMM_MI355X:
         self._xfn = _lib.ALLREDUCE_FN(cb)      # kept alive as long as the handle
         self._check(self.lib.piadmm_set_allreduce(self._h, ctypes.cast(self._xfn, ctypes.c_void_p), None))
 
+    def set_candidate_graph(self, edges: np.ndarray):
+        """Replace the candidate graph between MPC steps (a dynamic graph, e.g. rebuilt from the
+        current states by piadmm.candidates): the scenario restarts from the current states with
+        the new pairs (per-pair duals and warm starts reset, as at the start of a reference step,
+        casadi/main.py:52-63)."""
+        if self.shard is not None:
+            raise ValueError("a sharded handle keeps its graph")
+        edges = np.ascontiguousarray(edges, np.int32).reshape(-1, 2)
+        self.scn = Scenario(spd=self.scn.spd, xt0=np.ascontiguousarray(self.xt, np.float64), ref=self.scn.ref,
+                            edges=edges, n_steps=self.scn.n_steps)
+        self.E = edges.shape[0]
+        flat = edges.reshape(-1)
+        self._check(self.lib.piadmm_set_scenario(self._h, _lib.dptr(np.ascontiguousarray(self.scn.spd, np.float64)),
+                                                 _lib.dptr(self.scn.xt0),
+                                                 _lib.dptr(np.ascontiguousarray(self.scn.ref, np.float64)),
+                                                 self.scn.ref.shape[2], _lib.iptr(flat) if flat.size else None,
+                                                 self.E))
+        self.C = self.lib.piadmm_n_components(self._h)
+
     def run(self, n_steps: int | None = None) -> list[StepResult]:
         n = self.scn.n_steps if n_steps is None else n_steps
         return [self.mpc_step() for _ in range(n)]

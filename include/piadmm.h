@@ -209,6 +209,17 @@ int32_t piadmm_comm_init(piadmm_handle_t h, const uint8_t* id /* 128 bytes */, i
  * executed outer iterations (equal on every rank). */
 int32_t piadmm_global_resid(piadmm_handle_t h, double* resid_out, int32_t* iters_out);
 
+/* Candidate pairs for large N: all pairs i < j of the n points
+ * xy (n x 2) with |xy_i - xy_j| <= radius_i + radius_j, in increasing (i, j) order, found on a
+ * uniform grid hash in O(n) on the handle's device (replaces the O(N^2) pair loop of
+ * casadi/main.py:110-113 as the source of the candidate graph: with radius_i = spd_i H dt +
+ * d / 2 -- piadmm.candidates.reach_radii -- no other pair can collide within the horizon).
+ * Writes min(total, max_pairs) pairs to pairs_out (max_pairs x 2) and the total to
+ * *n_pairs_out (call again with a larger buffer when total > max_pairs); ms_out (may be NULL):
+ * device time of the detection kernels, inputs resident. */
+int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double* radius, int32_t n,
+                               int32_t* pairs_out, int32_t max_pairs, int32_t* n_pairs_out, float* ms_out);
+
 /* Diagnostic builds (-DPIADMM_STAMPS, libpiadmm_stamps.so) only: per-component
  * cycle sums of the kernel phases (C x 32 uint64); PIADMM_E_STATE otherwise. */
 int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n);

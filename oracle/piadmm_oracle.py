@@ -550,3 +550,23 @@ def pair_residuals_global_pi(p_v1, p_v2, hat_e, last_e, rho):
     sk = np.sqrt(np.sum((rho * (last_e.reshape(4, -1) - hat)) ** 2))
     rk = np.sqrt(np.sum((pos - hat) ** 2))
     return rk, sk
+
+
+def candidate_pairs(xy, radius, block=2048):
+    """All pairs i < j with |xy_i - xy_j|^2 <= (r_i + r_j)^2 in (i, j) order -- the brute-force
+    statement of the candidate graph (the all-pairs loop of casadi/main.py:110-113 over the
+    reach discs; checker of piadmm_candidate_pairs), same fp64 operations as the kernel."""
+    xy = np.asarray(xy, np.float64).reshape(-1, 2)
+    r = np.asarray(radius, np.float64).reshape(-1)
+    n = xy.shape[0]
+    out = []
+    for a in range(0, n, block):
+        i = np.arange(a, min(n, a + block))
+        dx = xy[None, :, 0] - xy[i, None, 0]
+        dy = xy[None, :, 1] - xy[i, None, 1]
+        d2 = dx * dx + dy * dy
+        rr = (r[i, None] + r[None, :]) * (r[i, None] + r[None, :])
+        ok = (d2 <= rr) & (np.arange(n)[None, :] > i[:, None])
+        ii, jj = np.nonzero(ok)
+        out.append(np.stack([i[ii], jj], 1))
+    return np.concatenate(out).astype(np.int32) if out else np.zeros((0, 2), np.int32)
