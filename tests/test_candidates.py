@@ -92,3 +92,39 @@ def test_gpu_candidate_pairs_million_agents():
         np.testing.assert_array_equal(pairs[starts[i]:ends[i], 1], cand)
     print(f"\n1M agents: {pairs.shape[0]} candidate pairs in {ms:.3f} ms of device time")
     assert ms > 0
+
+
+@pytest.mark.gpu
+def test_dynamic_candidate_graph_planner_matches_oracle():
+    """A receding-horizon planner on a dynamic candidate graph: every MPC step the graph is
+    rebuilt on the GPU from the current states (reach discs) and the step runs on it; the
+    oracle, given the same graph each step, follows the same trajectory."""
+    from piadmm import scenario
+    from piadmm.solver import PI_ADMM_MI355X
+    H = 12
+    cfg = config.matlab_pi(H=H)
+    # two crossings 60 m apart: far-apart vehicles never become candidates of each other
+    a, b = scenario.crossing(4, H, n_steps=14, seed=1), scenario.crossing(4, H, n_steps=14, seed=2)
+    b.xt0[:, 0] += 60.0
+    b.ref[:, 0, :] += 60.0
+    scn = scenario.concat([a, b])
+    with PI_ADMM_MI355X(cfg, scn) as s:
+        xt = scn.xt0.copy()
+        n_edges = []
+        for k in range(10):
+            r = candidates.reach_radii(cfg, scn.spd, xt[:, 2])
+            edges = candidates.candidate_pairs(s, xt[:, :2], r)
+            np.testing.assert_array_equal(edges, O.candidate_pairs(xt[:, :2], r))
+            assert edges.shape[0] <= 12 and np.all((edges[:, 0] < 4) == (edges[:, 1] < 4))
+            n_edges.append(edges.shape[0])
+            s.set_candidate_graph(edges)
+            rg = s.mpc_step(k)
+            sub = scenario.Scenario(spd=scn.spd, xt0=xt, ref=scn.ref, edges=edges, n_steps=scn.n_steps)
+            orc = O.Oracle(cfg, sub)
+            orc.t = k
+            ro = orc.mpc_step()
+            assert np.all(rg.status == 0)
+            np.testing.assert_array_equal(rg.iters, ro.iters)
+            np.testing.assert_allclose(rg.xt, ro.xt, rtol=1e-8, atol=1e-8)
+            xt = rg.xt
+        assert n_edges[0] < max(n_edges) and max(n_edges) >= 4     # the graph grows as the vehicles close in
