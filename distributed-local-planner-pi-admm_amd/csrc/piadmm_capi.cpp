@@ -890,7 +890,10 @@ int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double
   int* d_pcnt = (int*)get((size_t)n * sizeof(int));
   int* d_off = (int*)get(((size_t)n + 1) * sizeof(int));
   long long* d_total = (long long*)get(sizeof(long long));
-  if (tmp.size() != 10) {
+  int* d_bsum = (int*)get(((size_t)T / pd::DETECT_SCAN_B + 2) * sizeof(int));   // T >= n: the larger scan
+  double* d_xs = (double*)get((size_t)n * 2 * sizeof(double));                     // bucket-ordered copies
+  double* d_rs = (double*)get((size_t)n * sizeof(double));
+  if (tmp.size() != 13) {
     release();
     return fail(h, PIADMM_E_HIP, "hipMalloc failed (candidate pairs)");
   }
@@ -906,7 +909,7 @@ int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double
   rc |= hipMemcpyAsync(d_r, radius, (size_t)n * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess;
   rc |= hipEventRecord(e[0], s) != hipSuccess;
   rc |= pd::launch_detect_count(d_xy, d_r, n, 1.0 / cs, T, d_key, d_cnt, d_start, d_fill, d_order, d_pcnt, d_off,
-                                d_total, s) != 0;
+                                d_total, d_bsum, d_xs, d_rs, s) != 0;
   rc |= hipEventRecord(e[1], s) != hipSuccess;
   rc |= hipMemcpyAsync(&total, d_total, sizeof(long long), hipMemcpyDeviceToHost, s) != hipSuccess;
   rc |= hipStreamSynchronize(s) != hipSuccess;
@@ -924,7 +927,7 @@ int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double
     return fail(h, PIADMM_E_HIP, "hipMalloc failed (candidate pairs output)");
   }
   rc |= hipEventRecord(e[2], s) != hipSuccess;
-  rc |= pd::launch_detect_emit(d_xy, d_r, n, 1.0 / cs, T, d_start, d_order, d_off, d_out, s) != 0;
+  rc |= pd::launch_detect_emit(d_xs, d_rs, n, 1.0 / cs, T, d_start, d_order, d_off, d_out, s) != 0;
   rc |= hipEventRecord(e[3], s) != hipSuccess;
   const long long ncopy = std::min<long long>(total, max_pairs);
   if (ncopy > 0)

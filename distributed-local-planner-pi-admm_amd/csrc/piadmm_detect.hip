@@ -37,6 +37,8 @@ __device__ __forceinline__ unsigned bucket_of(long long cx, long long cy, unsign
   return (unsigned)((h ^ (h >> 29)) & mask);
 }
 
+__global__ void k_copy_last(const int* src, int* dst) { *dst = *src; }
+
 __global__ void __launch_bounds__(DT) k_hash(const double* xy, int n, double inv_cs, unsigned mask, unsigned* key,
                                              int* cnt) {
   const int i = blockIdx.x * DT + threadIdx.x;
@@ -47,7 +49,7 @@ __global__ void __launch_bounds__(DT) k_hash(const double* xy, int n, double inv
 }
 
 // Exclusive scan of m ints in one workgroup (1024 threads, each a contiguous chunk); out[m] =
-// total.  m <= a few million: one pass over HBM each way.
+// total.  Used for the block sums of the multi-workgroup scan below (<= 2^16 of them).
 __global__ void __launch_bounds__(1024) k_scan(const int* in, int m, int* out, long long* total) {
   __shared__ long long part[1024];
   const int t = threadIdx.x;
@@ -75,6 +77,53 @@ __global__ void __launch_bounds__(1024) k_scan(const int* in, int m, int* out, l
   }
 }
 
+// Multi-workgroup exclusive scan: SCAN_B consecutive ints per workgroup (SCAN_T threads x 4,
+// coalesced 16-byte loads), (1) the workgroups' sums, (2) their exclusive scan in one
+// workgroup (k_scan), (3) each workgroup's local scan plus its offset.
+constexpr int SCAN_T = 256, SCAN_B = 4 * SCAN_T;
+
+__device__ __forceinline__ int block_excl_scan(int v, int* sh, int& tot) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < SCAN_T; o <<= 1) {
+    const int a = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += a;
+    __syncthreads();
+  }
+  tot = sh[SCAN_T - 1];
+  const int incl = sh[t];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ void __launch_bounds__(SCAN_T) k_scan_sums(const int* in, int m, int* bsum) {
+  __shared__ int sh[SCAN_T];
+  const int i0 = blockIdx.x * SCAN_B + 4 * threadIdx.x;
+  int v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v += (i0 + k < m) ? in[i0 + k] : 0;
+  int tot;
+  (void)block_excl_scan(v, sh, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(SCAN_T) k_scan_down(const int* in, int m, const int* boff, int* out) {
+  __shared__ int sh[SCAN_T];
+  const int i0 = blockIdx.x * SCAN_B + 4 * threadIdx.x;
+  int e[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) e[k] = (i0 + k < m) ? in[i0 + k] : 0;
+  int tot;
+  int run = block_excl_scan(e[0] + e[1] + e[2] + e[3], sh, tot) + boff[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (i0 + k < m) out[i0 + k] = run;
+    run += e[k];
+  }
+}
+
 __global__ void __launch_bounds__(DT) k_scatter(int n, const unsigned* key, const int* start, int* fill, int* order) {
   const int i = blockIdx.x * DT + threadIdx.x;
   if (i >= n) return;
@@ -82,17 +131,31 @@ __global__ void __launch_bounds__(DT) k_scatter(int n, const unsigned* key, cons
   order[start[k] + atomicAdd(&fill[k], 1)] = i;
 }
 
-// Partners j > i of agent i in its 3 x 3 cell neighbourhood (buckets deduplicated: two cells
-// of the neighbourhood may hash to one bucket).  EMIT = 0: count into cnt[i]; 1: write them at
-// out[off[i] ...] and sort the agent's segment by j.
+// Positions and radii in bucket order (xs[p] = xy[order[p]]): a bucket is then a contiguous
+// run, and the threads of a wave (consecutive sorted positions: spatial neighbours) read the
+// same runs -- the gathers of the neighbourhood scans become cache-line reuse.
+__global__ void __launch_bounds__(DT) k_permute(const double* xy, const double* r, int n, const int* order, double* xs,
+                                                double* rs) {
+  const int p = blockIdx.x * DT + threadIdx.x;
+  if (p >= n) return;
+  const int i = order[p];
+  xs[2 * p] = xy[2 * i];
+  xs[2 * p + 1] = xy[2 * i + 1];
+  rs[p] = r[i];
+}
+
+// Partners j > i of agent i = order[p] in its 3 x 3 cell neighbourhood (buckets deduplicated:
+// two cells of the neighbourhood may hash to one bucket).  EMIT = 0: count into cnt[i]; 1: write
+// them at out[off[i] ...] and sort the agent's segment by j.
 template <int EMIT>
-__global__ void __launch_bounds__(DT) k_pairs(const double* xy, const double* r, int n, double inv_cs, unsigned mask,
+__global__ void __launch_bounds__(DT) k_pairs(const double* xs, const double* rs, int n, double inv_cs, unsigned mask,
                                               const int* start, const int* order, int* cnt, const int* off,
                                               int* out) {
 #pragma clang fp contract(off)
-  const int i = blockIdx.x * DT + threadIdx.x;
-  if (i >= n) return;
-  const double xi = xy[2 * i], yi = xy[2 * i + 1], ri = r[i];
+  const int p0 = blockIdx.x * DT + threadIdx.x;
+  if (p0 >= n) return;
+  const int i = order[p0];
+  const double xi = xs[2 * p0], yi = xs[2 * p0 + 1], ri = rs[p0];
   const long long cx = cell_of(xi, inv_cs), cy = cell_of(yi, inv_cs);
   unsigned seen[9];
   int ns = 0, c = 0;
@@ -108,9 +171,9 @@ __global__ void __launch_bounds__(DT) k_pairs(const double* xy, const double* r,
       for (int p = b0; p < b1; ++p) {
         const int j = order[p];
         if (j <= i) continue;
-        const double ddx = xy[2 * j] - xi, ddy = xy[2 * j + 1] - yi;
+        const double ddx = xs[2 * p] - xi, ddy = xs[2 * p + 1] - yi;
         const double d2 = ddx * ddx + ddy * ddy;
-        const double rr = (ri + r[j]) * (ri + r[j]);
+        const double rr = (ri + rs[p]) * (ri + rs[p]);
         if (d2 <= rr) {
           if (EMIT) out[2 * (base + c) + 1] = j;
           ++c;
@@ -138,28 +201,41 @@ __global__ void __launch_bounds__(DT) k_pairs(const double* xy, const double* r,
 
 inline int blocks(int n) { return (n + DT - 1) / DT; }
 
+// out[0..m) = exclusive scan of in, out[m] = total (and *total); bsum: (m + SCAN_B - 1) / SCAN_B + 1 ints
+void scan(const int* in, int m, int* out, int* bsum, long long* total, hipStream_t s) {
+  const int nb = (m + SCAN_B - 1) / SCAN_B;
+  hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(SCAN_T), 0, s, in, m, bsum);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, bsum, nb, bsum, total);   // in place: block offsets
+  hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(SCAN_T), 0, s, in, m, bsum, out);
+  // out[m] = total = bsum[nb] (k_scan wrote it there)
+  hipLaunchKernelGGL(k_copy_last, dim3(1), dim3(1), 0, s, bsum + nb, out + m);
+}
+
 }  // namespace
 
 // Device part of piadmm_candidate_pairs (piadmm_capi.cpp): all pointers device-resident, sized
-// by the caller (key, order, pcnt: n; cnt, fill: T; start: T + 1; off: n + 1; out: 2 * max_pairs).
+// by the caller (key, order, pcnt, rs: n; xs: 2n; cnt, fill: T; start: T + 1; off: n + 1; out:
+// 2 * total).  The emit phase takes the bucket-ordered xs, rs of the count phase.
 // Returns 0 after enqueueing the count phase; *total is available after the stream syncs.
 int launch_detect_count(const double* xy, const double* r, int n, double inv_cs, unsigned T, unsigned* key, int* cnt,
-                        int* start, int* fill, int* order, int* pcnt, int* off, long long* total, hipStream_t s) {
+                        int* start, int* fill, int* order, int* pcnt, int* off, long long* total, int* bsum,
+                        double* xs, double* rs, hipStream_t s) {
   const unsigned mask = T - 1;
   if (hipMemsetAsync(cnt, 0, (size_t)T * sizeof(int), s) != hipSuccess) return -1;
   if (hipMemsetAsync(fill, 0, (size_t)T * sizeof(int), s) != hipSuccess) return -1;
   hipLaunchKernelGGL(k_hash, dim3(blocks(n)), dim3(DT), 0, s, xy, n, inv_cs, mask, key, cnt);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, cnt, (int)T, start, (long long*)nullptr);
+  scan(cnt, (int)T, start, bsum, nullptr, s);
   hipLaunchKernelGGL(k_scatter, dim3(blocks(n)), dim3(DT), 0, s, n, key, start, fill, order);
-  hipLaunchKernelGGL(k_pairs<0>, dim3(blocks(n)), dim3(DT), 0, s, xy, r, n, inv_cs, mask, start, order, pcnt,
+  hipLaunchKernelGGL(k_permute, dim3(blocks(n)), dim3(DT), 0, s, xy, r, n, order, xs, rs);
+  hipLaunchKernelGGL(k_pairs<0>, dim3(blocks(n)), dim3(DT), 0, s, xs, rs, n, inv_cs, mask, start, order, pcnt,
                      nullptr, nullptr);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, pcnt, n, off, total);
+  scan(pcnt, n, off, bsum, total, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_detect_emit(const double* xy, const double* r, int n, double inv_cs, unsigned T, const int* start,
+int launch_detect_emit(const double* xs, const double* rs, int n, double inv_cs, unsigned T, const int* start,
                        const int* order, const int* off, int* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_pairs<1>, dim3(blocks(n)), dim3(DT), 0, s, xy, r, n, inv_cs, T - 1, start, order, nullptr,
+  hipLaunchKernelGGL(k_pairs<1>, dim3(blocks(n)), dim3(DT), 0, s, xs, rs, n, inv_cs, T - 1, start, order, nullptr,
                      off, out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
