@@ -116,46 +116,40 @@ def latest_profile(kind: str, workload: str):
     return None
 
 
-def cpu_baseline(wl: dict, budget_s: float) -> dict:
-    """The CPU baseline on this host, timed BEFORE anything touches the GPU: the oracle over a
-    pool of processes on all host cores (oracle/cpu_parallel.py), else on one core."""
+def cpu_baseline(wl: dict, budget_s: float, K: int) -> dict:
+    """The CPU baselines on this host, timed BEFORE anything touches the GPU.
+
+    Primary (B-opt): oracle/piadmm_cpu.cpp -- C++ -O3 + OpenMP over tiles on
+    min(16, host) threads, the GPU kernel's algorithm with exact answers equal to the oracle's
+    (tests/test_cpu_bopt.py) -- on the same job as the GPU (same seeded tiles, steps 0..K-1, fixed
+    iterations; its natural-termination ms per step next to it).  Second (``numpy_oracle``): the
+    NumPy oracle over a process pool (oracle/cpu_parallel.py), the stand-in for the reference's
+    one-QP-at-a-time Python loop (B-ref, which cannot run here: CasADi / OSQP are absent)."""
     sys.path.insert(0, ROOT)
     from piadmm import config, scenario
     n_tiles, H = wl["tiles"], wl["H"]
-    cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=1, max_outer=wl["max_outer"], tighten=wl["tighten"])
+    cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=1, max_outer=wl["max_outer"], tighten=wl["tighten"],
+                                        term_global=1)
+    bopt = pool = None
+    try:
+        from oracle import cpu_bopt
+        bopt = cpu_bopt.time_baseline(cfg, n_tiles, 0.6 * budget_s, n_steps=K)
+        scn = scenario.tiled(n_tiles, H, n_steps=K, perturb=True, seed=0)
+        r = cpu_bopt.run(cfg.replace(fixed_iters=0), scn, K, bopt["cores"])
+        bopt["natural_ms_per_step"] = 1e3 * r["seconds"] / K
+        bopt["natural_outer_iters_per_step"] = float(r["iters"][:, 0].mean())
+    except Exception as e:          # noqa: BLE001 -- report the NumPy pool alone
+        print(f"bench.py: B-opt CPU baseline failed ({e})", file=sys.stderr)
     try:
         from oracle import cpu_parallel
-        return cpu_parallel.time_baseline(cfg, n_tiles, budget_s)
-    except Exception as e:          # noqa: BLE001 -- fall back to the one-core sample below
-        print(f"bench.py: parallel CPU baseline failed ({e}); one core instead", file=sys.stderr)
-    from oracle import piadmm_oracle as O
-    try:
-        from threadpoolctl import threadpool_limits
-    except ImportError:      # pragma: no cover
-        threadpool_limits = None
-    scn = scenario.tiled(n_tiles, H, n_steps=4)
-    done, t_used = 0, 0.0
-    limit = threadpool_limits(limits=1) if threadpool_limits else None   # one core
-    try:
-        orc = O.Oracle(cfg, scn)
-        for c in range(orc.n_comp):
-            orc.xt = scn.xt0.copy()
-            orc.t = 0
-            t0 = time.perf_counter()
-            orc.mpc_step(components=[c])
-            t_used += time.perf_counter() - t0
-            done += 1
-            if t_used > budget_s:
-                break
-    finally:
-        if limit is not None:
-            limit.restore_original_limits()
-    it_s = 1.0 / (t_used / (done * wl["max_outer"]) * n_tiles)
-    return {"value": it_s, "unit": "outer_iters/s", "cores": 1, "kind": "port",
-            "sample": f"NumPy oracle (oracle/piadmm_oracle.py, exact active-set QPs, one QP at a time "
-                      f"like casadi/main.py), MPC step t=0 of {done} of {n_tiles} tiles x "
-                      f"{wl['max_outer']} outer iterations, {t_used:.1f} s, scaled linearly to {n_tiles} tiles; "
-                      f"host {platform.processor() or platform.machine()}, {os.cpu_count()} cpus visible"}
+        pool = cpu_parallel.time_baseline(cfg, n_tiles, 0.4 * budget_s)
+    except Exception as e:          # noqa: BLE001
+        print(f"bench.py: NumPy oracle pool failed ({e})", file=sys.stderr)
+    if bopt is None:
+        return pool
+    if pool is not None:
+        bopt["numpy_oracle"] = {k: pool[k] for k in ("value", "unit", "cores", "kind", "sample")}
+    return bopt
 
 
 def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_rank: int, dist, split="components"):
@@ -232,7 +226,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline timing (rank 0, N=1)")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline timing (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-natural", action="store_true", help="skip the natural-termination co-headline")
     ap.add_argument("--natural", action="store_true", help="natural termination as the headline itself")
@@ -260,7 +254,7 @@ def main():
     # pool is started with the spawn method)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and wl.get("kind") != "crossing":
-        cpu = cpu_baseline(wl, args.cpu_budget)
+        cpu = cpu_baseline(wl, args.cpu_budget, args.steps)
 
     from piadmm import _lib
     lib = _lib.load()                       # HIP runtime loaded before torch (same SONAME)
@@ -371,6 +365,8 @@ def main():
     if cpu is not None:
         line["cpu_baseline"] = cpu
         line["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        if "natural" in line and cpu.get("natural_ms_per_step"):
+            line["natural"]["speedup_vs_cpu_baseline"] = cpu["natural_ms_per_step"] / line["natural"]["ms_per_step"]
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

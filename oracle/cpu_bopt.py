@@ -1,0 +1,126 @@
+"""ctypes front end of the B-opt CPU baseline (oracle/piadmm_cpu.cpp -> oracle/libpiadmm_cpu.so).
+
+MEASUREMENT / TEST INFRASTRUCTURE ONLY: bench.py's ``cpu_baseline`` leg and tests/ use it.  It
+runs the tiled workload (components of two agents, candidate pair (2k, 2k+1)) through the
+oracle's loop (oracle/piadmm_oracle.py, casadi/main.py:43-201) in C++ with OpenMP over tiles and
+returns the same per-step records, so tests/test_cpu_bopt.py can hold it to the NumPy oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libpiadmm_cpu.so")
+
+_INT_FIELDS = ("H", "max_outer", "dual_mode", "windup", "round_decimals", "collide_sq_thres",
+               "alias_dual_residual", "pos_model", "term_dist_check", "fixed_iters", "term_global", "tighten")
+_DBL_FIELDS = ("dt", "L", "dis_thres", "beta", "Pnorm", "Pcost", "rho", "eps_pri", "eps_dual", "u_max",
+               "du_max", "kI", "theta1", "theta2", "windup_sat", "tight_p", "avg_delay", "var_delay", "qp_tol")
+
+
+class _Cfg(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int) for f in _INT_FIELDS] + [(f, ctypes.c_double) for f in _DBL_FIELDS]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-C", HERE, "-s", "libpiadmm_cpu.so"], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = ctypes.CDLL(LIB)
+        lib.piadmm_cpu_cfg_size.restype = ctypes.c_int
+        P = ctypes.c_void_p
+        lib.piadmm_cpu_run.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, P, P, P, P, P, P]
+        lib.piadmm_cpu_run.restype = ctypes.c_int
+        if lib.piadmm_cpu_cfg_size() != ctypes.sizeof(_Cfg):
+            raise RuntimeError("libpiadmm_cpu.so config layout differs from oracle/cpu_bopt.py")
+        _lib = lib
+    return _lib
+
+
+def _cfg(cfg) -> _Cfg:
+    if cfg.dual_mode not in (0, 1) or cfg.warm_duals or cfg.no_collision_gate:
+        raise ValueError("the B-opt baseline covers dual modes 0/1 without warm_duals / no_collision_gate")
+    c = _Cfg()
+    for f in _INT_FIELDS:
+        setattr(c, f, int(getattr(cfg, f)))
+    for f in _DBL_FIELDS:
+        setattr(c, f, float(getattr(cfg, f)))
+    return c
+
+
+def is_tiled(scn) -> bool:
+    N = scn.n_agents
+    return N % 2 == 0 and scn.n_edges == N // 2 and np.array_equal(
+        scn.edges, np.stack([np.arange(0, N, 2), np.arange(1, N, 2)], 1))
+
+
+def run(cfg, scn, n_steps: int, threads: int = 1, t0: int = 0, records: bool = True):
+    """n_steps MPC steps of a tiled scenario.  Returns dict(seconds, xt (S,N,3), u (S,N,H),
+    iters (S,T), resid (S,T,max_outer,2) NaN-padded, counters)."""
+    if not is_tiled(scn):
+        raise ValueError("the B-opt baseline runs tiled scenarios (pairs (2k, 2k+1))")
+    lib = load()
+    c = _cfg(cfg)
+    N, H, MO = scn.n_agents, cfg.H, cfg.max_outer
+    T = N // 2
+    spd = np.ascontiguousarray(scn.spd, np.float64)
+    xt0 = np.ascontiguousarray(scn.xt0, np.float64)
+    ref = np.ascontiguousarray(scn.ref, np.float64)
+    xt = np.zeros((n_steps, N, 3)) if records else None
+    u = np.zeros((n_steps, N, H)) if records else None
+    iters = np.zeros((n_steps, T), np.int32) if records else None
+    resid = np.zeros((n_steps, T, MO, 2)) if records else None
+    secs = ctypes.c_double(0.0)
+    cnt = np.zeros(5, np.int64)
+    ptr = (lambda a: a.ctypes.data if a is not None else None)
+    rc = lib.piadmm_cpu_run(ctypes.byref(c), T, spd.ctypes.data, xt0.ctypes.data, ref.ctypes.data, ref.shape[2],
+                            t0, n_steps, threads, ptr(xt), ptr(u), ptr(iters), ptr(resid), ctypes.byref(secs),
+                            cnt.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"piadmm_cpu_run failed ({rc})")
+    return {"seconds": secs.value, "xt": xt, "u": u, "iters": iters, "resid": resid,
+            "counters": dict(zip(("x_qps", "z_qps", "x_hits", "gi_steps", "inexact"), cnt.tolist()))}
+
+
+def time_baseline(cfg, n_tiles: int, budget_s: float, n_steps: int = 20, threads: int | None = None,
+                  perturb: bool = True) -> dict:
+    """Outer iterations per second of the n_tiles-tile job (bench.py's workload: seeded tiles,
+    fixed outer iterations) on `threads` host cores: median of repeats within ~budget_s."""
+    import time
+    from piadmm import scenario
+    ncpu = os.cpu_count() or 1
+    threads = threads or max(1, min(16, ncpu))      # the GPU box's CPU share is 16 cores
+    scn = scenario.tiled(n_tiles, cfg.H, n_steps=n_steps, perturb=perturb, seed=0)
+    run(cfg, scn, 1, threads, records=False)            # warm-up (page-in, thread pool)
+    times, t_end, cnt = [], time.perf_counter() + budget_s, None
+    while len(times) < 5 or (time.perf_counter() < t_end and len(times) < 15):
+        r = run(cfg, scn, n_steps, threads, records=False)
+        times.append(r["seconds"])
+        cnt = r["counters"]
+        if time.perf_counter() > t_end and len(times) >= 1 and times[0] * 5 > budget_s:
+            break
+    med = float(np.median(times))
+    it_per_step = cfg.max_outer if cfg.fixed_iters else None
+    value = n_steps * it_per_step / med if it_per_step else None
+    return {"value": value, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+            "ms_per_step": 1e3 * med / n_steps,
+            "sample": f"B-opt: C++ -O3 (x86-64-v3) + OpenMP over tiles, {threads} threads "
+                      f"(oracle/piadmm_cpu.cpp: the GPU kernel's algorithm -- dual active set with bounded "
+                      f"hinge multipliers, cached working-set factors -- exact answers, equal to the oracle, "
+                      f"tests/test_cpu_bopt.py); the full job: {n_tiles} tiles x MPC steps 0..{n_steps - 1} x "
+                      f"{cfg.max_outer} outer iterations, median of {len(times)} runs ({med:.3f} s each); "
+                      f"{cnt['x_qps']} x-QPs ({cnt['x_hits']} cached-set hits), {cnt['z_qps']} pair QPs, "
+                      f"{cnt['inexact']} uncertified per run; host {ncpu} cpus visible"}

@@ -1,0 +1,56 @@
+"""The B-opt CPU baseline (oracle/piadmm_cpu.cpp, bench.py's cpu_baseline) computes what the
+oracle computes: same outer-iteration counts, residual histories, controls and states (1e-8) over
+MPC steps where the tile vehicles meet (pair QPs, hinge kinks, PI saturation).  A baseline that
+solved an easier problem would not be a baseline."""
+import numpy as np
+import pytest
+
+from oracle import cpu_bopt
+from oracle import piadmm_oracle as O
+from piadmm import config, scenario
+
+CASES = [
+    ("matlab_pi", 10, {}, 38),
+    ("casadi_default", 10, {}, 38),
+    ("matlab_pi", 15, {"term_global": 1}, 34),
+    ("matlab_pi", 12, {"tighten": 1}, 36),
+    ("casadi_default", 8, {"fixed_iters": 1, "max_outer": 20, "term_global": 1}, 40),
+]
+
+
+@pytest.mark.parametrize("preset,H,kw,n_steps", CASES, ids=[f"{p}-H{h}-{'-'.join(k) or 'natural'}" for p, h, k, _ in CASES])
+def test_bopt_matches_oracle(preset, H, kw, n_steps):
+    cfg = config.PRESETS[preset](H=H, **kw)
+    scn = scenario.tiled(3, H, n_steps=n_steps, seed=5)
+    r = cpu_bopt.run(cfg, scn, n_steps, threads=2)
+    assert r["counters"]["inexact"] == 0
+    orc = O.Oracle(cfg, scn)
+    for st in range(n_steps):
+        ro = orc.mpc_step()
+        np.testing.assert_array_equal(ro.iters, r["iters"][st])
+        np.testing.assert_allclose(r["u"][st], ro.u, rtol=0, atol=1e-8)
+        np.testing.assert_allclose(r["xt"][st], ro.xt, rtol=1e-8, atol=1e-8)
+        for k in range(3):
+            res = np.array(ro.resid[k], np.float64).reshape(-1, 2)
+            mine = r["resid"][st, k]
+            np.testing.assert_allclose(mine[:len(res)], res, rtol=1e-8, atol=1e-8)
+            assert np.all(np.isnan(mine[len(res):]))
+    z_qps = r["counters"]["z_qps"]
+    assert z_qps > 0          # the window covers the coupled steps
+
+
+def test_bopt_threads_do_not_change_results():
+    cfg = config.matlab_pi(H=12, term_global=1)
+    scn = scenario.tiled(8, 12, n_steps=30, seed=9)
+    a = cpu_bopt.run(cfg, scn, 30, threads=1)
+    b = cpu_bopt.run(cfg, scn, 30, threads=4)
+    for key in ("xt", "u", "iters"):
+        np.testing.assert_array_equal(a[key], b[key])
+    np.testing.assert_array_equal(np.nan_to_num(a["resid"], nan=-1), np.nan_to_num(b["resid"], nan=-1))
+
+
+def test_bopt_rejects_what_it_does_not_cover():
+    with pytest.raises(ValueError):
+        cpu_bopt.run(config.casadi_old_pi(H=5), scenario.tiled(1, 5, n_steps=2), 1)
+    with pytest.raises(ValueError):
+        cpu_bopt.run(config.matlab_pi(H=5), scenario.crossing(3, 5, n_steps=2), 1)
