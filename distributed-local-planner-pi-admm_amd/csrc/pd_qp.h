@@ -1638,7 +1638,8 @@ constexpr int ADAPT_EVERY = PIADMM_ADAPT_EVERY;
 template <int NV, bool TWO, int XU = XGEMV_U>
 __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
                                         bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
-                                        double* x_out, int& n_admm, int& n_pdas, int& n_gi) {
+                                        double* x_out, int& n_admm, int& n_pdas, int& n_gi,
+                                        bool gi_first = false) {
   constexpr int NR = QP<NV>::NR;
   double x[NV], y[NR];
   bool ok = false;
@@ -1653,7 +1654,10 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       // its certificate fails, the dual active set warm-started from those labels finds the
       // new working set in a few steps, and one reduced solve on it certifies (instead of a
       // table rebuild per one-step PDAS label move, then ADMM)
-      ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
+      // (gi_first: the first QP of an MPC step, whose warm labels are the previous step's
+      // shifted -- their reduced solve would cost a table rebuild and rarely certifies, so the
+      // dual active set starts from them directly)
+      if (!gi_first) ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
       if (__builtin_expect(!ok, 0)) {
         int ngi = 0;
         signed char glab[NR];
@@ -1661,7 +1665,13 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         if (gi_solve(P, flab, glab, x, y, ngi)) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = glab[s];
-          ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+          // the dual active set's own answer (exact solve of its final working set + one step
+          // of refinement), certified by the KKT test: no table rebuild here -- the parametric
+          // tables of the new working set are built when a later x-QP tries these labels (in a
+          // natural-termination step the last x-QP's tables are never used)
+          signed char nl[NR];
+          ok = kkt_check(P, lab, x, y, nl);
+          if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
         }
         n_gi += ngi;
         if (!ok) {

@@ -24,7 +24,8 @@ struct DevArgs {
   piadmm_config_t cfg;
   int N, E, C, T;
   int pair_gi;              // 1: pair QPs try the dual active set first (env PIADMM_PAIR_SOLVER)
-  int x_gi;                 // 1: x-step working-set changes by the dual active set (env PIADMM_X_SOLVER)
+  int x_gi;                 // 1: x-step working-set changes by the dual active set, 2: and the step's first
+                            //    x-QP starts it without the warm labels' reduced solve (env PIADMM_X_SOLVER)
   // scenario (read-only during a step)
   const double* spd;        // N
   const double* ref;        // N*2*T

@@ -262,16 +262,17 @@ def test_pair_solvers_agree(Solver, H, monkeypatch):
             s_admm.close()
 
 
-@pytest.mark.parametrize("H", [15, 30, 40])
-def test_xstep_solvers_agree(Solver, H, monkeypatch):
-    """x-step working-set changes by the dual active set (default) or by one-step PDAS label
-    moves + ADMM (PIADMM_X_SOLVER=pdas): the same certified minimisers, iteration counts and
-    residual histories, and both match the oracle."""
+@pytest.mark.parametrize("H,alt", [(15, "pdas"), (30, "pdas"), (40, "pdas"), (30, "gi"), (40, "gi")])
+def test_xstep_solvers_agree(Solver, H, alt, monkeypatch):
+    """x-step working-set changes by the dual active set started directly from the shifted labels
+    at a step's first x-QP (default), by the dual active set after their reduced solve (gi), or
+    by one-step PDAS label moves + ADMM (pdas): the same certified minimisers, iteration counts
+    and residual histories, and all match the oracle."""
     cfg = config.matlab_pi(H=H)
     scn = scenario.tiled(10, H, n_steps=8, perturb=True, seed=21)
     orc = O.Oracle(cfg, scn)
     with Solver(cfg, scn) as s_gi:
-        monkeypatch.setenv("PIADMM_X_SOLVER", "pdas")
+        monkeypatch.setenv("PIADMM_X_SOLVER", alt)
         s_pd = Solver(cfg, scn)
         monkeypatch.delenv("PIADMM_X_SOLVER")
         try:
@@ -285,7 +286,7 @@ def test_xstep_solvers_agree(Solver, H, monkeypatch):
                 assert np.all(r1.status == 0) and np.all(r2.status == 0)
             c1, c2 = s_gi.counters(), s_pd.counters()
             assert c1["x_qps"] == c2["x_qps"]
-            if H <= 32:      # LDS mode: the x-step's dual active set replaces ADMM
+            if H <= 32 and alt == "pdas":      # LDS mode: the x-step's dual active set replaces ADMM
                 assert c1["admm_x"] < c2["admm_x"]
         finally:
             s_pd.close()
