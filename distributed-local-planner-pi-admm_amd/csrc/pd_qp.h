@@ -1018,6 +1018,17 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
   return wall(ok);
 }
 
+// the x-step's parametric tables hold labels lab's working set (the signature reduced_solve_x
+// compares): a reduced solve on lab is one fused pass, not a rebuild
+template <int NV>
+__device__ __forceinline__ bool tables_match(const QP<NV>& P, const signed char* lab) {
+  if constexpr (NV != 1) return true;
+  int sig = 0;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) sig |= ((P.valid(s) && lab[s] != FREE) ? (int)lab[s] : 0) << (2 * s);
+  return wall(sig == P.csig);
+}
+
 template <int NV, int XU = XGEMV_U>
 __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y, int& nsolve,
                                      int steps = PDAS_STEPS) {
@@ -1654,10 +1665,11 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       // its certificate fails, the dual active set warm-started from those labels finds the
       // new working set in a few steps, and one reduced solve on it certifies (instead of a
       // table rebuild per one-step PDAS label move, then ADMM)
-      // (gi_first: the first QP of an MPC step, whose warm labels are the previous step's
-      // shifted -- their reduced solve would cost a table rebuild and rarely certifies, so the
-      // dual active set starts from them directly)
-      if (!gi_first) ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
+      // Only when the parametric tables hold the warm labels' working set (a hit pass): a
+      // reduced solve on other labels costs a table rebuild (~20 us) and after a dual update or
+      // at a step's first x-QP (gi_first: the previous step's labels shifted) rarely certifies,
+      // so the dual active set starts from those labels directly
+      if (!gi_first && tables_match(P, lab)) ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
       if (__builtin_expect(!ok, 0)) {
         int ngi = 0;
         signed char glab[NR];
@@ -1669,9 +1681,17 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
           // of refinement), certified by the KKT test: no table rebuild here -- the parametric
           // tables of the new working set are built when a later x-QP tries these labels (in a
           // natural-termination step the last x-QP's tables are never used)
-          signed char nl[NR];
-          ok = kkt_check(P, lab, x, y, nl);
-          if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+          bool stable = true;
+#pragma unroll
+          for (int s = 0; s < NR; ++s) stable &= !P.valid(s) || glab[s] == flab[s];
+          if (wall(stable)) {
+            // the working set held: build its tables now for the cheap hits that follow
+            ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+          } else {
+            signed char nl[NR];
+            ok = kkt_check(P, lab, x, y, nl);
+            if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+          }
         }
         n_gi += ngi;
         if (!ok) {

@@ -364,10 +364,9 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     const char* ps = std::getenv("PIADMM_PAIR_SOLVER");
     A.pair_gi = (ps && std::strcmp(ps, "admm") == 0) ? 0 : 1;
     // PIADMM_X_SOLVER: "pdas" = one-step label moves + ADMM only; "gi" = the dual active set
-    // after a failed reduced solve of the warm labels at every x-QP; default ("gi_first") = the
-    // same, except that an MPC step's first x-QP starts the dual active set from the previous
-    // step's shifted labels without that reduced solve (it costs a table rebuild, ~20 us, and
-    // rarely certifies: natural step 0.532 -> 0.491 ms, fixed 0.743 -> 0.703 ms at 256 x H30)
+    // after a failed reduced solve of the warm labels; default ("gi_first") = the same, except
+    // that an MPC step's first x-QP starts the dual active set from the previous step's shifted
+    // labels without that reduced solve (a table rebuild, ~20 us, that rarely certifies)
     const char* xs = std::getenv("PIADMM_X_SOLVER");
     A.x_gi = (xs && std::strcmp(xs, "pdas") == 0) ? 0 : (xs && std::strcmp(xs, "gi") == 0) ? 1 : 2;
   }
