@@ -103,3 +103,27 @@ def test_config5_256_agents_H50_tightening_sampled_tiles(Solver):
         for _ in range(2):
             ro, rg = orc.mpc_step(components=comps), s.mpc_step()
             check_tiles(rg, ro, comps, 50, cfg.max_outer)
+
+
+@pytest.mark.parametrize("preset,H,tiles,n_steps,kw", [
+    ("matlab_pi", 30, 128, 6, {"fixed_iters": 1, "term_global": 1}),      # bench mode, configs[2]
+    ("matlab_pi", 30, 128, 24, {"term_global": 1}),                       # natural co-headline
+    ("casadi_default", 20, 32, 8, {"fixed_iters": 1, "max_outer": 200}),  # configs[1]
+])
+def test_gpu_equals_bopt_cpu_baseline_at_full_size(Solver, preset, H, tiles, n_steps, kw):
+    """The GPU and the B-opt CPU baseline (oracle/piadmm_cpu.cpp, bench.py's cpu_baseline)
+    compute the same job at the bench's full sizes: every tile, every step, identical
+    outer-iteration counts, states and controls within 1e-8 -- the CPU number is a baseline
+    for this exact work."""
+    from oracle import cpu_bopt
+    cfg = config.PRESETS[preset](H=H, **kw)
+    scn = scenario.tiled(tiles, H, n_steps=n_steps, perturb=True, seed=0)
+    rc = cpu_bopt.run(cfg, scn, n_steps, threads=4)
+    assert rc["counters"]["inexact"] == 0
+    with Solver(cfg, scn) as s:
+        for k in range(n_steps):
+            rg = s.mpc_step()
+            assert np.all(rg.status == 0)
+            np.testing.assert_array_equal(rg.iters, rc["iters"][k])
+            close(rg.u, rc["u"][k], rtol=0)
+            close(rg.xt, rc["xt"][k])
