@@ -77,7 +77,13 @@ def spawn_ranks(n: int) -> int:
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, env=env)
+    # relay rank 0's JSON line on stdout; everything else the ranks print (gloo connection
+    # notices, launcher messages) goes to stderr, so stdout stays ONE JSON line
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return p.wait()
 
 
 def algorithmic_bytes(cnt: dict, H: int) -> float:
@@ -173,9 +179,20 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
         scn = scenario.concat([scenario.crossing(4, H, n_steps=n_steps, seed=1000 * rank + k) for k in range(wl["tiles"])])
     else:
         scn = scenario.tiled(wl["tiles"], H, n_steps=n_steps, perturb=True, seed=1000 * rank)
-    solver = PI_ADMM_MI355X(cfg, scn, device=local_rank, shard=shard)
+    from piadmm.solver import device_count
+    solver = PI_ADMM_MI355X(cfg, scn, device=local_rank % max(device_count(), 1), shard=shard)
     try:
-        if dist is not None:
+        if dist is not None and os.environ.get("PIADMM_BENCH_TRANSPORT") == "host":
+            # rehearsal transport (several ranks sharing one GPU, where RCCL refuses duplicate
+            # devices): the library's host all-reduce callback over the gloo group
+            import torch
+
+            def host_allreduce(buf):
+                t = torch.from_numpy(buf.copy())
+                dist.all_reduce(t)
+                buf[:] = t.numpy()
+            solver.set_allreduce(host_allreduce)
+        elif dist is not None:
             def bcast(b):
                 obj = [b]
                 dist.broadcast_object_list(obj, src=0)
@@ -303,6 +320,8 @@ def main():
             "outer_iters_per_step": m["job_iters"] / K,
             "job_outer_iters_per_s": m["job_iters"] / m["wall"],
             "agent_qps_per_s": cnt["x_qps"] * world / m["wall"],
+            "transport": ("host all-reduce over gloo (rehearsal)" if os.environ.get("PIADMM_BENCH_TRANSPORT") == "host"
+                          else "RCCL") if world > 1 else None,
             "parallelism": (f"agents sharded over {world} GPU(s), every tile across two ranks: one all-reduce of "
                             f"the boundary exchange buffer per outer iteration + " if m["xchg"] else
                             f"components sharded over {world} GPU(s); ") + (

@@ -17,6 +17,10 @@
 
 #include "piadmm_internal.h"
 
+namespace pd {
+thread_local hipError_t g_launch_err = hipSuccess;
+}
+
 struct piadmm_ctx {
   piadmm_config_t cfg{};
   hipStream_t stream = nullptr;
@@ -527,6 +531,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     const char* nc = std::getenv("PIADMM_NO_COOP");
     h->coop = h->cfg.term_global && !h->cfg.fixed_iters && !(nc && nc[0] == '1') && !h->xchg &&
               (A.graph ? pd::graph_coop_fits(A, h->cfg.device) : pd::coop_fits(A, h->cfg.device));
+    (void)hipGetLastError();   // a refused query must not surface as the next launch's error
   }
   h->have_scn = true;
   return PIADMM_OK;
@@ -570,7 +575,7 @@ int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
 #define LAUNCH(h, expr)                                                                       \
   do {                                                                                        \
     if ((expr) != 0)                                                                          \
-      return fail((h), PIADMM_E_HIP, std::string("kernel launch: ") + hipGetErrorString(hipGetLastError())); \
+      return fail((h), PIADMM_E_HIP, std::string("kernel launch " #expr ": ") + hipGetErrorString(pd::g_launch_err)); \
   } while (0)
 #define NCCLCHK(h, expr)                                                                      \
   do {                                                                                        \
@@ -859,6 +864,7 @@ int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double
   *n_pairs_out = 0;
   if (ms_out) *ms_out = 0.0f;
   if (n == 0) return PIADMM_OK;
+  (void)hipGetLastError();   // a stale error of an earlier runtime call is not this call's
   double rmax = 0.0;
   for (int i = 0; i < n; ++i) {
     if (!std::isfinite(xy[2 * i]) || !std::isfinite(xy[2 * i + 1]) || !std::isfinite(radius[i]) || radius[i] < 0)

@@ -230,14 +230,14 @@ int launch_detect_count(const double* xy, const double* r, int n, double inv_cs,
   hipLaunchKernelGGL(k_pairs<0>, dim3(blocks(n)), dim3(DT), 0, s, xs, rs, n, inv_cs, mask, start, order, pcnt,
                      nullptr, nullptr);
   scan(pcnt, n, off, bsum, total, s);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return launch_rc(hipGetLastError());
 }
 
 int launch_detect_emit(const double* xs, const double* rs, int n, double inv_cs, unsigned T, const int* start,
                        const int* order, const int* off, int* out, hipStream_t s) {
   hipLaunchKernelGGL(k_pairs<1>, dim3(blocks(n)), dim3(DT), 0, s, xs, rs, n, inv_cs, T - 1, start, order, nullptr,
                      off, out);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return launch_rc(hipGetLastError());
 }
 
 }  // namespace pd

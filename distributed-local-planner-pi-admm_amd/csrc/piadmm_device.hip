@@ -800,19 +800,21 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
   const void* fn = big ? (const void*)k_mpc_step<true> : (const void*)k_mpc_step<false>;
   // the dynamic-LDS limit is a per-device function attribute: set it on every launch (cheap),
   // so handles on several devices of one process each get it
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return -1;
+  if (launch_rc(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)) != 0) return -1;
   if (flags & F_COOP) {
     // every workgroup must be resident for the grid barrier: the cooperative launch fails
     // (and the caller falls back to host-decided termination) rather than deadlock
     DevArgs aa = a;
     void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
-    return hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NW * WAVE), args, (unsigned)sh, s) == hipSuccess ? 0 : -1;
+    (void)hipGetLastError();
+    return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NW * WAVE), args, (unsigned)sh, s));
   }
+  (void)hipGetLastError();   // a stale error of an earlier runtime call is not this launch's
   if (big)
     hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
   else
     hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return launch_rc(hipGetLastError());
 }
 
 // Can every workgroup of a k_mpc_step launch be resident at once (cooperative launch)?
@@ -830,19 +832,22 @@ bool coop_fits(const DevArgs& a, int device) {
 }
 
 int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s) {
+  (void)hipGetLastError();
   hipLaunchKernelGGL(k_term_partials, dim3(1), dim3(NW * WAVE), 0, s, a, it, out);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return launch_rc(hipGetLastError());
 }
 
 int launch_resid_history(const DevArgs& a, int nsteps, double* out, hipStream_t s) {
+  (void)hipGetLastError();
   hipLaunchKernelGGL(k_resid_history, dim3(a.cfg.max_outer, nsteps), dim3(256), 0, s, a, out);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return launch_rc(hipGetLastError());
 }
 
 int launch_pair_deff(const DevArgs& a, hipStream_t s) {
   if (a.E == 0) return 0;
+  (void)hipGetLastError();
   hipLaunchKernelGGL(k_pair_deff, dim3((a.E + 255) / 256), dim3(256), 0, s, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return launch_rc(hipGetLastError());
 }
 
 }  // namespace pd

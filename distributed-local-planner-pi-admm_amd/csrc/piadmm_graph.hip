@@ -744,17 +744,19 @@ int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int
   const size_t sh = graph_lds_bytes(a.cfg.H);
   const bool big = a.cfg.H > HMAX;
   const void* fn = big ? (const void*)k_graph_step<true> : (const void*)k_graph_step<false>;
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return -1;
+  if (launch_rc(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)) != 0) return -1;
   if (flags & F_COOP) {
     DevArgs aa = a;
     void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
-    return hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(GW * WAVE), args, (unsigned)sh, s) == hipSuccess ? 0 : -1;
+    (void)hipGetLastError();
+    return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(GW * WAVE), args, (unsigned)sh, s));
   }
+  (void)hipGetLastError();   // a stale error of an earlier runtime call is not this launch's
   if (big)
     hipLaunchKernelGGL(k_graph_step<true>, dim3(a.C), dim3(GW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
   else
     hipLaunchKernelGGL(k_graph_step<false>, dim3(a.C), dim3(GW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return launch_rc(hipGetLastError());
 }
 
 bool graph_coop_fits(const DevArgs& a, int device) {
@@ -770,8 +772,9 @@ bool graph_coop_fits(const DevArgs& a, int device) {
 }
 
 int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s) {
+  (void)hipGetLastError();
   hipLaunchKernelGGL(k_graph_partials, dim3(1), dim3(GW * WAVE), 0, s, a, out);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return launch_rc(hipGetLastError());
 }
 
 }  // namespace pd

@@ -4,6 +4,15 @@
 
 namespace pd {
 
+// The HIP error of the last kernel launch (launchers return launch_rc(...); the C-ABI's error
+// message reports it -- hipGetLastError() is consumed by the launcher itself).
+extern thread_local hipError_t g_launch_err;
+inline int launch_rc(hipError_t e) {
+  g_launch_err = e;
+  return e == hipSuccess ? 0 : -1;
+}
+
+
 constexpr int WAVE = 64;
 constexpr int NW = 2;        // waves per workgroup = agents per component (max)
 constexpr int HCAP = 64;     // storage stride of per-lane state: lane k <-> time index k, H <= 63
