@@ -1650,7 +1650,7 @@ template <int NV, bool TWO, int XU = XGEMV_U>
 __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
                                         bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
                                         double* x_out, int& n_admm, int& n_pdas, int& n_gi,
-                                        bool gi_first = false) {
+                                        int gi_first = 0) {
   constexpr int NR = QP<NV>::NR;
   double x[NV], y[NR];
   bool ok = false;
@@ -1669,12 +1669,12 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       // reduced solve on other labels costs a table rebuild (~20 us) and after a dual update or
       // at a step's first x-QP (gi_first: the previous step's labels shifted) rarely certifies,
       // so the dual active set starts from those labels directly
-      if (!gi_first && tables_match(P, lab)) ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
+      if ((gi_first == 0 || gi_first == 3) && tables_match(P, lab)) ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
       if (__builtin_expect(!ok, 0)) {
         int ngi = 0;
         signed char glab[NR];
         ensure_q(P);
-        if (gi_solve(P, flab, glab, x, y, ngi)) {
+        if (gi_solve(P, gi_first >= 2 ? nullptr : flab, glab, x, y, ngi)) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = glab[s];
           // the dual active set's own answer (exact solve of its final working set + one step

@@ -368,11 +368,14 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     const char* ps = std::getenv("PIADMM_PAIR_SOLVER");
     A.pair_gi = (ps && std::strcmp(ps, "admm") == 0) ? 0 : 1;
     // PIADMM_X_SOLVER: "pdas" = one-step label moves + ADMM only; "gi" = the dual active set
-    // after a failed reduced solve of the warm labels; default ("gi_first") = the same, except
-    // that an MPC step's first x-QP starts the dual active set from the previous step's shifted
-    // labels without that reduced solve (a table rebuild, ~20 us, that rarely certifies)
+    // warm-started from the labels after a failed reduced solve of them; "gi_warm" = the same,
+    // except that an MPC step's first x-QP skips that reduced solve (a table rebuild, ~20 us,
+    // that rarely certifies); default ("gi_cold") = that first x-QP's dual active set starts
+    // cold (from the unconstrained minimiser: cheaper on a wave than appending and dropping the
+    // previous step's shifted rows); "gi_cold_all" = every x-step dual active set starts cold
     const char* xs = std::getenv("PIADMM_X_SOLVER");
-    A.x_gi = (xs && std::strcmp(xs, "pdas") == 0) ? 0 : (xs && std::strcmp(xs, "gi") == 0) ? 1 : 2;
+    A.x_gi = (xs && std::strcmp(xs, "pdas") == 0) ? 0 : (xs && std::strcmp(xs, "gi") == 0) ? 1
+           : (xs && std::strcmp(xs, "gi_warm") == 0) ? 2 : (xs && std::strcmp(xs, "gi_cold_all") == 0) ? 4 : 3;
   }
   A.N = N;
   A.E = n_edges;

@@ -345,7 +345,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
-                               qx.fld, ustar, n_admm_x, n_pdas_x, n_gi, A.x_gi == 2 && first && it == it0);
+                               qx.fld, ustar, n_admm_x, n_pdas_x, n_gi, (A.x_gi >= 2 && first && it == it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
       ++n_xqp;

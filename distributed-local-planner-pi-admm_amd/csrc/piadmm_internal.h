@@ -33,8 +33,8 @@ struct DevArgs {
   piadmm_config_t cfg;
   int N, E, C, T;
   int pair_gi;              // 1: pair QPs try the dual active set first (env PIADMM_PAIR_SOLVER)
-  int x_gi;                 // 1: x-step working-set changes by the dual active set, 2: and the step's first
-                            //    x-QP starts it without the warm labels' reduced solve (env PIADMM_X_SOLVER)
+  int x_gi;                 // x-step working-set changes by the dual active set (1); the step's first x-QP
+                            // without the labels' reduced solve (2), started cold (3); all cold (4); PIADMM_X_SOLVER
   // scenario (read-only during a step)
   const double* spd;        // N
   const double* ref;        // N*2*T

@@ -262,12 +262,13 @@ def test_pair_solvers_agree(Solver, H, monkeypatch):
             s_admm.close()
 
 
-@pytest.mark.parametrize("H,alt", [(15, "pdas"), (30, "pdas"), (40, "pdas"), (30, "gi"), (40, "gi")])
+@pytest.mark.parametrize("H,alt", [(15, "pdas"), (30, "pdas"), (40, "pdas"), (30, "gi"), (40, "gi"),
+                                   (30, "gi_warm"), (15, "gi_cold_all")])
 def test_xstep_solvers_agree(Solver, H, alt, monkeypatch):
-    """x-step working-set changes by the dual active set started directly from the shifted labels
-    at a step's first x-QP (default), by the dual active set after their reduced solve (gi), or
-    by one-step PDAS label moves + ADMM (pdas): the same certified minimisers, iteration counts
-    and residual histories, and all match the oracle."""
+    """x-step working-set changes by the dual active set started cold at a step's first x-QP
+    (default), from the shifted labels (gi_warm), after their reduced solve (gi), cold at every
+    x-QP (gi_cold_all), or by one-step PDAS label moves + ADMM (pdas): the same certified
+    minimisers, iteration counts and residual histories, and all match the oracle."""
     cfg = config.matlab_pi(H=H)
     scn = scenario.tiled(10, H, n_steps=8, perturb=True, seed=21)
     orc = O.Oracle(cfg, scn)
