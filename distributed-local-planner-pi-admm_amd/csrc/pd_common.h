@@ -21,7 +21,12 @@ __shared__ unsigned long long s_stamps[64];
     const unsigned long long _d = __builtin_amdgcn_s_memtime() - (t0);                       \
     if (__lane_id() == 0) atomicAdd(&s_stamps[(slot)], _d);                                  \
   } while (0)
+#define STAMP_CNT(slot, n)                                                                    \
+  do {                                                                                        \
+    if (__lane_id() == 0) atomicAdd(&s_stamps[(slot)], (unsigned long long)(n));             \
+  } while (0)
 #else
+#define STAMP_CNT(slot, n) ((void)(n))
 #define STAMP_T() 0ull
 #define STAMP_ADD(slot, t0) ((void)(t0))
 #endif
@@ -29,7 +34,9 @@ enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL
                  ST_KERNEL, ST_RED_GEMV, ST_RED_S, ST_RED_CHOL, ST_RED_X, ST_ADMM, ST_XQ, ST_TERM,
                  ST_SZ_RUIZ, ST_SZ_KMAT, ST_SZ_GJ, ST_SZ_PRE, ST_ZR_GEMV, ST_ZR_S, ST_ZR_CHOL, ST_ZR_X,
                  ST_ZR_SOLVE, ST_XR_SOLVE, ST_ZKKT, ST_XKKT, ST_GI_SEARCH, ST_GI_SOLVE, ST_GI_UPD,
-                 ST_SYNC_A, ST_TERMW, ST_SYNC_B, ST_RSX_PRE, ST_QEPI, ST_ROUND, NSTAMP = 64 };
+                 ST_SYNC_A, ST_TERMW, ST_SYNC_B, ST_RSX_PRE, ST_QEPI, ST_ROUND,
+                 // graph kernel: event counts (not cycles) in the same buffer
+                 ST_N_GIZ = 40, ST_N_GIX, ST_N_ZQP, ST_N_ZFAIL, ST_N_XREBUILD, NSTAMP = 64 };
 
 // ============================================================ wave primitives
 __device__ __forceinline__ int lid() { return (int)__lane_id(); }

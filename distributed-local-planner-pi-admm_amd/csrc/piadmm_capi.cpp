@@ -54,6 +54,10 @@ struct piadmm_ctx {
   void* xctx = nullptr;
   double* h_x = nullptr;         // pinned staging of the host transport
   size_t h_x_n = 0;
+  // host-stepped MPC step (piadmm_outer_iter / piadmm_step_finish): the open step, the next
+  // outer iteration, and the host-decided stop state of the global scope
+  bool step_open = false;
+  int step_t = -1, step_it = 0, step_flag = 0, step_nanlast = 0, step_stop = 0;
 };
 
 namespace {
@@ -238,6 +242,14 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     const int v1 = edges[2 * e], v2 = edges[2 * e + 1];
     if (v1 < 0 || v2 >= N || v1 >= v2) return fail(h, PIADMM_E_ARG, "edge must satisfy 0 <= v1 < v2 < N");
   }
+  {
+    // a pair listed twice would add its AL term twice to both x-steps and solve its QP twice
+    std::vector<long long> key((size_t)n_edges);
+    for (int e = 0; e < n_edges; ++e) key[e] = (long long)edges[2 * e] * N + edges[2 * e + 1];
+    std::sort(key.begin(), key.end());
+    if (std::adjacent_find(key.begin(), key.end()) != key.end())
+      return fail(h, PIADMM_E_ARG, "duplicate candidate pair (the same (v1, v2) twice)");
+  }
   // The fused kernel (piadmm_device.hip) takes components of one agent or one pair (v, v+1);
   // any other candidate graph -- components of more agents, agents in several pairs -- runs
   // on the graph kernel (piadmm_graph.hip).  PIADMM_GRAPH=1 forces graph mode (tests).
@@ -283,6 +295,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   HIPCHK(h, hipSetDevice(h->cfg.device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   free_all(h);
+  h->step_open = false;
   h->comp_ptr.assign(1, 0);
   h->comp_edge.clear();
   std::vector<int> nbr(N, 0);
@@ -563,6 +576,7 @@ int32_t piadmm_set_allreduce(piadmm_handle_t h, piadmm_allreduce_fn fn, void* ct
 int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
   if (!h || !xt) return fail(h, PIADMM_E_ARG, "null argument");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  h->step_open = false;
   HIPCHK(h, hipSetDevice(h->cfg.device));
   HIPCHK(h, hipMemcpyAsync(h->a.xt, xt, (size_t)h->N * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
   // a new state breaks the receding-horizon sequence: no label warm start for the next step
@@ -653,6 +667,36 @@ static int32_t run_steps_xchg(piadmm_handle_t h, int32_t t, int32_t n, bool sync
   return PIADMM_OK;
 }
 
+// One outer iteration `it` of MPC step t under host-decided global termination (term_global
+// without the in-kernel stop test: an RCCL communicator, a host transport, or host stepping):
+// the iteration launch, the job's termination partials (all-reduced), and the reference's stop
+// rules over all agents (casadi/main.py:115-118,174-178; MATLAB :191-210).  flag / nanlast carry
+// the step's state; *stop = 1 when the step ends at this iteration.
+static int32_t global_iteration(piadmm_handle_t h, int32_t tk, int it, int& flag, int& nanlast, int* stop) {
+  const piadmm_config_t& c = h->cfg;
+  hipStream_t s = h->stream;
+  *stop = 0;
+  LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
+  double* part = h->d_part + (size_t)5 * it;
+  LAUNCH(h, h->a.graph ? pd::launch_graph_partials(h->a, part, s) : pd::launch_term_partials(h->a, it, part, s));
+  if (int rc = allreduce(h, part, part, 5)) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
+  const double n_seen = h->h_part[3], n_bad = h->h_part[4];
+  if (n_act == 0.0 && flag == 0) {      // no pair collides anywhere: stop (casadi/main.py:115-116)
+    nanlast = 1;
+    *stop = 1;
+    return PIADMM_OK;
+  }
+  flag = 1;
+  h->ghist[2 * it + 0] = rk;
+  h->ghist[2 * it + 1] = sk;
+  const bool dist_ok = n_seen > 0.0 && n_bad == 0.0;
+  if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok)) *stop = 1;
+  return PIADMM_OK;
+}
+
 static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outputs) {
   const piadmm_config_t& c = h->cfg;
   hipStream_t s = h->stream;
@@ -698,24 +742,10 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
     h->ghist.assign((size_t)2 * M, NAN);
     int flag = 0, nit = 0, nanlast = 0;
     for (int it = 0; it < M; ++it) {
-      LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
-      double* part = h->d_part + (size_t)5 * it;
-      LAUNCH(h, h->a.graph ? pd::launch_graph_partials(h->a, part, s) : pd::launch_term_partials(h->a, it, part, s));
-      if (int rc = allreduce(h, part, part, 5)) return rc;
-      HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
-      HIPCHK(h, hipStreamSynchronize(s));
-      const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
-      const double n_seen = h->h_part[3], n_bad = h->h_part[4];
+      int stop = 0;
+      if (int rc = global_iteration(h, tk, it, flag, nanlast, &stop)) return rc;
       nit = it + 1;
-      if (n_act == 0.0 && flag == 0) {      // no pair collides anywhere: stop (casadi/main.py:115-116)
-        nanlast = 1;
-        break;
-      }
-      flag = 1;
-      h->ghist[2 * it + 0] = rk;
-      h->ghist[2 * it + 1] = sk;
-      const bool dist_ok = n_seen > 0.0 && n_bad == 0.0;
-      if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok)) break;
+      if (stop) break;
     }
     h->giters = nit;
     LAUNCH(h, launch_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
@@ -726,6 +756,7 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
 static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  if (h->step_open) return fail(h, PIADMM_E_STATE, "a host-stepped MPC step is open: piadmm_step_finish first");
   if (n < 0 || t0 < 0 || t0 + (n > 0 ? n - 1 : 0) + h->cfg.H + 1 > h->T)
     return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
   HIPCHK(h, hipSetDevice(h->cfg.device));
@@ -748,7 +779,7 @@ int32_t piadmm_sync(piadmm_handle_t h) {
 }
 
 int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_old, double* hat, double* lam,
-                         uint8_t* edge_active, int32_t* iters) {
+                         double* S, double* D, uint8_t* edge_active, int32_t* iters) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
   const int N = h->N, E = h->E, C = h->C, H = h->cfg.H, H1 = H + 1;
@@ -759,8 +790,70 @@ int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_o
   if (pos_old) HIPCHK(h, hipMemcpyAsync(pos_old, h->a.pos_old, (size_t)N * 2 * H1 * 8, hipMemcpyDeviceToHost, s));
   if (hat && E) HIPCHK(h, hipMemcpyAsync(hat, h->a.hat, (size_t)E * 4 * H1 * 8, hipMemcpyDeviceToHost, s));
   if (lam && E) HIPCHK(h, hipMemcpyAsync(lam, h->a.lam, (size_t)E * 4 * H1 * 8, hipMemcpyDeviceToHost, s));
+  if (S && E) HIPCHK(h, hipMemcpyAsync(S, h->a.Sacc, (size_t)E * 4 * H1 * 8, hipMemcpyDeviceToHost, s));
+  if (D && E) HIPCHK(h, hipMemcpyAsync(D, h->a.Dacc, (size_t)E * 4 * H1 * 8, hipMemcpyDeviceToHost, s));
   if (edge_active && E) HIPCHK(h, hipMemcpyAsync(edge_active, h->a.edge_active, E, hipMemcpyDeviceToHost, s));
   if (iters) HIPCHK(h, hipMemcpyAsync(iters, h->a.iters, (size_t)C * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  return PIADMM_OK;
+}
+
+// Host stepping of one MPC step, one outer iteration per call (SURVEY.md 8b piadmm_outer_iter):
+// the state of casadi/main.py:78-181 after each iteration (pos_old, hat, lam and the PI
+// accumulators S, D of ADMM_CVX_..._PI_antiwindup.m:160-188) is read with piadmm_get_state.
+int32_t piadmm_outer_iter(piadmm_handle_t h, int32_t t, int32_t it, int32_t* stop_out) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  if (h->xchg) return fail(h, PIADMM_E_STATE, "host stepping of a sharded graph is not supported");
+  const piadmm_config_t& c = h->cfg;
+  if (it < 0 || it >= c.max_outer) return fail(h, PIADMM_E_ARG, "it must be in [0, max_outer)");
+  if (t < 0 || t + c.H + 1 > h->T) return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
+  if (it == 0) {
+    h->step_open = true;
+    h->step_t = t;
+    h->step_flag = h->step_nanlast = h->step_stop = 0;
+    h->ghist.assign((size_t)2 * c.max_outer, NAN);
+  } else if (!h->step_open || t != h->step_t || it != h->step_it) {
+    return fail(h, PIADMM_E_STATE, "outer_iter out of order: iterations of a step run 0, 1, 2, ...");
+  } else if (h->step_stop) {
+    return fail(h, PIADMM_E_STATE, "the step's stop rule already fired: piadmm_step_finish");
+  }
+  HIPCHK(h, hipSetDevice(c.device));
+  hipStream_t s = h->stream;
+  int stop = 0;
+  if (c.term_global) {
+    if (it == 0 && !h->a.graph) LAUNCH(h, pd::launch_pair_deff(h->a, s));
+    if (int rc = global_iteration(h, t, it, h->step_flag, h->step_nanlast, &stop)) return rc;
+    h->giters = it + 1;
+  } else {
+    // per-component stop: a component whose stop rule fired keeps its state (the kernels skip it)
+    LAUNCH(h, launch_step(h->a, t, 1, it, it + 1, it == 0 ? pd::F_FIRST : 0, s));
+    std::vector<int> cst((size_t)h->C * 4);
+    HIPCHK(h, hipMemcpyAsync(cst.data(), h->a.cst, cst.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    stop = 1;
+    for (int ci = 0; ci < h->C; ++ci) stop &= cst[(size_t)ci * 4 + 3] != 0;
+  }
+  h->step_it = it + 1;
+  h->step_stop = stop;
+  if (stop_out) *stop_out = stop;
+  return PIADMM_OK;
+}
+
+int32_t piadmm_step_finish(piadmm_handle_t h, double* xt_out, double* u_out) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!h->step_open) return fail(h, PIADMM_E_STATE, "no host-stepped MPC step is open");
+  const piadmm_config_t& c = h->cfg;
+  HIPCHK(h, hipSetDevice(c.device));
+  hipStream_t s = h->stream;
+  const int nit = h->step_it;
+  int flags = pd::F_LAST;
+  if (c.term_global) flags |= pd::F_GLOBAL | (h->step_nanlast ? pd::F_NANLAST : 0);
+  LAUNCH(h, launch_step(h->a, h->step_t, 1, nit, nit, flags, s));
+  h->step_open = false;
+  const int N = h->N, H = c.H;
+  if (xt_out) HIPCHK(h, hipMemcpyAsync(xt_out, h->a.xt, (size_t)N * 3 * 8, hipMemcpyDeviceToHost, s));
+  if (u_out) HIPCHK(h, hipMemcpyAsync(u_out, h->a.u, (size_t)N * H * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(h, hipStreamSynchronize(s));
   return PIADMM_OK;
 }
@@ -903,7 +996,7 @@ int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double
   int* d_pcnt = (int*)get((size_t)n * sizeof(int));
   int* d_off = (int*)get(((size_t)n + 1) * sizeof(int));
   long long* d_total = (long long*)get(sizeof(long long));
-  int* d_bsum = (int*)get(((size_t)T / pd::DETECT_SCAN_B + 2) * sizeof(int));   // T >= n: the larger scan
+  long long* d_bsum = (long long*)get(((size_t)T / pd::DETECT_SCAN_B + 2) * sizeof(long long));   // T >= n: the larger scan
   double* d_xs = (double*)get((size_t)n * 2 * sizeof(double));                     // bucket-ordered copies
   double* d_rs = (double*)get((size_t)n * sizeof(double));
   if (tmp.size() != 13) {

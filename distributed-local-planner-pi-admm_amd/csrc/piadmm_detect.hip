@@ -37,7 +37,7 @@ __device__ __forceinline__ unsigned bucket_of(long long cx, long long cy, unsign
   return (unsigned)((h ^ (h >> 29)) & mask);
 }
 
-__global__ void k_copy_last(const int* src, int* dst) { *dst = *src; }
+__global__ void k_copy_last(const long long* src, int* dst) { *dst = (int)*src; }
 
 __global__ void __launch_bounds__(DT) k_hash(const double* xy, int n, double inv_cs, unsigned mask, unsigned* key,
                                              int* cnt) {
@@ -48,9 +48,11 @@ __global__ void __launch_bounds__(DT) k_hash(const double* xy, int n, double inv
   atomicAdd(&cnt[k], 1);
 }
 
-// Exclusive scan of m ints in one workgroup (1024 threads, each a contiguous chunk); out[m] =
-// total.  Used for the block sums of the multi-workgroup scan below (<= 2^16 of them).
-__global__ void __launch_bounds__(1024) k_scan(const int* in, int m, int* out, long long* total) {
+// Exclusive scan of m 64-bit block sums in one workgroup (1024 threads, each a contiguous chunk);
+// out[m] = total.  Used for the block sums of the multi-workgroup scan below (<= 2^16 of them):
+// 64-bit, so that a dense cluster's pair count (> 2^31 in total) is reported exactly and refused
+// by the caller instead of wrapping.
+__global__ void __launch_bounds__(1024) k_scan(const long long* in, int m, long long* out, long long* total) {
   __shared__ long long part[1024];
   const int t = threadIdx.x;
   const int chunk = (m + 1023) / 1024;
@@ -67,12 +69,12 @@ __global__ void __launch_bounds__(1024) k_scan(const int* in, int m, int* out, l
   }
   long long run = part[t] - s;     // exclusive prefix of this chunk
   for (int i = a; i < b; ++i) {
-    const int v = in[i];
-    out[i] = (int)run;
+    const long long v = in[i];
+    out[i] = run;
     run += v;
   }
   if (t == 1023) {
-    out[m] = (int)part[1023];
+    out[m] = part[1023];
     if (total) *total = part[1023];
   }
 }
@@ -82,41 +84,43 @@ __global__ void __launch_bounds__(1024) k_scan(const int* in, int m, int* out, l
 // workgroup (k_scan), (3) each workgroup's local scan plus its offset.
 constexpr int SCAN_T = 256, SCAN_B = 4 * SCAN_T;
 
-__device__ __forceinline__ int block_excl_scan(int v, int* sh, int& tot) {
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* sh, T& tot) {
   const int t = threadIdx.x;
   sh[t] = v;
   __syncthreads();
   for (int o = 1; o < SCAN_T; o <<= 1) {
-    const int a = t >= o ? sh[t - o] : 0;
+    const T a = t >= o ? sh[t - o] : 0;
     __syncthreads();
     sh[t] += a;
     __syncthreads();
   }
   tot = sh[SCAN_T - 1];
-  const int incl = sh[t];
+  const T incl = sh[t];
   __syncthreads();
   return incl - v;
 }
 
-__global__ void __launch_bounds__(SCAN_T) k_scan_sums(const int* in, int m, int* bsum) {
-  __shared__ int sh[SCAN_T];
+__global__ void __launch_bounds__(SCAN_T) k_scan_sums(const int* in, int m, long long* bsum) {
+  __shared__ long long sh[SCAN_T];
   const int i0 = blockIdx.x * SCAN_B + 4 * threadIdx.x;
-  int v = 0;
+  long long v = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) v += (i0 + k < m) ? in[i0 + k] : 0;
-  int tot;
+  long long tot;
   (void)block_excl_scan(v, sh, tot);
   if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
-__global__ void __launch_bounds__(SCAN_T) k_scan_down(const int* in, int m, const int* boff, int* out) {
+// (int offsets: only used when the caller accepted the 64-bit total, <= 2^30)
+__global__ void __launch_bounds__(SCAN_T) k_scan_down(const int* in, int m, const long long* boff, int* out) {
   __shared__ int sh[SCAN_T];
   const int i0 = blockIdx.x * SCAN_B + 4 * threadIdx.x;
   int e[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) e[k] = (i0 + k < m) ? in[i0 + k] : 0;
   int tot;
-  int run = block_excl_scan(e[0] + e[1] + e[2] + e[3], sh, tot) + boff[blockIdx.x];
+  int run = block_excl_scan<int>(e[0] + e[1] + e[2] + e[3], sh, tot) + (int)boff[blockIdx.x];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (i0 + k < m) out[i0 + k] = run;
@@ -202,7 +206,7 @@ __global__ void __launch_bounds__(DT) k_pairs(const double* xs, const double* rs
 inline int blocks(int n) { return (n + DT - 1) / DT; }
 
 // out[0..m) = exclusive scan of in, out[m] = total (and *total); bsum: (m + SCAN_B - 1) / SCAN_B + 1 ints
-void scan(const int* in, int m, int* out, int* bsum, long long* total, hipStream_t s) {
+void scan(const int* in, int m, int* out, long long* bsum, long long* total, hipStream_t s) {
   const int nb = (m + SCAN_B - 1) / SCAN_B;
   hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(SCAN_T), 0, s, in, m, bsum);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, bsum, nb, bsum, total);   // in place: block offsets
@@ -218,7 +222,7 @@ void scan(const int* in, int m, int* out, int* bsum, long long* total, hipStream
 // 2 * total).  The emit phase takes the bucket-ordered xs, rs of the count phase.
 // Returns 0 after enqueueing the count phase; *total is available after the stream syncs.
 int launch_detect_count(const double* xy, const double* r, int n, double inv_cs, unsigned T, unsigned* key, int* cnt,
-                        int* start, int* fill, int* order, int* pcnt, int* off, long long* total, int* bsum,
+                        int* start, int* fill, int* order, int* pcnt, int* off, long long* total, long long* bsum,
                         double* xs, double* rs, hipStream_t s) {
   const unsigned mask = T - 1;
   if (hipMemsetAsync(cnt, 0, (size_t)T * sizeof(int), s) != hipSuccess) return -1;

@@ -104,6 +104,11 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   const bool last_launch = (flags & F_LAST) != 0;
   const bool global = (flags & F_GLOBAL) != 0;
   const bool coop = (flags & F_COOP) != 0;   // global stop decided in-kernel (cooperative launch)
+  // a component whose step already ended in an earlier launch of this step (per-component stop,
+  // host-stepped by piadmm_outer_iter) runs no further iteration: its state is only carried
+  const bool skip = !first && A.cst[(size_t)ci * 4 + 3] != 0;
+  const int it_end = skip ? it0 : it1;
+  bool stopped = skip;
   int gflag = 0;                             // coop: some pair ever collided (casadi/main.py:115)
   bool nanlast = (flags & F_NANLAST) != 0;
   // ---- seeds (casadi/main.py:48-49) and zero per-step state (:52-63)
@@ -285,7 +290,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   const double thr = c.collide_sq_thres ? deff * deff : deff;
   int flag = first ? 0 : A.cst[(size_t)ci * 4 + 0];
   int aliased = first ? 0 : A.cst[(size_t)ci * 4 + 1];
-  int iters = it0;
+  int iters = skip ? A.iters[ci] : it0;
   int n_xqp = 0, n_zqp = 0, n_admm_x = 0, n_admm_z = 0, n_pdas_x = 0, n_pdas_z = 0, n_inexact = 0, n_gi = 0;
   bool act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
   double dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
@@ -323,7 +328,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     }
   };
   load_cp();
-  for (int it = it0; it < it1; ++it) {
+  for (int it = it0; it < it_end; ++it) {
     iters = it + 1;
     // this iteration's pos_old buffer: a wave may start the next iteration's x-step while
     // the other still reads this one's positions (no second barrier without a z-step)
@@ -379,7 +384,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       }
       act = wany(hit);
     }
-    if (!act && flag == 0 && !c.fixed_iters && !global) break;   // no edge ever: stop (:115-116)
+    if (!act && flag == 0 && !c.fixed_iters && !global) {   // no edge ever: stop (:115-116)
+      stopped = true;
+      break;
+    }
     flag = 1;
     // -------- z-step + dual update on the colliding pair (casadi/main.py:121-162)
     if (__builtin_expect(act && w == 0, 0)) {     // cold: about once per MPC step
@@ -512,8 +520,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     const double sk = act ? S.sc[1] : 0.0;
     if (act) dis_chk = S.sc[2];
     if (!c.fixed_iters && !global && rk <= c.eps_pri && sk <= c.eps_dual &&
-        (!c.term_dist_check || dis_chk > deff))
+        (!c.term_dist_check || dis_chk > deff)) {
+      stopped = true;
       break;
+    }
     if (coop && !c.fixed_iters) {
       // -------- global termination over all components, in-kernel (single rank): the
       // partials of k_term_partials, one grid barrier, every workgroup sums them in the same
@@ -557,6 +567,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       STAMP_ADD(ST_TERM, t_gb);
       if (tact == 0.0 && gflag == 0) {       // no pair collides anywhere: stop (:115-116)
         nanlast = true;
+        stopped = true;
         break;
       }
       gflag = 1;
@@ -565,7 +576,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
         A.ghist[((size_t)slot * c.max_outer + it) * 2 + 1] = tsk;
       }
       const bool dist_ok = tseen > 0.0 && tbad == 0.0;
-      if (trk <= c.eps_pri && tsk <= c.eps_dual && (!c.term_dist_check || dist_ok)) break;
+      if (trk <= c.eps_pri && tsk <= c.eps_dual && (!c.term_dist_check || dist_ok)) {
+        stopped = true;
+        break;
+      }
     }
     if (c.alias_dual_residual) aliased = 1;
   }
@@ -583,7 +597,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned long long* cn = A.counters + (size_t)ci * 8;
-      cn[0] += (unsigned long long)(iters - it0);
+      cn[0] += (unsigned long long)(skip ? 0 : iters - it0);
       for (int k = 0; k < 6; ++k) {
         unsigned long long sum = 0;
         for (int ww = 0; ww < NW; ++ww) sum += (unsigned long long)s_cnt[ww][k];
@@ -603,8 +617,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     }
     A.cst[(size_t)ci * 4 + 0] = flag;
     A.cst[(size_t)ci * 4 + 1] = aliased;
+    A.cst[(size_t)ci * 4 + 3] = stopped ? 1 : 0;
     if (coop && ci == 0) A.giters[slot] = iters;
-    if (nanlast && iters > 0) {      // global stop at the collision test of this iteration
+    if (nanlast && iters > 0 && !skip) {      // global stop at the collision test of this iteration
       resid[2 * (iters - 1) + 0] = NAN;
       resid[2 * (iters - 1) + 1] = NAN;
     }
@@ -620,7 +635,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   }
   if (w < na) {
     const int a = a0 + w;
-    const double* posl = S.pos + ((iters - 1) & 1) * 4 * H1;   // the last executed iteration's buffer
+    // the last executed iteration's buffer (a skipped launch: the buffer its state was restored to)
+    const double* posl = S.pos + ((skip ? it0 - 1 : iters - 1) & 1) * 4 * H1;
     for (int i = l; i < 2 * H1; i += WAVE) A.pos_old[(size_t)a * 2 * H1 + i] = posl[w * 2 * H1 + i];
     const double u = (l < H) ? S.u[w * H + l] : 0.0;
     if (l < H) A.u[(size_t)a * H + l] = u;

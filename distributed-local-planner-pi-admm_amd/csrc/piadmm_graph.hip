@@ -93,7 +93,10 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GW
     for (int k = k0; k < k1; ++k) rs = rs + A.rho_pi[A.nbr_edge[k]];
     coef = 2.0 * c.Pnorm + rs;
   }
+  unsigned long long t_su = STAMP_T();
   const bool rebuilt = setup_agent(A, a, qx, gx, W.fac, coef);
+  STAMP_ADD(ST_SETUP_X, t_su);
+  STAMP_CNT(ST_N_XREBUILD, rebuilt ? 1 : 0);
   // warm state of this QP (written by the previous x-step of the agent, or the step init)
   const double* qs = A.qs_x + (size_t)a * 5 * WAVE;
   const signed char* ql = A.ql_x + (size_t)a * 2 * WAVE;
@@ -124,8 +127,12 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GW
   qx.wq = (l < H) ? wsh : 0.0;
   qx.qvalid = false;
   double ustar[1];
+  unsigned long long t_q = STAMP_T();
+  const int gi0 = n.gi;
   const int st = qp_solve<1, false, 8>(qx, xs, zs, ys, lab, warm, c.max_inner, c.polish_every, W.fac, qx.fld, ustar,
                                        n.admm_x, n.pdas_x, n.gi);
+  STAMP_ADD(ST_XQP, t_q);
+  STAMP_CNT(ST_N_GIX, n.gi - gi0);
   ++n.xqp;
   n.inexact += (st & PIADMM_QP_INEXACT) ? 1 : 0;
   // round (casadi/main.py:103), pos_old = dynamic_update_local (:105)
@@ -244,7 +251,9 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
   if (l == 0) W.zfs[0] = -1;
   wsync();
   const double sd[4] = {A.seed_g[2 * v1], A.seed_g[2 * v1 + 1], A.seed_g[2 * v2], A.seed_g[2 * v2 + 1]};
+  unsigned long long t_sz = STAMP_T();
   setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, sd, W.fac, Ke, deff, gpi ? rw : -1.0);
+  STAMP_ADD(ST_SETUP_Z, t_sz);
   const double* qs = A.qs_e + (size_t)e * 12 * WAVE;
   const signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
   double xs[2] = {qs[l], qs[WAVE + l]}, zs[5], ys[5];
@@ -275,8 +284,14 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
     qe.qvalid = true;
   }
   double uh[2];
+  unsigned long long t_zq = STAMP_T();
+  const int giz0 = n.gi;
   const int st = qp_solve<2, BIG>(qe, xs, zs, ys, lab, warm, c.max_inner, c.polish_every, BIG ? Ke : W.fac,
                                   BIG ? 2 * H : LD, uh, n.admm_z, n.pdas_z, n.gi);
+  STAMP_ADD(ST_ZQP, t_zq);
+  STAMP_CNT(ST_N_GIZ, n.gi - giz0);
+  STAMP_CNT(ST_N_ZQP, 1);
+  STAMP_CNT(ST_N_ZFAIL, (st & PIADMM_QP_INEXACT) ? 1 : 0);
   ++n.zqp;
   n.inexact += (st & PIADMM_QP_INEXACT) ? 1 : 0;
   // hat positions: nonlinear rollout of the rounded pair controls (casadi/main.py:153-158)
@@ -539,8 +554,14 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   const bool xonly = (flags & F_XONLY) != 0;
   const bool zonly = (flags & F_ZONLY) != 0;
   bool nanlast = (flags & F_NANLAST) != 0;
+  // a component whose step already ended in an earlier launch of this step (per-component stop,
+  // host-stepped by piadmm_outer_iter) runs no further iteration
+  const bool skip = !first && A.cst[(size_t)ci * 4 + 3] != 0;
+  const int it_end = skip ? it0 : it1;
+  bool stopped = skip;
   double* resid = A.resid + ((size_t)slot * A.C + ci) * M * 2;
 
+  unsigned long long t_body = STAMP_T();
   if (first) {
     g_step_init(A, ci, w);
     for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
@@ -560,16 +581,20 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   }
   __syncthreads();
   GCnt n;
-  int iters = it0, gflag = 0;
-  for (int it = it0; it < it1; ++it) {
+  int iters = skip ? A.iters[ci] : it0, gflag = 0;
+  for (int it = it0; it < it_end; ++it) {
     iters = it + 1;
     // -------- X: x-steps of the component's agents (casadi/main.py:81-106)
     if (!(zonly && it == it0)) {
+      unsigned long long t_xp = STAMP_T();
       for (int i = a0 + w; i < a1; i += GW) {
         const int a = A.comp_alist[i];
         if (!A.owned || A.owned[a]) g_xstep<BIG>(A, a, t, W, n);
       }
+      STAMP_ADD(ST_XSTEP, t_xp);
+      unsigned long long t_sa = STAMP_T();
       __syncthreads();
+      STAMP_ADD(ST_SYNC_A, t_sa);
     }
     if (xonly) break;
     // -------- ghosts (sharded job): the positions and controls their owner rank computed in this
@@ -586,8 +611,13 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       __syncthreads();
     }
     // -------- Z: collision test + pair QPs + dual updates (casadi/main.py:110-162)
+    unsigned long long t_zp = STAMP_T();
     for (int j = e0 + w; j < e1; j += GW) g_zstep<BIG>(A, A.comp_elist[j], t, W, n);
+    STAMP_ADD(ST_ZSTEP, t_zp);
+    unsigned long long t_sb = STAMP_T();
     __syncthreads();
+    STAMP_ADD(ST_SYNC_B, t_sb);
+    unsigned long long t_tm = STAMP_T();
     // -------- T: the component's residuals in pair order and the stop rules (:164-181)
     if (threadIdx.x == 0) {
       double rk = 0.0, sk = 0.0, nact = 0.0, nseen = 0.0, nbad = 0.0;
@@ -622,7 +652,11 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
     const bool anyact = s_sc[2] != 0.0;
     const bool dist_ok = s_sc[3] > 0.0 && s_sc[4] == 0.0;
     __syncthreads();
-    if (!anyact && flag == 0 && !c.fixed_iters && !global) break;    // no pair collided: stop (:115-116)
+    STAMP_ADD(ST_TERM, t_tm);
+    if (!anyact && flag == 0 && !c.fixed_iters && !global) {    // no pair collided: stop (:115-116)
+      stopped = true;
+      break;
+    }
     flag = 1;
     if (threadIdx.x == 0) {
       resid[2 * it + 0] = rk;
@@ -660,6 +694,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       __syncthreads();
       if (tact == 0.0 && gflag == 0) {       // no pair collides anywhere: stop (:115-116)
         nanlast = true;
+        stopped = true;
         break;
       }
       gflag = 1;
@@ -669,7 +704,10 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       }
       if (trk <= c.eps_pri && tsk <= c.eps_dual && (!c.term_dist_check || (tseen > 0.0 && tbad == 0.0))) stop = true;
     }
-    if (stop) break;
+    if (stop) {
+      stopped = true;
+      break;
+    }
     // last_iter_hat_pos = hat_pos_old (casadi/main.py:180; MATLAB copies): after the decision
     // (host-decided global termination: at the start of the next launch, once the host has
     // decided to continue)
@@ -691,7 +729,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long* cn = A.counters + (size_t)ci * 8;
-    if (!xonly) cn[0] += (unsigned long long)(iters - it0);
+    if (!xonly && !skip) cn[0] += (unsigned long long)(iters - it0);
     for (int k = 0; k < 7; ++k) {
       unsigned long long sum = 0;
       for (int ww = 0; ww < GW; ++ww) sum += (unsigned long long)s_cnt[ww][k];
@@ -700,22 +738,31 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
     if (!xonly) A.iters[ci] = iters;
     A.cst[(size_t)ci * 4 + 0] = flag;
     A.cst[(size_t)ci * 4 + 1] = aliased;
+    if (!xonly) A.cst[(size_t)ci * 4 + 3] = stopped ? 1 : 0;
     if (coop && ci == 0) A.giters[slot] = iters;
-    if (nanlast && iters > 0) {
+    if (nanlast && iters > 0 && !skip) {
       resid[2 * (iters - 1) + 0] = NAN;
       resid[2 * (iters - 1) + 1] = NAN;
     }
   }
   if (last_launch) g_step_final(A, ci, w);
+  STAMP_ADD(ST_KERNEL, t_body);
 }
 
 template <bool BIG>
 __global__ void __launch_bounds__(GW * WAVE) k_graph_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
+#ifdef PIADMM_STAMPS
+  if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
+  __syncthreads();
+#endif
   int nbar = 0;
   for (int k = 0; k < nsteps; ++k) {
     graph_step_body<BIG>(A, t0 + k, it0, it1, flags, k, nbar);
     __syncthreads();
   }
+#ifdef PIADMM_STAMPS
+  if (threadIdx.x < 64 && g_stamps) atomicAdd(&g_stamps[blockIdx.x * 64 + threadIdx.x], s_stamps[threadIdx.x]);
+#endif
 }
 
 }  // namespace pd
@@ -742,6 +789,13 @@ __global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double*
 
 int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s) {
   const size_t sh = graph_lds_bytes(a.cfg.H);
+#ifdef PIADMM_STAMPS
+  static unsigned long long* last = nullptr;
+  if (a.stamps != last) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &a.stamps, sizeof(void*)) != hipSuccess) return -1;
+    last = a.stamps;
+  }
+#endif
   const bool big = a.cfg.H > HMAX;
   const void* fn = big ? (const void*)k_graph_step<true> : (const void*)k_graph_step<false>;
   if (launch_rc(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)) != 0) return -1;

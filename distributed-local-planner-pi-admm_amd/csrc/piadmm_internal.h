@@ -187,9 +187,9 @@ constexpr int F_ZONLY = 64;
 int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 // candidate-pair detection (piadmm_detect.hip)
 int launch_detect_count(const double* xy, const double* r, int n, double inv_cs, unsigned T, unsigned* key, int* cnt,
-                        int* start, int* fill, int* order, int* pcnt, int* off, long long* total, int* bsum,
+                        int* start, int* fill, int* order, int* pcnt, int* off, long long* total, long long* bsum,
                         double* xs, double* rs, hipStream_t s);
-constexpr int DETECT_SCAN_B = 1024;   // ints per workgroup of the detection's scans (bsum sizing)
+constexpr int DETECT_SCAN_B = 1024;   // ints per workgroup of the detection's scans (bsum sizing, 64-bit sums)
 int launch_detect_emit(const double* xs, const double* rs, int n, double inv_cs, unsigned T, const int* start,
                        const int* order, const int* off, int* out, hipStream_t s);
 bool graph_coop_fits(const DevArgs& a, int device);

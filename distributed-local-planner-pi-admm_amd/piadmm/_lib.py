@@ -69,7 +69,9 @@ SYMBOLS = [
     ("piadmm_mpc_steps_async", c_i32, [_H, c_i32, c_i32]),
     ("piadmm_sync", c_i32, [_H]),
     ("piadmm_time_steps", c_i32, [_H, c_i32, c_i32, _P(ctypes.c_float)]),
-    ("piadmm_get_state", c_i32, [_H, _dp, _dp, _dp, _dp, _dp, _P(ctypes.c_uint8), _ip]),
+    ("piadmm_get_state", c_i32, [_H, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _P(ctypes.c_uint8), _ip]),
+    ("piadmm_outer_iter", c_i32, [_H, c_i32, c_i32, _ip]),
+    ("piadmm_step_finish", c_i32, [_H, _dp, _dp]),
     ("piadmm_n_components", c_i32, [_H]),
     ("piadmm_steps_per_launch", c_i32, [_H]),
     ("piadmm_get_counters", c_i32, [_H, _P(ctypes.c_uint64)]),

@@ -29,7 +29,9 @@ def reach_radii(cfg, spd, theta=None) -> np.ndarray:
     |p_k - p_0| <= sum_k dt s sqrt(1 + (k dt s u_max / L)^2).  Plus half the collision distance
     (sqrt(dis_thres) for the Python test d^2 < dis_thres, quirk B2; dis_thres for MATLAB's) and,
     with ``tighten``, the agent's delay offset |delta| (decentralized/util.py:81-96) at heading
-    ``theta`` (the worst heading when None)."""
+    ``theta`` (the worst heading when None): MATLAB's test adds |delta_i| per agent; the Python
+    test's distance sqrt(dis_thres + |delta_i| + |delta_j|) is bounded by half of
+    sqrt(dis_thres + 2 max |delta|) per agent."""
     spd = np.asarray(spd, np.float64)
     H, dt = cfg.H, cfg.dt
     k = np.arange(H, dtype=np.float64)
@@ -49,7 +51,13 @@ def reach_radii(cfg, spd, theta=None) -> np.ndarray:
             c, s = np.cos(theta), np.sin(theta)
             d = np.hypot(cfg.avg_delay * spd * c + kap * (cfg.var_delay * spd * c) ** 2,
                          cfg.avg_delay * spd * s + kap * (cfg.var_delay * spd * s) ** 2)
-        r = r + d
+        if cfg.collide_sq_thres:
+            r = r + d               # MATLAB test d < d_eff = dis_thres + |delta_i| + |delta_j|
+        else:
+            # Python test d^2 < d_eff (quirk B2): the collision distance sqrt(dis_thres + |delta_i| +
+            # |delta_j|) is at most sqrt(dis_thres + 2 max |delta|), split evenly over the pair (the
+            # per-agent 0.5 sqrt(dis_thres) + |delta_i| bounds it only when 2 sqrt(dis_thres) + delta >= 1)
+            r = reach + 0.5 * math.sqrt(cfg.dis_thres + 2.0 * float(np.max(d)) if d.size else cfg.dis_thres)
     # a little slack over the rounding of the positions (u rounded to 1e-4, B6)
     return r * (1.0 + 1e-9) + 1e-9
 

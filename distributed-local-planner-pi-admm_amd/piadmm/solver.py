@@ -149,6 +149,12 @@ class PI_ADMM_MI355X:
         casadi/main.py:52-63)."""
         if self.shard is not None:
             raise ValueError("a sharded handle keeps its graph")
+        if self.cfg.dual_mode == 2:
+            # the global-PI law keeps each pair's adaptive penalty across MPC steps
+            # (casadi_old_PI_ADMM/main.py:137-139, PI_ADMM.param.rho is never reset); a new
+            # scenario would restart every pair from cfg.rho, silently departing from that law
+            raise ValueError("set_candidate_graph does not carry the global-PI pair penalties "
+                             "(dual_mode 2): keep a static candidate graph for that preset")
         edges = np.ascontiguousarray(edges, np.int32).reshape(-1, 2)
         self.scn = Scenario(spd=self.scn.spd, xt0=np.ascontiguousarray(self.xt, np.float64), ref=self.scn.ref,
                             edges=edges, n_steps=self.scn.n_steps)
@@ -203,17 +209,39 @@ class PI_ADMM_MI355X:
         self.xt = xt.copy()
 
     def state(self) -> dict:
+        """xt, u, pos_old, hat, lam and the PI accumulators S, D (ADMM_CVX_..._PI_antiwindup.m:160-188)
+        of the last step -- or of the last outer iteration of a host-stepped step."""
         H1 = self.cfg.H + 1
         out = dict(xt=np.empty((self.N, 3)), u=np.empty((self.N, self.cfg.H)),
                    pos_old=np.empty((self.N, 2, H1)), hat=np.empty((self.E, 2, 2, H1)),
-                   lam=np.empty((self.E, 2, 2, H1)), edge_active=np.empty(self.E, np.uint8),
-                   iters=np.empty(self.C, np.int32))
+                   lam=np.empty((self.E, 2, 2, H1)), S=np.empty((self.E, 2, 2, H1)), D=np.empty((self.E, 2, 2, H1)),
+                   edge_active=np.empty(self.E, np.uint8), iters=np.empty(self.C, np.int32))
         ea = out["edge_active"].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if self.E else None
+        e = (lambda k: _lib.dptr(out[k]) if self.E else None)
         self._check(self.lib.piadmm_get_state(
             self._h, _lib.dptr(out["xt"]), _lib.dptr(out["u"]), _lib.dptr(out["pos_old"]),
-            _lib.dptr(out["hat"]) if self.E else None, _lib.dptr(out["lam"]) if self.E else None,
-            ea, _lib.iptr(out["iters"])))
+            e("hat"), e("lam"), e("S"), e("D"), ea, _lib.iptr(out["iters"])))
         return out
+
+    def outer_iter(self, it: int, t: int | None = None) -> bool:
+        """ONE outer ADMM iteration of MPC step t (``for i_iter``, casadi/main.py:78-181): it = 0
+        starts the step, then 1, 2, ... in order; :meth:`state` shows the iteration's pos_old, hat,
+        lam, S, D.  Returns True when the reference's stop rules end the step here.  Finish the
+        step with :meth:`step_finish`."""
+        t = self.t if t is None else t
+        stop = ctypes.c_int32()
+        self._check(self.lib.piadmm_outer_iter(self._h, int(t), int(it), ctypes.byref(stop)))
+        self._stepping = int(t)
+        return bool(stop.value)
+
+    def step_finish(self):
+        """Propagate a host-stepped MPC step (casadi/main.py:185-192); returns (xt, u)."""
+        xt = np.empty((self.N, 3))
+        u = np.empty((self.N, self.cfg.H))
+        self._check(self.lib.piadmm_step_finish(self._h, _lib.dptr(xt), _lib.dptr(u)))
+        self.t = getattr(self, "_stepping", self.t) + 1
+        self.xt = xt
+        return xt, u
 
     def close(self):
         if getattr(self, "_h", None):

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PIADMM_ABI_VERSION 3
+#define PIADMM_ABI_VERSION 4
 
 enum {
   PIADMM_OK = 0,
@@ -173,11 +173,25 @@ int32_t piadmm_sync(piadmm_handle_t h);
 /* Device time (ms, hipEvent on the handle's stream) of n_steps MPC steps from t0. */
 int32_t piadmm_time_steps(piadmm_handle_t h, int32_t t0, int32_t n_steps, float* ms_out);
 
-/* State of the last step (any pointer may be NULL):
- *   xt N x 3, u N x H, pos_old N x 2 x (H+1), hat / lam E x 2 x 2 x (H+1)
- *   (direction 0 = hat_{v1 v2}, 1 = hat_{v2 v1}), edge_active E, iters C. */
+/* State of the last step, or of the last outer iteration of a host-stepped step (any pointer
+ * may be NULL):
+ *   xt N x 3, u N x H, pos_old N x 2 x (H+1), hat / lam / S / D E x 2 x 2 x (H+1)
+ *   (direction 0 = hat_{v1 v2}, 1 = hat_{v2 v1}; S, D: the PI integral and back-calculation
+ *   term of ADMM_CVX_..._PI_antiwindup.m:160-188), edge_active E, iters C.  (ABI 4: S, D added.) */
 int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_old,
-                         double* hat, double* lam, uint8_t* edge_active, int32_t* iters);
+                         double* hat, double* lam, double* S, double* D, uint8_t* edge_active, int32_t* iters);
+
+/* Host stepping of ONE outer ADMM iteration of MPC step t (the body of
+ * `for i_iter in range(iter_num)`, casadi/main.py:78-181): it = 0 starts the step (seeds, the
+ * per-step reset of :52-63), it = 1, 2, ... continue it in order.  After each call
+ * piadmm_get_state shows pos_old, hat, lam, S, D of that iteration.  *stop_out (may be NULL) = 1
+ * when the reference's stop rules end the step at this iteration (casadi/main.py:115-118,174-178:
+ * over all agents with term_global, else once every component has stopped -- a stopped
+ * component keeps its state while the others continue).  Calling on after a stop, or out of
+ * order, is PIADMM_E_STATE.  piadmm_step_finish then propagates (casadi/main.py:185-192); no
+ * other step call is accepted while a host-stepped step is open.  Not for sharded graphs. */
+int32_t piadmm_outer_iter(piadmm_handle_t h, int32_t t, int32_t it, int32_t* stop_out);
+int32_t piadmm_step_finish(piadmm_handle_t h, double* xt_out /* N x 3 */, double* u_out /* N x H */);
 
 int32_t piadmm_n_components(piadmm_handle_t h);
 /* MPC steps per persistent launch (after set_scenario; 1 under global natural termination). */
@@ -212,8 +226,11 @@ int32_t piadmm_global_resid(piadmm_handle_t h, double* resid_out, int32_t* iters
 /* Candidate pairs for large N: all pairs i < j of the n points
  * xy (n x 2) with |xy_i - xy_j| <= radius_i + radius_j, in increasing (i, j) order, found on a
  * uniform grid hash in O(n) on the handle's device (replaces the O(N^2) pair loop of
- * casadi/main.py:110-113 as the source of the candidate graph: with radius_i = spd_i H dt +
- * d / 2 -- piadmm.candidates.reach_radii -- no other pair can collide within the horizon).
+ * casadi/main.py:110-113 as the source of the candidate graph).  With radius_i the reach bound
+ * of piadmm.candidates.reach_radii no other pair can collide within the horizon: for the
+ * linearised position model (pos_model 0) it is sum_k dt s sqrt(1 + (k dt s u_max / L)^2) plus half
+ * the collision distance (and the delay offset with tighten) -- NOT the constant-speed s H dt,
+ * which the linearised rollout can exceed.
  * Writes min(total, max_pairs) pairs to pairs_out (max_pairs x 2) and the total to
  * *n_pairs_out (call again with a larger buffer when total > max_pairs); ms_out (may be NULL):
  * device time of the detection kernels, inputs resident. */

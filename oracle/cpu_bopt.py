@@ -96,14 +96,18 @@ def run(cfg, scn, n_steps: int, threads: int = 1, t0: int = 0, records: bool = T
 
 
 def time_baseline(cfg, n_tiles: int, budget_s: float, n_steps: int = 20, threads: int | None = None,
-                  perturb: bool = True) -> dict:
-    """Outer iterations per second of the n_tiles-tile job (bench.py's workload: seeded tiles,
-    fixed outer iterations) on `threads` host cores: median of repeats within ~budget_s."""
+                  perturb: bool = True, scn=None, desc: str | None = None) -> dict:
+    """Outer iterations per second of the job (bench.py's workload: by default n_tiles seeded tiles;
+    ``scn``: any candidate graph), fixed outer iterations, on the host cores oracle.hostinfo
+    reports: median and spread of repeats within ~budget_s."""
     import time
     from piadmm import scenario
-    ncpu = os.cpu_count() or 1
-    threads = threads or max(1, min(16, ncpu))      # the GPU box's CPU share is 16 cores
-    scn = scenario.tiled(n_tiles, cfg.H, n_steps=n_steps, perturb=perturb, seed=0)
+
+    from oracle import hostinfo
+    hi = hostinfo.host_cpu()
+    threads = threads or hi["threads"]
+    if scn is None:
+        scn = scenario.tiled(n_tiles, cfg.H, n_steps=n_steps, perturb=perturb, seed=0)
     run(cfg, scn, 1, threads, records=False)            # warm-up (page-in, thread pool)
     times, t_end, cnt = [], time.perf_counter() + budget_s, None
     while len(times) < 5 or (time.perf_counter() < t_end and len(times) < 15):
@@ -112,15 +116,23 @@ def time_baseline(cfg, n_tiles: int, budget_s: float, n_steps: int = 20, threads
         cnt = r["counters"]
         if time.perf_counter() > t_end and len(times) >= 1 and times[0] * 5 > budget_s:
             break
-    med = float(np.median(times))
+    ts = np.sort(np.asarray(times))
+    med = float(np.median(ts))
     it_per_step = cfg.max_outer if cfg.fixed_iters else None
     value = n_steps * it_per_step / med if it_per_step else None
+    job = desc or f"{n_tiles} tiles"
     return {"value": value, "unit": "outer_iters/s", "cores": threads, "kind": "port",
             "ms_per_step": 1e3 * med / n_steps,
-            "sample": f"B-opt: C++ -O3 (x86-64-v3) + OpenMP over tiles, {threads} threads "
+            "spread": {"runs": len(ts), "min_ms_per_step": 1e3 * float(ts[0]) / n_steps,
+                       "max_ms_per_step": 1e3 * float(ts[-1]) / n_steps,
+                       "iqr_ms_per_step": 1e3 * float(np.percentile(ts, 75) - np.percentile(ts, 25)) / n_steps},
+            "host": hi,
+            "sample": f"B-opt: C++ -O3 (x86-64-v3) + OpenMP over components, "
+                      f"{hostinfo.describe(hi) if threads == hi['threads'] else f'{threads} threads'} "
                       f"(oracle/piadmm_cpu.cpp: the GPU kernel's algorithm -- dual active set with bounded "
                       f"hinge multipliers, cached working-set factors -- exact answers, equal to the oracle, "
-                      f"tests/test_cpu_bopt.py); the full job: {n_tiles} tiles x MPC steps 0..{n_steps - 1} x "
-                      f"{cfg.max_outer} outer iterations, median of {len(times)} runs ({med:.3f} s each); "
+                      f"tests/test_cpu_bopt.py); the full job: {job} x MPC steps 0..{n_steps - 1} x "
+                      f"{cfg.max_outer} outer iterations, median of {len(times)} runs ({med:.3f} s each, "
+                      f"min {ts[0]:.3f} max {ts[-1]:.3f}); "
                       f"{cnt['x_qps']} x-QPs ({cnt['x_hits']} cached-set hits), {cnt['z_qps']} pair QPs, "
-                      f"{cnt['inexact']} uncertified per run; host {ncpu} cpus visible"}
+                      f"{cnt['inexact']} uncertified per run"}

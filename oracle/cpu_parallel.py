@@ -50,8 +50,9 @@ def _worker(args):
 
 def time_baseline(cfg, n_tiles: int, budget_s: float, n_steps: int = 5, workers: int | None = None) -> dict:
     """Outer iterations per second of the n_tiles-tile job on all host cores (bounded sample)."""
-    ncpu = os.cpu_count() or 1
-    workers = workers or max(1, min(16, ncpu))      # the GPU box's CPU share is 16 cores
+    from oracle import hostinfo
+    hi = hostinfo.host_cpu()
+    workers = workers or hi["threads"]
     ctx = mp.get_context("spawn")
     deadline = time.time() + budget_s
     jobs = [(cfg, n_tiles, cfg.H, n_steps, list(range(w, n_tiles, workers)), deadline) for w in range(workers)]
@@ -69,5 +70,4 @@ def time_baseline(cfg, n_tiles: int, budget_s: float, n_steps: int = 5, workers:
                       f"casadi/main.py) on a pool of {workers} processes x 1 BLAS thread, {tiles} of {n_tiles} "
                       f"tiles x MPC steps 0..{n_steps - 1} x {cfg.max_outer} outer iterations (fixed) in "
                       f"{wall:.1f} s wall ({busy:.0f} core-s of compute); job rate = sum of the workers' tile-iterations/s "
-                      f"/ {n_tiles}; "
-                      f"host {ncpu} cpus visible"}
+                      f"/ {n_tiles}; {hostinfo.describe(hi)}", "host": hi}

@@ -335,7 +335,7 @@ class Oracle:
         sy = around(xt[:, 1] + c.dt * self.scn.spd * np.sin(xt[:, 2]), c.round_decimals)
         return np.stack([sx, sy], axis=1)
 
-    def mpc_step(self, components=None, reduce=None, exchange=None) -> StepRecord:
+    def mpc_step(self, components=None, reduce=None, exchange=None, on_iter=None) -> StepRecord:
         """One ``num_step`` body of ``casadi/main.py:43-201``.
 
         Iteration-major: every outer iteration runs the x-steps of all agents, the
@@ -350,6 +350,10 @@ class Oracle:
         all processes: the all-reduce of the sharded path (tests/test_dist.py runs it on gloo).
         ``exchange(pos_old, primal_u)`` (a rank of a job whose pairs cross ranks) fills the ghost
         agents' rows in place after the x-steps: the boundary all-reduce of the sharded path.
+        ``on_iter(it, state)`` is called after every outer iteration with copies of pos_old, hat,
+        lam, S, D and ``stop`` (every termination group has stopped): the per-iteration state of
+        ``casadi/main.py:78-181`` / ``ADMM_CVX_..._PI_antiwindup.m:160-188`` that
+        ``piadmm_outer_iter`` exposes.
         """
         cfg, H, N, E = self.cfg, self.H, self.N, self.E
         if exchange is not None and not cfg.term_global:
@@ -468,6 +472,9 @@ class Oracle:
                     g_alias[g] = True
                 else:
                     last_hat[edges] = hat[edges]
+            if on_iter is not None:
+                on_iter(it, dict(pos_old=pos_old.copy(), hat=hat.copy(), lam=lam.copy(), S=S.copy(), D=D.copy(),
+                                 stop=all(g_done)))
         self.edge_state = (hat.copy(), lam.copy(), S.copy(), D.copy(), last_hat.copy())
         # ---- propagation, casadi/main.py:185-192 (of the components that ran)
         new_xt = self.xt.copy()

@@ -300,6 +300,10 @@ def test_errors_are_loud(Solver):
     bad.edges = np.array([[2, 0]], np.int32)
     with pytest.raises(_lib.PiadmmError, match="edge must satisfy"):
         Solver(config.matlab_pi(H=10), bad)
+    dup = scenario.tiled(2, 10)
+    dup.edges = np.array([[0, 1], [2, 3], [0, 1]], np.int32)     # the same pair twice
+    with pytest.raises(_lib.PiadmmError, match="duplicate candidate pair"):
+        Solver(config.matlab_pi(H=10), dup)
     with Solver(config.matlab_pi(H=10), scenario.intersection(10)) as s:
         with pytest.raises(_lib.PiadmmError, match="time index"):
             s.mpc_step(t=41)

@@ -148,3 +148,91 @@ def test_shard_argument_errors(Solver):
     from piadmm._lib import PiadmmError
     with pytest.raises(PiadmmError, match="term_global"):
         Solver(config.matlab_pi(H=10), shard=sh)
+
+
+def run_ranks(Solver, cfg, rank_scns, n_steps, shards=None):
+    """One handle per rank (threads on device 0, host all-reduce transport); mpc_step n_steps
+    times on every rank.  rank_scns: plain per-rank scenarios (whole components per rank), or
+    None with ``shards`` (pairs across ranks)."""
+    world = len(shards) if shards is not None else len(rank_scns)
+    ar = ThreadAllReduce(world)
+    solvers = []
+    for r in range(world):
+        s = Solver(cfg, shard=shards[r]) if shards is not None else Solver(cfg, rank_scns[r])
+        s.set_allreduce(ar.fn(r))
+        solvers.append(s)
+    out = [[] for _ in range(world)]
+    err = [None] * world
+
+    def work(r):
+        try:
+            for _ in range(n_steps):
+                out[r].append(solvers[r].mpc_step())
+        except Exception as e:          # noqa: BLE001 -- reported below
+            err[r] = e
+            ar.bar.abort()
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=900)
+    for s in solvers:
+        s.close()
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    for e in err:
+        if e is not None:
+            raise e
+    return out, ar
+
+
+@pytest.mark.parametrize("split", ["contiguous", "interleaved"])
+def test_config3_1024_agents_over_8_ranks(Solver, split):
+    """BASELINE.json configs[3] at its stated shape: 1024 agents x H30 (512 seeded tiles),
+    matlab_pi, the reference's global scope with fixed 100 outer iterations (the bench's mode),
+    sharded over 8 ranks -- ``contiguous``: whole tiles per rank (bench.py --strong, dist.shard:
+    128 agents per rank, no boundary, one all-reduce of the residual history per step);
+    ``interleaved``: agent a on rank a % 8, so every pair crosses ranks (bench.py --strong --split
+    interleaved: 128 own agents + 128 ghosts per rank, one all-reduce of the 1024-slot boundary
+    exchange buffer per outer iteration).  8 ranks = 8 threads with their own handles on the one
+    MI355X (host transport).  Equal to the unsharded 1024-agent job on one handle to 1e-10, the
+    job's residual history to 1e-9, and sampled tiles equal to the oracle (1e-8)."""
+    H, world, n_steps = 30, 8, 3
+    full = scenario.tiled(512, H, n_steps=n_steps + 2, perturb=True, seed=0)
+    N = full.n_agents
+    cfg = config.matlab_pi(H=H, fixed_iters=1, max_outer=100, term_global=1)
+    if split == "contiguous":
+        scns = [dist.shard(full, r, world) for r in range(world)]
+        out, ar = run_ranks(Solver, cfg, scns, n_steps)
+        bounds = [dist.shard_bounds(full, r, world) for r in range(world)]
+    else:
+        shards = [dist.shard_graph(full, r, world, dist.owners_interleaved(N, world)) for r in range(world)]
+        assert shards[0].n_slots == N
+        out, ar = run_ranks(Solver, cfg, None, n_steps, shards)
+    assert min(ar.calls) >= n_steps
+    with Solver(cfg, full) as s1:
+        ref = [s1.mpc_step() for _ in range(n_steps)]
+    for k in range(n_steps):
+        if split == "contiguous":
+            xt = np.concatenate([out[r][k].xt for r in range(world)])
+            u = np.concatenate([out[r][k].u for r in range(world)])
+            assert [b[1] - b[0] for b in bounds] == [128] * world
+            for r in range(world):
+                assert np.all(out[r][k].status == 0)
+        else:
+            xt, u = gather(shards, out, k, N, H)
+        np.testing.assert_allclose(xt, ref[k].xt, rtol=1e-10, atol=1e-10, err_msg=f"step {k}")
+        np.testing.assert_allclose(u, ref[k].u, rtol=1e-10, atol=1e-10, err_msg=f"step {k}")
+        for r in range(world):
+            assert out[r][k].global_iters == ref[k].global_iters == 100
+            np.testing.assert_allclose(out[r][k].global_resid, ref[k].global_resid, rtol=1e-9, atol=1e-12)
+    # sampled tiles against the oracle (under fixed iterations a tile's trajectory is its own:
+    # the global scope only sums the residual history)
+    for k in (0, 357):
+        sub = scenario.Scenario(spd=full.spd[2 * k:2 * k + 2], xt0=full.xt0[2 * k:2 * k + 2],
+                                ref=full.ref[2 * k:2 * k + 2], edges=np.array([[0, 1]], np.int32),
+                                n_steps=full.n_steps)
+        orc = O.Oracle(cfg, sub)
+        for j in range(n_steps):
+            ro = orc.mpc_step()
+            np.testing.assert_allclose(ref[j].xt[2 * k:2 * k + 2], ro.xt, rtol=1e-8, atol=1e-8)
+            np.testing.assert_allclose(ref[j].u[2 * k:2 * k + 2], ro.u, rtol=1e-8, atol=1e-8)
