@@ -684,12 +684,17 @@ static int32_t global_iteration(piadmm_handle_t h, int32_t tk, int it, int& flag
   HIPCHK(h, hipStreamSynchronize(s));
   const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
   const double n_seen = h->h_part[3], n_bad = h->h_part[4];
-  if (n_act == 0.0 && flag == 0) {      // no pair collides anywhere: stop (casadi/main.py:115-116)
+  if (n_act == 0.0 && flag == 0 && !c.fixed_iters) {   // no pair collides anywhere: stop (casadi/main.py:115-116)
     nanlast = 1;
     *stop = 1;
     return PIADMM_OK;
   }
   flag = 1;
+  if (c.fixed_iters) {                  // throughput mode: the history only, never a stop
+    h->ghist[2 * it + 0] = rk;
+    h->ghist[2 * it + 1] = sk;
+    return PIADMM_OK;
+  }
   h->ghist[2 * it + 0] = rk;
   h->ghist[2 * it + 1] = sk;
   const bool dist_ok = n_seen > 0.0 && n_bad == 0.0;

@@ -28,8 +28,8 @@ def Solver():
     return PI_ADMM_MI355X
 
 
-def close(a, b, what, it):
-    np.testing.assert_allclose(a, b, rtol=TOL, atol=TOL, err_msg=f"{what} after outer iteration {it}")
+def close(a, b, what, it, scale=1.0):
+    np.testing.assert_allclose(a, b, rtol=TOL, atol=TOL * scale, err_msg=f"{what} after outer iteration {it}")
 
 
 def step_by_iterations(s, orc, t, check_sd=True):
@@ -44,7 +44,9 @@ def step_by_iterations(s, orc, t, check_sd=True):
         close(g["lam"], ost["lam"], "lam", it)
         if check_sd:
             close(g["S"], ost["S"], "S", it)
-            close(g["D"], ost["D"], "D", it)
+            # D = lam_sat - lam_raw with lam_raw = S + K_P e: a difference of O(|S|) quantities, so
+            # its absolute error scales with |S| (the integral grows over the step's iterations)
+            close(g["D"], ost["D"], "D", it, scale=max(1.0, float(np.max(np.abs(ost["S"])))))
         assert stop == ost["stop"], f"stop flag at outer iteration {it}"
     xt, u = s.step_finish()
     np.testing.assert_allclose(xt, rec.xt, rtol=TOL, atol=TOL)
