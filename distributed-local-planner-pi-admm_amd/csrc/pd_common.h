@@ -36,7 +36,10 @@ enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL
                  ST_ZR_SOLVE, ST_XR_SOLVE, ST_ZKKT, ST_XKKT, ST_GI_SEARCH, ST_GI_SOLVE, ST_GI_UPD,
                  ST_SYNC_A, ST_TERMW, ST_SYNC_B, ST_RSX_PRE, ST_QEPI, ST_ROUND,
                  // graph kernel: event counts (not cycles) in the same buffer
-                 ST_N_GIZ = 40, ST_N_GIX, ST_N_ZQP, ST_N_ZFAIL, ST_N_XREBUILD, NSTAMP = 64 };
+                 ST_N_GIZ = 40, ST_N_GIX, ST_N_ZQP, ST_N_ZFAIL, ST_N_XREBUILD,
+                 // dual active set detail (pair QPs only): cycles of fwd / bwd / Y pass / drop, and counts
+                 ST_GI_FWD = 45, ST_GI_BWD, ST_GI_YPASS, ST_GI_DROP, ST_N_DROP, ST_N_APPEND, ST_N_WARMROW,
+                 ST_SUM_M, ST_SUM_MEND, ST_N_GICALL, NSTAMP = 64 };
 
 // ============================================================ wave primitives
 __device__ __forceinline__ int lid() { return (int)__lane_id(); }

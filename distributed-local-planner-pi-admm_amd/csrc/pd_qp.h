@@ -1062,57 +1062,99 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
 // form.  From the unconstrained minimiser x0 = -P^-1 q it adds the most violated one-sided
 // constraint n_p'x >= b_p at a time (box/rate row r: side 0 = a_r'x >= lo, side 1 =
 // -a_r'x >= -hi; hinge row: a_r'x >= h with multiplier cap beta), taking partial (dual)
-// steps that drop a constraint whose multiplier reaches 0.  The active set's Schur
-// complement S = N P^-1 N' is kept as a Cholesky factor L (LDS, insertion order): an add
-// appends one row (its forward-solve vector w and sqrt(S_pp - w'w)), a drop deletes row k and
-// restores the trailing block by a rank-one update.  Y holds the columns P^-1 n_a.  Each step
-// costs two m-step triangular solves, one m-column pass over Y and a few wave reductions --
-// no K_s^-1 and no ADMM.  On the recorded bench pair QPs (tools/gi_sim.py) it certifies every
-// one in 28 steps on average (max 51) where ADMM + PDAS took ~45 ADMM iterations and ~6
-// full reduced solves.  A hinge multiplier reaching the cap, a full factor or the step limit
-// return false and the caller falls back to ADMM + PDAS; the result is certified by the same
-// KKT test either way.
-// Triangular solves with lane = row, the factor's column (fwd) / row (bwd) entries of a batch
-// of TRI_U steps loaded before the batch's dependent chain: one LDS latency per batch
-// instead of one per step.
-constexpr int TRI_U = 8;
-__device__ __forceinline__ double tri_fwd(const double* L, int ld, double linv, double b, int m) {
-  const int l = lid();
-  const int lr = (l < m) ? l : 0;
-  for (int k0 = 0; k0 < m; k0 += TRI_U) {
-    double Lv[TRI_U];
-#pragma unroll
-    for (int u = 0; u < TRI_U; ++u) Lv[u] = L[lr * ld + min(k0 + u, 63)];
-#pragma unroll
-    for (int u = 0; u < TRI_U; ++u) {
-      const int k = k0 + u;
-      if (k < m) {
-        const double zk = rdl(b * linv, k);
-        if (l == k) b = zk;
-        if (l > k && l < m) b -= Lv[u] * zk;
-      }
-    }
-  }
-  return (l < m) ? b : 0.0;
+// steps that drop a constraint whose multiplier reaches 0.  The active set's Schur complement
+// S = N P^-1 N' is kept as its EXPLICIT INVERSE (LDS, lane = column, symmetric, any order of the
+// active constraints): an add borders it (r = S^-1 v, delta = s_pp - v'r: S^-1 += r r'/delta plus
+// one row and column), a drop downdates it (S^-1 - c c'/d over the other rows) and moves the last
+// active constraint into the freed slot.  Every piece is an m-term lane-parallel pass over LDS
+// (one broadcast operand per term, batched loads) -- no sequential triangular solve: on a
+// wave the m-step readlane chains of a Cholesky factor cost ~170 cycles per step (r03 stamps,
+// tools/graph_stamps.py), the parallel passes a few cycles per term.  Y holds the columns
+// P^-1 n_a.  The final answer is the equality-constrained minimiser on the final active set with
+// three steps of iterative refinement against the exact residual A_W x - b (x from Y, so S is
+// never needed explicitly); the KKT certificate judges it either way.  On the recorded bench
+// pair QPs (tools/gi_sim.py) the method certifies every one in 28 steps on average (max 51)
+// where ADMM + PDAS took ~45 ADMM iterations and ~6 full reduced solves.  A hinge multiplier
+// reaching the cap, a full set or the step limit return false and the caller falls back to
+// ADMM + PDAS; the result is certified by the same KKT test either way.
+
+// LDS-typed views: the QP struct's pointers are generic (LDS or HBM by mode), which makes the
+// compiler emit flat loads (TA path, vmcnt + lgkmcnt waits) for what is LDS -- the passes below
+// address the wave's scratch through address_space(3) pointers so they become ds_read / ds_write.
+typedef __attribute__((address_space(3))) double ldsd;
+__device__ __forceinline__ ldsd* lds_ptr(double* p) { return (ldsd*)p; }
+// generic pointer into LDS? (device pass only; the host pass never runs device code)
+__device__ __forceinline__ bool in_lds(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)p);
+#else
+  (void)p;
+  return false;
+#endif
 }
-__device__ __forceinline__ double tri_bwd(const double* L, int ld, double linv, double b, int m) {
+
+// The broadcast operand of an m-term pass: vbuf[a] = v (lanes a < m), 0 up to lane 63, so the
+// batched loads of a pass (never beyond lane 63: m <= 63, batches of 8 from multiples of 8) need
+// no bounds test and use immediate offsets.
+__device__ __forceinline__ void put_bcast(ldsd* vb, double v, int m) {
   const int l = lid();
-  const int lc = (l < m) ? l : 0;
-  for (int k0 = m - 1; k0 >= 0; k0 -= TRI_U) {
-    double Lv[TRI_U];
+  vb[l] = (l < m) ? v : 0.0;
+  wsync();
+}
+
+// r = S^-1 v over the m active constraints (v, r at lanes a < m): lane = column of the symmetric
+// inverse (LDS, stride ld), v broadcast from LDS (vbuf: 64 doubles of the wave's vector buffer).
+constexpr int SINV_U = 8;
+__device__ __forceinline__ double sinv_gemv(double* Si_, int ld, double* vbuf_, double v, int m) {
+  const int l = lid();
+  ldsd* vb = lds_ptr(vbuf_);
+  const ldsd* col = lds_ptr(Si_) + ((l < m) ? l : 0);
+  put_bcast(vb, v, m);
+  double a0 = 0.0, a1 = 0.0;
+  for (int j0 = 0; j0 < m; j0 += SINV_U) {
+    double sv[SINV_U], vv[SINV_U];
 #pragma unroll
-    for (int u = 0; u < TRI_U; ++u) Lv[u] = L[max(k0 - u, 0) * ld + lc];
+    for (int u = 0; u < SINV_U; ++u) {
+      sv[u] = col[min(j0 + u, m - 1) * ld];
+      vv[u] = vb[j0 + u];
+    }
 #pragma unroll
-    for (int u = 0; u < TRI_U; ++u) {
-      const int k = k0 - u;
-      if (k >= 0) {
-        const double xk = rdl(b * linv, k);
-        if (l == k) b = xk;
-        if (l < k) b -= Lv[u] * xk;
-      }
+    for (int u = 0; u < SINV_U; u += 2) {
+      a0 += sv[u] * vv[u];
+      a1 += sv[u + 1] * vv[u + 1];
     }
   }
-  return (l < m) ? b : 0.0;
+  wsync();
+  return (l < m) ? a0 + a1 : 0.0;
+}
+
+// z[v] -= sum_{a < m} coef_a Y[a][v] (lane = variable; coef at lanes a < m, broadcast from LDS).
+template <int NV, typename YP>
+__device__ __forceinline__ void y_axpy_t(YP Y, int H, ldsd* vb, int m, double* z) {
+  const int l = lid(), H2 = NV * H;
+  const int lc = (l < H) ? l : 0;
+  for (int a0 = 0; a0 < m; a0 += SINV_U) {
+    double yv[SINV_U][NV], cv[SINV_U];
+#pragma unroll
+    for (int u = 0; u < SINV_U; ++u) {
+      const int a = min(a0 + u, m - 1);
+      cv[u] = vb[a0 + u];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) yv[u][v] = Y[a * H2 + v * H + lc];
+    }
+#pragma unroll
+    for (int u = 0; u < SINV_U; ++u)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) z[v] -= cv[u] * yv[u][v];
+  }
+}
+template <int NV>
+__device__ __forceinline__ void y_axpy(double* Y, int H, double* vbuf_, double coef, int m, double* z) {
+  ldsd* vb = lds_ptr(vbuf_);
+  put_bcast(vb, coef, m);
+  if (in_lds(Y)) y_axpy_t<NV>((const ldsd*)lds_ptr(Y), H, vb, m, z);
+  else y_axpy_t<NV>((const double*)Y, H, vb, m, z);   // big mode: the columns in HBM / L2
+  wsync();
 }
 
 // P^-1 n for the one-sided constraint (row id, sign sg): lane = variable (one value per vehicle)
@@ -1153,16 +1195,19 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   constexpr int NR = QP<NV>::NR;
   const int l = lid(), H = P.H, ld = P.fld, H2 = NV * H;
   double* vb_ax = P.vb + 192;      // [192, 192 + NR*H): (A v) by row id
-  int* wc = P.ib;                  // active constraint codes 2*row + side, insertion order
-  double* L = P.fac;
+  double* vbuf = P.vb + 128;       // [128, 192): broadcast operand of the LDS passes
+  int* wc = P.ib;                  // active constraint codes 2*row + side
+  double* Si = P.fac;              // S^-1 (m x m, lane = column, stride ld; LDS in every mode)
+  ldsd* Sil = lds_ptr(Si);
+  ldsd* vbl = lds_ptr(vbuf);
   double* Y = P.Y;
   const int cap = min(P.mmax - 1, P.ycap);
   if (P.y_in_k) P.kready = false;  // Y overwrites the K_s^-1 region
-  if (l == 0) P.fstate[0] = -1;    // and L the cached PDAS factor
+  if (l == 0) P.fstate[0] = -1;    // and S^-1 the cached PDAS factor
   P.csig = -1;                     // (x-step: the factor scratch the parametric tables were built in)
   double x0[NV], xc[NV];
   int m = 0, wbits = 0;
-  double ua = 0.0, linv = 0.0;     // lane a < m: multiplier and 1/L_aa of active constraint a
+  double ua = 0.0;                 // lane a < m: multiplier of active constraint a
   // Pair: hinge rows in their linear regime (this lane's hinge row).  A hinge row's multiplier
   // is bounded, u in [0, beta] (dual of beta max(0, h - a'x)): when a step takes it to beta the
   // row turns linear -- its term beta (h - a'x) moves into q, i.e. x0 += beta P^-1 n, and the
@@ -1189,7 +1234,6 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     m = 0;
     wbits = 0;
     ua = 0.0;
-    linv = 0.0;
   };
 
   // y_p = P^-1 n_p (lane = variable), A y_p to vb_ax; returns n_p' P^-1 n_p
@@ -1206,20 +1250,35 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     wsync();
     return sgp * vb_ax[prow];
   };
-  // w = L^-1 (N y_p) for the current active set (lane a < m)
-  auto fwd = [&]() -> double {
+  // v = N y_p for the current active set (lane a < m)
+  auto nvec = [&]() -> double {
     const int myc = (l < m) ? wc[l] : 0;
-    const double va = (l < m) ? ((myc & 1) ? -1.0 : 1.0) * vb_ax[myc >> 1] : 0.0;   // n_a' y_p
-    return tri_fwd(L, ld, linv, va, m);
+    return (l < m) ? ((myc & 1) ? -1.0 : 1.0) * vb_ax[myc >> 1] : 0.0;   // n_a' y_p
   };
-  // append constraint pc: L row m = (w', sqrt(lpp2)), Y column m = y_p
-  auto append = [&](int pc, const double* yp, double w, double lpp2, double u0) {
+  // append constraint pc: border S^-1 with r = S^-1 v and delta = n_p'y_p - v'r; Y column m = y_p
+  auto append = [&](int pc, const double* yp, double r, double delta, double u0) {
     const int prow = pc >> 1, ps = prow / H, pk = prow - ps * H;
-    const double lmm = sqrt(lpp2);
-    if (l < m) L[m * ld + l] = w;
+    const double id = 1.0 / delta;
+    put_bcast(vbl, r, m);
+    if (l < m) {
+      const double rl = r * id;
+      ldsd* col = Sil + l;
+      for (int j0 = 0; j0 < m; j0 += SINV_U) {
+        double sv[SINV_U], rv[SINV_U];
+#pragma unroll
+        for (int u = 0; u < SINV_U; ++u) {
+          sv[u] = col[min(j0 + u, m - 1) * ld];
+          rv[u] = vbl[j0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < SINV_U; ++u)
+          if (j0 + u < m) col[(j0 + u) * ld] = sv[u] + rv[u] * rl;
+      }
+      Sil[m * ld + l] = -rl;      // row m, column l
+      Sil[l * ld + m] = -rl;      // row l, column m
+    }
     if (l == m) {
-      L[m * ld + m] = lmm;
-      linv = 1.0 / lmm;
+      Sil[m * ld + m] = id;
       ua = u0;
       wc[m] = pc;
     }
@@ -1232,47 +1291,62 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     if (P.gmem) gsync();
     else wsync();
   };
-  // drop active constraint k: delete row/column k of L, rank-one update of the trailing block
-  // with the deleted column, compact L, Y, codes and multipliers
+  // drop active constraint k: S^-1 of the others = S^-1 - c c'/d (c = column k, d = its diagonal),
+  // then the last active constraint moves into slot k (row, column, code, multiplier, Y column)
   auto drop = [&](int k) {
+    unsigned long long t_dr = STAMP_T();
+    if (NV == 2) STAMP_CNT(ST_N_DROP, 1);
     const int kc = rdli((l < m) ? wc[l] : 0, k);
     if (l == (kc >> 1) % H) wbits &= ~(1 << (2 * ((kc >> 1) / H) + (kc & 1)));
-    double xv = (l > k && l < m) ? L[l * ld + k] : 0.0;
-    for (int j = k + 1; j < m; ++j) {
-      const double Ljj = L[j * ld + j];
-      const double xj = rdl(xv, j);
-      const double rr = sqrt(Ljj * Ljj + xj * xj);
-      const double cc = rr / Ljj, sn = xj / Ljj;
-      if (l == j) L[j * ld + j] = rr;
-      if (l > j && l < m) {
-        const double Lij = (L[l * ld + j] + sn * xv) / cc;
-        xv = cc * xv - sn * Lij;
-        L[l * ld + j] = Lij;
+    const double c = (l < m) ? Sil[k * ld + l] : 0.0;
+    const double d = rdl(c, k);
+    put_bcast(vbl, c, m);
+    if (l < m && l != k) {
+      const double cl = c / d;
+      ldsd* col = Sil + l;
+      for (int j0 = 0; j0 < m; j0 += SINV_U) {
+        double sv[SINV_U], cv[SINV_U];
+#pragma unroll
+        for (int u = 0; u < SINV_U; ++u) {
+          sv[u] = col[min(j0 + u, m - 1) * ld];
+          cv[u] = vbl[j0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < SINV_U; ++u)
+          if (j0 + u < m) col[(j0 + u) * ld] = sv[u] - cv[u] * cl;
       }
     }
     wsync();
-    // compact: row i <- row i+1 (i >= k), column j <- column j+1 (j >= k); lane = column
-    for (int i = k; i < m - 1; ++i) {
-      const double v = (l < m - 1) ? L[(i + 1) * ld + l + (l >= k ? 1 : 0)] : 0.0;
+    const int last = m - 1;
+    if (k != last) {
+      // row last -> row k (lane b = column b < last; column k takes the diagonal of last)
+      if (l < last) {
+        const double v = Sil[last * ld + (l == k ? last : l)];
+        Sil[k * ld + l] = v;
+      }
       wsync();
-      if (l <= i) L[i * ld + l] = v;
-      wsync();
-    }
-    const int cnext = (l + 1 < m) ? wc[l + 1] : 0;
-    wsync();
-    if (l >= k && l < m - 1) wc[l] = cnext;
-    const double un = shdn(ua, 1);
-    if (l >= k) ua = (l < m - 1) ? un : 0.0;
-    for (int a = k; a < m - 1; ++a) {
+      // column last -> column k (lane a = row a < last, a != k)
+      if (l < last && l != k) {
+        const double v = Sil[l * ld + last];
+        Sil[l * ld + k] = v;
+      }
+      const int clast = wc[last];
+      const double ulast = rdl(ua, last);
       if (l < H) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) Y[a * H2 + v * H + l] = Y[(a + 1) * H2 + v * H + l];
+        for (int v = 0; v < NV; ++v) Y[k * H2 + v * H + l] = Y[last * H2 + v * H + l];
+      }
+      wsync();
+      if (l == k) {
+        wc[k] = clast;
+        ua = ulast;
       }
     }
+    if (l >= last) ua = 0.0;
     --m;
     if (P.gmem) gsync();
     else wsync();
-    linv = (l < m) ? 1.0 / L[l * ld + l] : 0.0;
+    if (NV == 2) STAMP_ADD(ST_GI_DROP, t_dr);
   };
   // multipliers of the equality-constrained minimiser on the active set (signed normals):
   // lam = S^-1 (N x0 - b); kernel multiplier of row a = sign_a * lam_a, GI multiplier -lam_a
@@ -1291,17 +1365,12 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       const double blo = P.hinge(rs) ? 0.0 : ((rs & 1) ? -P.dumax : -P.umax);   // hinge: hi = lo = h
       rhs = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
     }
-    return tri_bwd(L, ld, linv, tri_fwd(L, ld, linv, rhs, m), m);
+    return sinv_gemv(Si, ld, vbuf, rhs, m);
   };
   auto x_of = [&](double lam) {
-    const int lc = (l < H) ? l : 0;
 #pragma unroll
     for (int v = 0; v < NV; ++v) xc[v] = x0[v];
-    for (int a = 0; a < m; ++a) {
-      const double la = rdl(lam, a);
-#pragma unroll
-      for (int v = 0; v < NV; ++v) xc[v] -= la * Y[a * H2 + v * H + lc];
-    }
+    y_axpy<NV>(Y, H, vbuf, lam, m, xc);
   };
 
   // On failure (flab != nullptr): the current working set as PDAS labels -- a start for the
@@ -1322,9 +1391,11 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     if (m >= cap) return;
     double yp[NV];
     const double spp = prep(pc, yp);
-    const double w = fwd();
-    const double lpp2 = spp - wsum(w * w);
-    if (lpp2 > DEP_TOL * spp) append(pc, yp, w, lpp2, 0.0);
+    const double va = nvec();
+    const double r = sinv_gemv(Si, ld, vbuf, va, m);
+    const double delta = spp - wsum(va * r);
+    if (delta > DEP_TOL * spp) append(pc, yp, r, delta, 0.0);
+    if (NV == 2) STAMP_CNT(ST_N_WARMROW, 1);
   };
   start();
   bool warm = false;
@@ -1430,30 +1501,18 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
         return false;
       }
       unsigned long long t_gv = STAMP_T();
-      const double w = fwd();
-      const double r = tri_bwd(L, ld, linv, w, m);
+      if (NV == 2) STAMP_CNT(ST_SUM_M, m);
+      const double va = nvec();
+      const double r = sinv_gemv(Si, ld, vbuf, va, m);     // S^-1 N y_p
+      if (NV == 2) STAMP_ADD(ST_GI_FWD, t_gv);
+      unsigned long long t_yp = STAMP_T();
       // z = y_p - Y r
       double z[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) z[v] = yp[v];
-      {
-        const int lc = (l < H) ? l : 0;
-        for (int a0 = 0; a0 < m; a0 += GEMV_U) {
-          double yv[GEMV_U][NV], rv[GEMV_U];
-#pragma unroll
-          for (int u = 0; u < GEMV_U; ++u) {
-            const int a = min(a0 + u, m - 1);
-            rv[u] = (a0 + u < m) ? rdl(r, a) : 0.0;
-#pragma unroll
-            for (int v = 0; v < NV; ++v) yv[u][v] = Y[a * H2 + v * H + lc];
-          }
-#pragma unroll
-          for (int u = 0; u < GEMV_U; ++u)
-#pragma unroll
-            for (int v = 0; v < NV; ++v) z[v] -= rv[u] * yv[u][v];
-        }
-      }
-      const double lpp2 = spp - wsum(w * w);                   // n_p' z
+      y_axpy<NV>(Y, H, vbuf, r, m, z);
+      const double lpp2 = spp - wsum(va * r);                  // n_p' z
+      if (NV == 2) STAMP_ADD(ST_GI_YPASS, t_yp);
       STAMP_ADD(ST_GI_SOLVE, t_gv);
       unsigned long long t_gu = STAMP_T();
       const double t2 = (lpp2 > DEP_TOL * spp) ? -sp / lpp2 : INFINITY;
@@ -1514,7 +1573,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
           fail_labels();
           return false;
         }
-        append(pc, yp, w, lpp2, up);
+        append(pc, yp, r, lpp2, up);
+        if (NV == 2) STAMP_CNT(ST_N_APPEND, 1);
         STAMP_ADD(ST_GI_UPD, t_gu);
         break;
       }
@@ -1522,22 +1582,19 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       STAMP_ADD(ST_GI_UPD, t_gu);
     }
   }
-  // ---- exact solution of the final active set (the reduced solve with this factor):
-  // lam = S^-1 (N x0 - b), x = x0 - Y lam, then one step of primal refinement on the active
-  // rows' residual (see reduced_solve);  kernel multipliers y_a = sign_a * lam_a
+  // ---- exact solution of the final active set: lam = S^-1 (N x0 - b), x = x0 - Y lam, then three
+  // steps of iterative refinement on the active rows' exact residual A_W x - b (the inverse
+  // carries the rounding of its updates; the residual is formed from Y and A, not from S^-1);
+  // kernel multipliers y_a = sign_a * lam_a
   {
-    const double lam0 = eqp_lam(x0);
-    x_of(lam0);
-    const double dl = eqp_lam(xc);
-    {
-      const int lc = (l < H) ? l : 0;
-      for (int a = 0; a < m; ++a) {
-        const double da = rdl(dl, a);
-#pragma unroll
-        for (int v = 0; v < NV; ++v) xc[v] -= da * Y[a * H2 + v * H + lc];
-      }
+    double lam = eqp_lam(x0);
+    x_of(lam);
+#pragma unroll 1
+    for (int rf = 0; rf < 3; ++rf) {
+      const double dl = eqp_lam(xc);
+      y_axpy<NV>(Y, H, vbuf, dl, m, xc);
+      lam += dl;
     }
-    const double lam = lam0 + dl;
     const int myc = (l < m) ? wc[l] : 0;
     const int rw = myc >> 1;
     wsync();
@@ -1560,6 +1617,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       else lab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
       if (!P.valid(s)) lab[s] = 0;
     }
+    if (NV == 2) STAMP_CNT(ST_SUM_MEND, m);
+    if (NV == 2) STAMP_CNT(ST_N_GICALL, 1);
     // this step's active set: the next solve's warm start
     if (P.gws) {
       if (l < m) P.gws[2 + l] = myc;

@@ -19,7 +19,9 @@ NAMES = {0: "setup_x", 1: "setup_z", 2: "X phase", 3: "x qp", 6: "Z phase", 7: "
          23: "zr_chol", 24: "zr_x", 25: "zr_solve", 26: "xr_solve", 27: "zkkt", 28: "xkkt", 10: "red_gemv",
          11: "red_S", 12: "red_chol", 13: "red_x", 14: "admm", 32: "sync after X", 34: "sync after Z",
          35: "rsx_pre", 18: "sz_kmat", 19: "sz_gj", 20: "sz_pre", 17: "sz_ruiz"}
-COUNTS = {40: "gi steps z", 41: "gi steps x", 42: "z qps", 43: "z inexact", 44: "x setup rebuilds"}
+NAMES.update({45: "gi fwd (z)", 46: "gi bwd (z)", 47: "gi Ypass (z)", 48: "gi drop (z)"})
+COUNTS = {40: "gi steps z", 41: "gi steps x", 42: "z qps", 43: "z inexact", 44: "x setup rebuilds",
+          49: "z drops", 50: "z appends", 51: "z warm rows", 52: "z sum m/step", 53: "z sum m end", 54: "z gi ok"}
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 30
