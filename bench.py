@@ -122,6 +122,15 @@ def latest_profile(kind: str, workload: str):
     return None
 
 
+def make_scenario(wl: dict, n_steps: int, rank: int = 0):
+    """The workload's scenario on one rank (weak scaling: a seeded block per rank)."""
+    from piadmm import scenario
+    if wl.get("kind") == "crossing":
+        return scenario.concat([scenario.crossing(4, wl["H"], n_steps=n_steps, seed=1000 * rank + k)
+                                for k in range(wl["tiles"])])
+    return scenario.tiled(wl["tiles"], wl["H"], n_steps=n_steps, perturb=True, seed=1000 * rank)
+
+
 def cpu_baseline(wl: dict, budget_s: float, K: int) -> dict:
     """The CPU baselines on this host, timed BEFORE anything touches the GPU.
 
@@ -132,25 +141,28 @@ def cpu_baseline(wl: dict, budget_s: float, K: int) -> dict:
     NumPy oracle over a process pool (oracle/cpu_parallel.py), the stand-in for the reference's
     one-QP-at-a-time Python loop (B-ref, which cannot run here: CasADi / OSQP are absent)."""
     sys.path.insert(0, ROOT)
-    from piadmm import config, scenario
+    from piadmm import config
     n_tiles, H = wl["tiles"], wl["H"]
     cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=1, max_outer=wl["max_outer"], tighten=wl["tighten"],
                                         term_global=1)
+    crossing = wl.get("kind") == "crossing"
     bopt = pool = None
     try:
         from oracle import cpu_bopt
-        bopt = cpu_bopt.time_baseline(cfg, n_tiles, 0.6 * budget_s, n_steps=K)
-        scn = scenario.tiled(n_tiles, H, n_steps=K, perturb=True, seed=0)
+        scn = make_scenario(wl, K)
+        bopt = cpu_bopt.time_baseline(cfg, n_tiles, (0.6 if not crossing else 1.0) * budget_s, n_steps=K, scn=scn,
+                                      desc=f"{n_tiles} four-vehicle crossings" if crossing else None)
         r = cpu_bopt.run(cfg.replace(fixed_iters=0), scn, K, bopt["cores"])
         bopt["natural_ms_per_step"] = 1e3 * r["seconds"] / K
         bopt["natural_outer_iters_per_step"] = float(r["iters"][:, 0].mean())
     except Exception as e:          # noqa: BLE001 -- report the NumPy pool alone
         print(f"bench.py: B-opt CPU baseline failed ({e})", file=sys.stderr)
-    try:
-        from oracle import cpu_parallel
-        pool = cpu_parallel.time_baseline(cfg, n_tiles, 0.4 * budget_s)
-    except Exception as e:          # noqa: BLE001
-        print(f"bench.py: NumPy oracle pool failed ({e})", file=sys.stderr)
+    if not crossing:                # the NumPy pool parallelises over two-vehicle tiles
+        try:
+            from oracle import cpu_parallel
+            pool = cpu_parallel.time_baseline(cfg, n_tiles, 0.4 * budget_s)
+        except Exception as e:          # noqa: BLE001
+            print(f"bench.py: NumPy oracle pool failed ({e})", file=sys.stderr)
     if bopt is None:
         return pool
     if pool is not None:
@@ -175,10 +187,8 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
             scn = shard.scn
         else:
             scn = pdist.shard(full, rank, world)
-    elif wl.get("kind") == "crossing":
-        scn = scenario.concat([scenario.crossing(4, H, n_steps=n_steps, seed=1000 * rank + k) for k in range(wl["tiles"])])
     else:
-        scn = scenario.tiled(wl["tiles"], H, n_steps=n_steps, perturb=True, seed=1000 * rank)
+        scn = make_scenario(wl, n_steps, rank)
     from piadmm.solver import device_count
     solver = PI_ADMM_MI355X(cfg, scn, device=local_rank % max(device_count(), 1), shard=shard)
     try:
@@ -270,7 +280,7 @@ def main():
     # the CPU baseline first, on the host cores, before this process touches the GPU (its worker
     # pool is started with the spawn method)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and wl.get("kind") != "crossing":
+    if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(wl, args.cpu_budget, args.steps)
 
     from piadmm import _lib
@@ -311,7 +321,9 @@ def main():
         "scaling": wl["scaling"],
         "vs_baseline": None,
         "dtype": "f64",
-        "data": f"synthetic: seeded tiles of the reference 2-vehicle intersection ({agents_job} agents in the job)",
+        "data": (f"synthetic: seeded four-vehicle all-pairs crossings (lanes 0, 1 = the reference's 2-vehicle "
+                 f"intersection; {agents_job} agents in the job)" if wl.get("kind") == "crossing" else
+                 f"synthetic: seeded tiles of the reference 2-vehicle intersection ({agents_job} agents in the job)"),
         "config": {
             "workload": wl["desc"] + ", " + (
                 f"global natural termination (max {M} outer iterations)" if args.natural else

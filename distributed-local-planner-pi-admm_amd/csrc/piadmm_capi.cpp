@@ -58,6 +58,12 @@ struct piadmm_ctx {
   // outer iteration, and the host-decided stop state of the global scope
   bool step_open = false;
   int step_t = -1, step_it = 0, step_flag = 0, step_nanlast = 0, step_stop = 0;
+  // device-decided global termination (F_DEVSTOP): pinned copy of the stop state, iterations
+  // enqueued per chunk (the last step's count), PIADMM_HOST_DECIDE=1 keeps one host decision
+  // per outer iteration
+  int* h_ctl = nullptr;
+  int chunk_guess = 2;
+  bool host_decide = false;
 };
 
 namespace {
@@ -206,6 +212,11 @@ int32_t piadmm_create(const piadmm_config_t* cfg, piadmm_handle_t* out) {
   if (e == hipSuccess) e = hipEventCreate(&h->ev0);
   if (e == hipSuccess) e = hipEventCreate(&h->ev1);
   if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_part, (size_t)std::max(cfg->max_outer, 1) * 5 * sizeof(double));
+  if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_ctl, 4 * sizeof(int));
+  {
+    const char* hd = std::getenv("PIADMM_HOST_DECIDE");
+    h->host_decide = hd && hd[0] == '1';
+  }
   if (e != hipSuccess) {
     g_err = std::string("HIP init: ") + hipGetErrorString(e);
     delete h;
@@ -222,6 +233,7 @@ int32_t piadmm_destroy(piadmm_handle_t h) {
   free_all(h);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   if (h->h_part) (void)hipHostFree(h->h_part);
+  if (h->h_ctl) (void)hipHostFree(h->h_ctl);
   if (h->h_x) (void)hipHostFree(h->h_x);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -452,6 +464,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   rc |= dalloc(h, &A.gpart, (size_t)2 * C * 5);
   rc |= dalloc(h, &A.ghist, (size_t)h->step_cap * std::max(h->cfg.max_outer, 1) * 2);
   rc |= dalloc(h, &A.giters, (size_t)h->step_cap);
+  rc |= dalloc(h, &A.gctl, 4);
   int *d_gap = nullptr, *d_gal = nullptr, *d_gep = nullptr, *d_gel = nullptr, *d_gnp = nullptr, *d_gne = nullptr,
       *d_gnd = nullptr;
   if (A.graph) {
@@ -621,6 +634,60 @@ static int launch_step(const pd::DevArgs& a, int t, int n, int it0, int it1, int
 // collision test, pair QP and dual update; a cross-rank pair counts its residual on the rank
 // of its first agent only).  Natural termination adds the 5-double all-reduce of the
 // termination partials and the host decision of the unsharded host-decided path.
+// One MPC step under device-decided global termination (term_global with natural termination
+// across ranks -- RCCL or the host transport -- or PIADMM_NO_COOP on one rank).  Chunks of outer
+// iterations are enqueued ahead: per iteration the iteration launch (an X launch, the exchange
+// all-reduce and a Z launch for a sharded graph), the termination partials, their all-reduce and
+// k_decide, which applies the reference's stop rules (casadi/main.py:115-118,174-178) on the
+// device and sets the stop flag; launches after the stop return at once.  The host reads the stop
+// state once per chunk (chunk = the previous step's iteration count, doubled while the step runs
+// on), instead of one host round trip per outer iteration; the LAST launch takes the iteration
+// count and the NANLAST case from the device.
+static int32_t devstop_step(piadmm_handle_t h, int32_t tk, bool sync_outputs) {
+  const piadmm_config_t& c = h->cfg;
+  hipStream_t s = h->stream;
+  const int M = c.max_outer;
+  const size_t nx = h->xchg ? (size_t)h->n_slots * 3 * (c.H + 1) : 0;
+  HIPCHK(h, hipMemsetAsync(h->a.gctl, 0, 4 * sizeof(int), s));
+  if (!h->a.graph) LAUNCH(h, pd::launch_pair_deff(h->a, s));
+  int it = 0, K = std::max(1, std::min(h->chunk_guess, M));
+  while (true) {
+    const int n = std::min(K, M - it);
+    for (int j = 0; j < n; ++j, ++it) {
+      const int f = (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | pd::F_DEVSTOP;
+      if (h->xchg) {
+        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f | pd::F_XONLY, s));
+        if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
+        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, pd::F_GLOBAL | pd::F_DEVSTOP | pd::F_ZONLY, s));
+      } else {
+        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f, s));
+      }
+      double* part = h->d_part + (size_t)5 * it;
+      LAUNCH(h, h->a.graph ? pd::launch_graph_partials(h->a, part, s, 1) : pd::launch_term_partials(h->a, it, part, s, 1));
+      if (int rc = allreduce(h, part, part, 5)) return rc;
+      LAUNCH(h, pd::launch_decide(h->a, it, part, s));
+    }
+    HIPCHK(h, hipMemcpyAsync(h->h_ctl, h->a.gctl, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    if (h->h_ctl[0] || it >= M) break;
+    K *= 2;
+  }
+  const int nit = h->h_ctl[2], nanlast = h->h_ctl[1];
+  h->chunk_guess = std::max(1, nit);
+  h->giters = nit;
+  LAUNCH(h, launch_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | pd::F_DEVSTOP, s));
+  if (sync_outputs) {
+    const int nrec = nanlast ? nit - 1 : nit;
+    h->ghist.assign((size_t)2 * M, NAN);
+    if (nrec > 0) {
+      HIPCHK(h, hipMemcpyAsync(h->h_part, h->a.ghist, (size_t)2 * nrec * sizeof(double), hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      std::copy(h->h_part, h->h_part + 2 * nrec, h->ghist.begin());
+    }
+  }
+  return PIADMM_OK;
+}
+
 static int32_t run_steps_xchg(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outputs) {
   const piadmm_config_t& c = h->cfg;
   hipStream_t s = h->stream;
@@ -628,6 +695,10 @@ static int32_t run_steps_xchg(piadmm_handle_t h, int32_t t, int32_t n, bool sync
   const size_t nx = (size_t)h->n_slots * 3 * (c.H + 1);
   for (int k = 0; k < n; ++k) {
     const int tk = t + k;
+    if (!c.fixed_iters && !h->host_decide) {
+      if (int rc = devstop_step(h, tk, sync_outputs && k == n - 1)) return rc;
+      continue;
+    }
     h->ghist.assign((size_t)2 * M, NAN);
     int flag = 0, nit = 0, nanlast = 0;
     for (int it = 0; it < M; ++it) {
@@ -743,6 +814,10 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
   }
   for (int k = 0; k < n; ++k) {
     const int tk = t + k;
+    if (!h->host_decide) {
+      if (int rc = devstop_step(h, tk, sync_outputs && k == n - 1)) return rc;
+      continue;
+    }
     LAUNCH(h, pd::launch_pair_deff(h->a, s));
     h->ghist.assign((size_t)2 * M, NAN);
     int flag = 0, nit = 0, nanlast = 0;

@@ -720,6 +720,14 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t0, int n
   if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
   __syncthreads();
 #endif
+  if (flags & F_DEVSTOP) {      // device-decided global stop (uniform: every thread reads it)
+    if (!(flags & F_LAST)) {
+      if (A.gctl[0]) return;
+    } else {
+      it0 = it1 = A.gctl[2];
+      if (A.gctl[1]) flags |= F_NANLAST;
+    }
+  }
   int nbar = 0;   // grid barriers so far (coop): parity of the termination partials
   for (int k = 0; k < nsteps; ++k) {
     mpc_step_body<BIG>(A, t0 + k, it0, it1, flags, k, nbar);
@@ -735,7 +743,8 @@ __global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t0, int n
 // The summation order is the in-kernel (cooperative) stop test's: thread k accumulates
 // components k, k + NW*WAVE, ... in order, then the per-thread sums are added in thread order,
 // so the host-decided / RCCL path and the single-rank in-kernel path take identical decisions.
-__global__ void __launch_bounds__(NW * WAVE) k_term_partials(DevArgs A, int it, double* out) {
+__global__ void __launch_bounds__(NW * WAVE) k_term_partials(DevArgs A, int it, double* out, int devstop) {
+  if (devstop && A.gctl[0]) return;
   constexpr int NT = NW * WAVE;
   __shared__ double red[5][NT];
   double v[5] = {0, 0, 0, 0, 0};
@@ -847,9 +856,37 @@ bool coop_fits(const DevArgs& a, int device) {
   return (long long)per * ncu >= (long long)a.C;
 }
 
-int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s) {
+int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s, int devstop) {
   (void)hipGetLastError();
-  hipLaunchKernelGGL(k_term_partials, dim3(1), dim3(NW * WAVE), 0, s, a, it, out);
+  hipLaunchKernelGGL(k_term_partials, dim3(1), dim3(NW * WAVE), 0, s, a, it, out, devstop);
+  return launch_rc(hipGetLastError());
+}
+
+// The reference's stop rules over the job (casadi/main.py:115-118,174-178; MATLAB :191-210) on
+// the all-reduced partials of outer iteration `it`, decided on the device (F_DEVSTOP): the same
+// rules as the host decision in piadmm_capi.cpp global_iteration.  gctl: [0] stop, [1] the stop
+// came at the collision test (NANLAST), [2] iterations executed, [3] some pair ever collided.
+__global__ void k_decide(DevArgs A, int it, const double* part) {
+  int* g = A.gctl;
+  if (g[0]) return;
+  const piadmm_config_t& c = A.cfg;
+  const double rk = part[0], sk = part[1], n_act = part[2], n_seen = part[3], n_bad = part[4];
+  g[2] = it + 1;
+  if (n_act == 0.0 && g[3] == 0 && !c.fixed_iters) {
+    g[1] = 1;
+    g[0] = 1;
+    return;
+  }
+  g[3] = 1;
+  A.ghist[2 * it + 0] = rk;
+  A.ghist[2 * it + 1] = sk;
+  if (!c.fixed_iters && rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || (n_seen > 0.0 && n_bad == 0.0)))
+    g[0] = 1;
+}
+
+int launch_decide(const DevArgs& a, int it, const double* part, hipStream_t s) {
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(k_decide, dim3(1), dim3(1), 0, s, a, it, part);
   return launch_rc(hipGetLastError());
 }
 

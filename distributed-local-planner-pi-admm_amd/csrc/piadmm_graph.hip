@@ -751,6 +751,14 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
 
 template <bool BIG>
 __global__ void __launch_bounds__(GW * WAVE) k_graph_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
+  if (flags & F_DEVSTOP) {      // device-decided global stop (uniform: every thread reads it)
+    if (!(flags & F_LAST)) {
+      if (A.gctl[0]) return;
+    } else {
+      it0 = it1 = A.gctl[2];
+      if (A.gctl[1]) flags |= F_NANLAST;
+    }
+  }
 #ifdef PIADMM_STAMPS
   if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
   __syncthreads();
@@ -772,7 +780,8 @@ namespace pd {
 // Termination partials of the last iteration summed over components (host-decided global
 // termination in graph mode): the in-kernel (cooperative) order -- thread k accumulates
 // components k, k + GW*WAVE, ... in order, then the per-thread sums in thread order.
-__global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double* out) {
+__global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double* out, int devstop) {
+  if (devstop && A.gctl[0]) return;
   constexpr int NT = GW * WAVE;
   __shared__ double red[5][NT];
   double v[5] = {0, 0, 0, 0, 0};
@@ -825,9 +834,9 @@ bool graph_coop_fits(const DevArgs& a, int device) {
   return (long long)per * ncu >= (long long)a.C;
 }
 
-int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s) {
+int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s, int devstop) {
   (void)hipGetLastError();
-  hipLaunchKernelGGL(k_graph_partials, dim3(1), dim3(GW * WAVE), 0, s, a, out);
+  hipLaunchKernelGGL(k_graph_partials, dim3(1), dim3(GW * WAVE), 0, s, a, out, devstop);
   return launch_rc(hipGetLastError());
 }
 

@@ -88,6 +88,7 @@ struct DevArgs {
   double* gpart;            // 2*C*5 coop: per-component termination partials (iteration parity)
   double* ghist;            // step_cap*max_outer*2 coop: global (rk, sk) history per step
   int* giters;              // step_cap coop: global outer iterations per step
+  int* gctl;                // 4: device-decided global stop (F_DEVSTOP): stop, nanlast, iterations, flag
   // ---- graph mode (k_graph_step): any static candidate graph (components of any size, agents
   // in several pairs).  All per-QP state lives in HBM between the phases of an outer iteration.
   int graph;                // 1: the scenario runs on k_graph_step
@@ -183,6 +184,11 @@ inline size_t graph_lds_bytes(int H) {
 // its x-step or its z-step + termination half (the exchange of a sharded job sits between).
 constexpr int F_XONLY = 32;
 constexpr int F_ZONLY = 64;
+// Device-decided global termination (term_global across ranks, RCCL or host transport): iteration
+// launches return at once when A.gctl[0] (stop) is set -- a chunk of iterations is enqueued ahead
+// with the all-reduce and k_decide between them, and the host reads the stop state once per
+// chunk; the LAST launch takes its iteration count and NANLAST from A.gctl.
+constexpr int F_DEVSTOP = 128;
 
 int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 // candidate-pair detection (piadmm_detect.hip)
@@ -193,9 +199,10 @@ constexpr int DETECT_SCAN_B = 1024;   // ints per workgroup of the detection's s
 int launch_detect_emit(const double* xs, const double* rs, int n, double inv_cs, unsigned T, const int* start,
                        const int* order, const int* off, int* out, hipStream_t s);
 bool graph_coop_fits(const DevArgs& a, int device);
-int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s);
+int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s, int devstop = 0);
+int launch_decide(const DevArgs& a, int it, const double* part, hipStream_t s);
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
-int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s);
+int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s, int devstop = 0);
 int launch_resid_history(const DevArgs& a, int nsteps, double* out, hipStream_t s);
 int launch_pair_deff(const DevArgs& a, hipStream_t s);
 bool coop_fits(const DevArgs& a, int device);

@@ -1,9 +1,10 @@
 """ctypes front end of the B-opt CPU baseline (oracle/piadmm_cpu.cpp -> oracle/libpiadmm_cpu.so).
 
 MEASUREMENT / TEST INFRASTRUCTURE ONLY: bench.py's ``cpu_baseline`` leg and tests/ use it.  It
-runs the tiled workload (components of two agents, candidate pair (2k, 2k+1)) through the
-oracle's loop (oracle/piadmm_oracle.py, casadi/main.py:43-201) in C++ with OpenMP over tiles and
-returns the same per-step records, so tests/test_cpu_bopt.py can hold it to the NumPy oracle.
+runs any scenario (the tiled intersection, the all-pairs crossings, any static candidate graph)
+through the oracle's loop (oracle/piadmm_oracle.py, casadi/main.py:43-201) in C++ with OpenMP over
+connected components and returns the same per-step records, so tests/test_cpu_bopt.py can hold it
+to the NumPy oracle.
 """
 from __future__ import annotations
 
@@ -17,7 +18,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libpiadmm_cpu.so")
 
 _INT_FIELDS = ("H", "max_outer", "dual_mode", "windup", "round_decimals", "collide_sq_thres",
-               "alias_dual_residual", "pos_model", "term_dist_check", "fixed_iters", "term_global", "tighten")
+               "alias_dual_residual", "pos_model", "term_dist_check", "fixed_iters", "term_global", "tighten",
+               "warm_duals", "no_collision_gate")
 _DBL_FIELDS = ("dt", "L", "dis_thres", "beta", "Pnorm", "Pcost", "rho", "eps_pri", "eps_dual", "u_max",
                "du_max", "kI", "theta1", "theta2", "windup_sat", "tight_p", "avg_delay", "var_delay", "qp_tol")
 
@@ -41,9 +43,9 @@ def load():
         lib = ctypes.CDLL(LIB)
         lib.piadmm_cpu_cfg_size.restype = ctypes.c_int
         P = ctypes.c_void_p
-        lib.piadmm_cpu_run.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int,
-                                       ctypes.c_int, ctypes.c_int, P, P, P, P, P, P]
-        lib.piadmm_cpu_run.restype = ctypes.c_int
+        lib.piadmm_cpu_run_graph.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int,
+                                             P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P, P]
+        lib.piadmm_cpu_run_graph.restype = ctypes.c_int
         if lib.piadmm_cpu_cfg_size() != ctypes.sizeof(_Cfg):
             raise RuntimeError("libpiadmm_cpu.so config layout differs from oracle/cpu_bopt.py")
         _lib = lib
@@ -51,8 +53,8 @@ def load():
 
 
 def _cfg(cfg) -> _Cfg:
-    if cfg.dual_mode not in (0, 1) or cfg.warm_duals or cfg.no_collision_gate:
-        raise ValueError("the B-opt baseline covers dual modes 0/1 without warm_duals / no_collision_gate")
+    if cfg.dual_mode not in (0, 1):
+        raise ValueError("the B-opt baseline covers dual modes 0/1 (not the global-PI law)")
     c = _Cfg()
     for f in _INT_FIELDS:
         setattr(c, f, int(getattr(cfg, f)))
@@ -68,29 +70,30 @@ def is_tiled(scn) -> bool:
 
 
 def run(cfg, scn, n_steps: int, threads: int = 1, t0: int = 0, records: bool = True):
-    """n_steps MPC steps of a tiled scenario.  Returns dict(seconds, xt (S,N,3), u (S,N,H),
-    iters (S,T), resid (S,T,max_outer,2) NaN-padded, counters)."""
-    if not is_tiled(scn):
-        raise ValueError("the B-opt baseline runs tiled scenarios (pairs (2k, 2k+1))")
+    """n_steps MPC steps of any scenario (candidate graph scn.edges).  Returns dict(seconds, xt
+    (S,N,3), u (S,N,H), iters (S,C), resid (S,C,max_outer,2) NaN-padded, counters); C = connected
+    components in order of their first agent (the oracle's Scenario.components())."""
     lib = load()
     c = _cfg(cfg)
     N, H, MO = scn.n_agents, cfg.H, cfg.max_outer
-    T = N // 2
+    C = int(scn.components()[1])
     spd = np.ascontiguousarray(scn.spd, np.float64)
     xt0 = np.ascontiguousarray(scn.xt0, np.float64)
     ref = np.ascontiguousarray(scn.ref, np.float64)
+    edges = np.ascontiguousarray(scn.edges, np.int32).reshape(-1)
     xt = np.zeros((n_steps, N, 3)) if records else None
     u = np.zeros((n_steps, N, H)) if records else None
-    iters = np.zeros((n_steps, T), np.int32) if records else None
-    resid = np.zeros((n_steps, T, MO, 2)) if records else None
+    iters = np.zeros((n_steps, C), np.int32) if records else None
+    resid = np.zeros((n_steps, C, MO, 2)) if records else None
     secs = ctypes.c_double(0.0)
     cnt = np.zeros(5, np.int64)
     ptr = (lambda a: a.ctypes.data if a is not None else None)
-    rc = lib.piadmm_cpu_run(ctypes.byref(c), T, spd.ctypes.data, xt0.ctypes.data, ref.ctypes.data, ref.shape[2],
-                            t0, n_steps, threads, ptr(xt), ptr(u), ptr(iters), ptr(resid), ctypes.byref(secs),
-                            cnt.ctypes.data)
-    if rc != 0:
-        raise RuntimeError(f"piadmm_cpu_run failed ({rc})")
+    rc = lib.piadmm_cpu_run_graph(ctypes.byref(c), N, spd.ctypes.data, xt0.ctypes.data, ref.ctypes.data,
+                                  ref.shape[2], scn.n_edges, edges.ctypes.data if edges.size else None, t0, n_steps,
+                                  threads, ptr(xt), ptr(u), ptr(iters), ptr(resid), ctypes.byref(secs),
+                                  cnt.ctypes.data)
+    if rc != C:
+        raise RuntimeError(f"piadmm_cpu_run_graph failed ({rc})")
     return {"seconds": secs.value, "xt": xt, "u": u, "iters": iters, "resid": resid,
             "counters": dict(zip(("x_qps", "z_qps", "x_hits", "gi_steps", "inexact"), cnt.tolist()))}
 

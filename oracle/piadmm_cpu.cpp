@@ -1,15 +1,16 @@
-// B-opt CPU baseline of the PI-ADMM hot path -- C++, OpenMP over components (tiles).
+// B-opt CPU baseline of the PI-ADMM hot path -- C++, OpenMP over connected components.
 //
 // MEASUREMENT / TEST INFRASTRUCTURE ONLY: bench.py's cpu_baseline leg and tests/ load it (through
 // oracle/cpu_bopt.py); the product path (libpiadmm.so, include/piadmm.h) never does.
 //
 // What it computes: the loop of oracle/piadmm_oracle.py (the NumPy restatement of
 // casadi/main.py:43-201 with the MATLAB PI anti-windup law, ADMM_CVX_..._PI_antiwindup.m:152-188)
-// for the benchmark's workload shape -- components of two agents joined by one candidate pair
-// (the tiled intersection, piadmm/scenario.py) -- with the same semantics flags (dual mode plain /
-// PI, windup, rounding, B2 threshold, B4 aliasing, B15 position model, MATLAB distance stop,
-// fixed iterations, delay tightening, per-component or global termination).  Every QP answer is
-// the exact minimiser, so the results equal the oracle's (tests/test_cpu_bopt.py, 1e-8).
+// on any static candidate graph -- the tiled intersection of the benchmark (components of two
+// agents), the 4-vehicle all-pairs crossings, chains -- with the same semantics flags (dual mode
+// plain / PI, windup, rounding, B2 threshold, B4 aliasing, B15 position model, MATLAB distance
+// stop, fixed iterations, delay tightening, warm duals (a12), no collision gate, per-component or
+// global termination).  Every QP answer is the exact minimiser, so the results equal the
+// oracle's (tests/test_cpu_bopt.py, 1e-8).  Not covered: the global-PI law (dual mode 2).
 //
 // How (SURVEY.md 8d "B-opt": same algorithm as the GPU kernel, -O3, OpenMP, all cores given):
 //   * x-step QP (casadi/PI_ADMM_class.py:114-135,172-192): P depends on the speed only, so each
@@ -42,7 +43,7 @@ namespace {
 
 struct CpuCfg {          // mirror: oracle/cpu_bopt.py _Cfg
   int H, max_outer, dual_mode, windup, round_decimals, collide_sq_thres, alias_dual_residual,
-      pos_model, term_dist_check, fixed_iters, term_global, tighten;
+      pos_model, term_dist_check, fixed_iters, term_global, tighten, warm_duals, no_collision_gate;
   double dt, L, dis_thres, beta, Pnorm, Pcost, rho, eps_pri, eps_dual, u_max, du_max, kI,
       theta1, theta2, windup_sat, tight_p, avg_delay, var_delay, qp_tol;
 };
@@ -502,31 +503,45 @@ bool gi_solve(const QPDef& Q, ActiveSet& A, const int* warm, int nwarm, char* li
   return true;
 }
 
-// ---------------------------------------------------------------- one component (tile)
+// ---------------------------------------------------------------- agents, pairs, components
+// Any static candidate graph (the reference's num_veh loop, casadi/main.py:81,110-162): an agent's
+// x-step sums the consensus term over its candidate neighbours in neighbour order
+// (PI_ADMM_class.py:126-129; oracle xstep_qp), every candidate pair is collision-tested and, when
+// it collides, gets its pair QP, hat rollouts and dual update in pair order; a connected component
+// is one termination group (or the whole job under term_global) -- the oracle's Oracle.mpc_step.
 struct Agent {
   double spd;
-  std::vector<double> Pinv;       // H x H (speed only: fixed for the run)
+  double xt[3], seeds[2];
+  std::vector<double> Pinv;       // H x H (speed and neighbour count only: fixed for the run)
   ActiveSet ws;                   // cached working set + factor (valid: P and rows are fixed)
   bool factor_ok = false;
   std::vector<double> u, px, py;  // primal_u, pos_old
+  std::vector<std::pair<int, int>> nbr;   // (pair, direction), sorted by neighbour id
 };
 
-struct Tile {
-  Agent ag[2];
-  double xt[2][3];
+struct Pair {
+  int v[2];
   std::vector<double> hat, lam, S, D, last;     // [d][2][H+1]
-  double seeds[2][2];
   double d_eff;
-  // pair QP
   std::vector<double> Ppinv;      // 2H x 2H block diagonal P^-1
   std::vector<int> pws;           // pair's last active set (codes)
   int pws_t = -1000;
-  // step state
-  bool active, seen, flag, alias, done;
-  double dis_chk;
+  bool active, seen;
+  double dis_chk, rk, sk;
+};
+
+struct Comp {
+  std::vector<int> agents, pairs;
+  bool flag, alias, done;
   int iters;
-  double rk, sk;
+  double part[5];
   std::vector<double> resid;      // per iteration (rk, sk) of this step
+};
+
+struct World {
+  std::vector<Agent> ag;
+  std::vector<Pair> pr;
+  std::vector<Comp> comps;
 };
 
 struct Run {
@@ -594,11 +609,11 @@ struct Ctx {
   int t;                 // MPC step (reference slice t .. t+H)
 };
 
-// x-step of agent v of tile (casadi/main.py:81-106)
-void x_step(Ctx& X, Tile& tl, int v, int tag, Work& W) {
+// x-step of agent a (casadi/main.py:81-106; oracle xstep_qp / solve_xstep)
+void x_step(Ctx& X, World& Wd, int a, Work& W) {
   const CpuCfg& c = X.c;
   const int H = c.H, R = H + 1;
-  Agent& A = tl.ag[v];
+  Agent& A = Wd.ag[a];
   W.ensure(2 * H);
   // constant part c of the linearised rollout (rollout_affine) and q = M'v through the rollout
   // matrix's structure M_a(t, j) = k_a tm (t-1-j)_+ (two reverse running sums, as the kernel's
@@ -609,7 +624,7 @@ void x_step(Ctx& X, Tile& tl, int v, int tag, Work& W) {
   double* vv = cc + 2 * R;            // 2R
   double* q = vv + 2 * R;             // H
   double* x = q + H;                  // H
-  const double* xt = tl.xt[v];
+  const double* xt = A.xt;
   const double s = A.spd, s0 = std::sin(xt[2]), c0 = std::cos(xt[2]);
   const double kx = -s * s0 * c.dt, ky = s * c0 * c.dt, tm = s / c.L * c.dt;
   cc[0] = xt[0];
@@ -618,17 +633,18 @@ void x_step(Ctx& X, Tile& tl, int v, int tag, Work& W) {
     cc[k + 1] = cc[k] + (-s * s0 * xt[2] + (s * c0 + s * xt[2] * s0)) * c.dt;
     cc[R + k + 1] = cc[R + k] + (s * c0 * xt[2] + (s * s0 - s * xt[2] * c0)) * c.dt;
   }
-  const double* ref = X.ref + (size_t)tag * 2 * X.T;
-  const int d = v;                       // agent v0 owns direction 0 (hat_{v1 v2}), v1 direction 1
-  const double* hat = &tl.hat[(size_t)d * 2 * R];
-  const double* lam = &tl.lam[(size_t)d * 2 * R];
-  for (int a = 0; a < 2; ++a)
+  const double* ref = X.ref + (size_t)a * 2 * X.T;
+  for (int ax = 0; ax < 2; ++ax)
     for (int k = 0; k < R; ++k) {
-      const int i = a * R + k;
-      double val = 2.0 * c.Pnorm * (cc[i] - ref[(size_t)a * X.T + X.t + k]);
-      val = val + c.rho * (cc[i] - hat[i] + lam[i]);
-      vv[i] = val;
+      const int i = ax * R + k;
+      vv[i] = 2.0 * c.Pnorm * (cc[i] - ref[(size_t)ax * X.T + X.t + k]);
     }
+  for (const auto& nd : A.nbr) {         // neighbour order (oracle: v = v + rho (c - hat + lam))
+    const Pair& p = Wd.pr[nd.first];
+    const double* hat = &p.hat[(size_t)nd.second * 2 * R];
+    const double* lam = &p.lam[(size_t)nd.second * 2 * R];
+    for (int i = 0; i < 2 * R; ++i) vv[i] = vv[i] + c.rho * (cc[i] - hat[i] + lam[i]);
+  }
   {
     double ax = 0.0, ay = 0.0, bx = 0.0, by = 0.0;   // sums over t >= j + 2
     for (int j = H - 1; j >= 0; --j) {
@@ -655,10 +671,10 @@ void x_step(Ctx& X, Tile& tl, int v, int tag, Work& W) {
   char lin_none[1] = {0};
   if (A.factor_ok) {                     // the cached working set (the GPU's parametric hit)
     for (int i = 0; i < H; ++i) {
-      double s = 0.0;
+      double sm = 0.0;
       const double* pr = &A.Pinv[(size_t)i * H];
-      for (int j = 0; j < H; ++j) s += pr[j] * q[j];
-      W.x0[i] = -s;
+      for (int j = 0; j < H; ++j) sm += pr[j] * q[j];
+      W.x0[i] = -sm;
     }
     final_x(Q, A.ws, W, x);
     ok = certify(Q, A.ws, x, lin_none);
@@ -674,25 +690,27 @@ void x_step(Ctx& X, Tile& tl, int v, int tag, Work& W) {
     if (!ok) ++X.run.inexact;
   }
   for (int k = 0; k < H; ++k) A.u[k] = around(x[k], c.round_decimals);
-  if (c.pos_model == 0) rollout_linear(tl.xt[v], A.u.data(), A.spd, c.dt, c.L, H, A.px.data(), A.py.data());
-  else rollout_nonlinear(tl.xt[v], A.u.data(), A.spd, c.dt, c.L, H, A.px.data(), A.py.data());
+  if (c.pos_model == 0) rollout_linear(A.xt, A.u.data(), A.spd, c.dt, c.L, H, A.px.data(), A.py.data());
+  else rollout_nonlinear(A.xt, A.u.data(), A.spd, c.dt, c.L, H, A.px.data(), A.py.data());
 }
 
 // pair z-step + hat rollouts (casadi/main.py:121-158, edge_qp / hinge_rows of the oracle)
-void z_step(Ctx& X, Tile& tl, int t, Work& W) {
+void z_step(Ctx& X, World& Wd, int e, int t, Work& W) {
   const CpuCfg& c = X.c;
   const int H = c.H, R = H + 1, n = 2 * H;
+  Pair& P = Wd.pr[e];
+  const Agent* ag[2] = {&Wd.ag[P.v[0]], &Wd.ag[P.v[1]]};
   W.ensure(n);
   std::vector<double> cv[2], Mv[2];
   for (int v = 0; v < 2; ++v) {
     cv[v].resize(2 * R);
     Mv[v].resize(2 * R * H);
-    rollout_affine(tl.xt[v], tl.ag[v].spd, c.dt, c.L, H, cv[v].data(), Mv[v].data());
+    rollout_affine(ag[v]->xt, ag[v]->spd, c.dt, c.L, H, cv[v].data(), Mv[v].data());
   }
   std::vector<double> q(n, 0.0), G((size_t)H * n, 0.0), h(H);
   for (int v = 0; v < 2; ++v) {
-    const double* p[2] = {tl.ag[v].px.data(), tl.ag[v].py.data()};
-    const double* lam = &tl.lam[(size_t)v * 2 * R];
+    const double* p[2] = {ag[v]->px.data(), ag[v]->py.data()};
+    const double* lam = &P.lam[(size_t)v * 2 * R];
     for (int j = 0; j < H; ++j) {
       double s = 0.0;
       for (int a = 0; a < 2; ++a)
@@ -704,9 +722,9 @@ void z_step(Ctx& X, Tile& tl, int t, Work& W) {
       q[v * H + j] = -c.rho * s;
     }
   }
-  const double db0 = tl.seeds[1][0] - tl.seeds[0][0], db1 = tl.seeds[1][1] - tl.seeds[0][1];
+  const double db0 = ag[1]->seeds[0] - ag[0]->seeds[0], db1 = ag[1]->seeds[1] - ag[0]->seeds[1];
   const double dd = db0 * db0 + db1 * db1;
-  const double D2 = tl.d_eff * tl.d_eff;
+  const double D2 = P.d_eff * P.d_eff;
   for (int k = 1; k <= H; ++k) {
     h[k - 1] = D2 + dd - 2.0 * (db0 * (cv[1][k] - cv[0][k]) + db1 * (cv[1][R + k] - cv[0][R + k]));
     for (int j = 0; j < H; ++j) {
@@ -718,7 +736,7 @@ void z_step(Ctx& X, Tile& tl, int t, Work& W) {
   Q.n = n;
   Q.H = H;
   Q.NV = 2;
-  Q.Pinv = tl.Ppinv.data();
+  Q.Pinv = P.Ppinv.data();
   Q.q = q.data();
   Q.G = G.data();
   Q.h = h.data();
@@ -728,11 +746,11 @@ void z_step(Ctx& X, Tile& tl, int t, Work& W) {
   Q.tol = c.qp_tol;
   // warm start: this step's last active set, or the previous step's shifted one slot
   std::vector<int> warm;
-  if (tl.pws_t == t) {
-    warm = tl.pws;
-  } else if (tl.pws_t == t - 1) {
+  if (P.pws_t == t) {
+    warm = P.pws;
+  } else if (P.pws_t == t - 1) {
     const int nb = 2 * H - 1;
-    for (int code : tl.pws) {
+    for (int code : P.pws) {
       const int row = code >> 1;
       int k, base;
       if (row >= 2 * nb) { k = row - 2 * nb; base = 2 * nb; }
@@ -752,13 +770,13 @@ void z_step(Ctx& X, Tile& tl, int t, Work& W) {
   if (!ok) DBG("pair gi fail t=%d\n", t);
   if (ok) { ok = certify(Q, As, x.data(), lin.data()); if (!ok) DBG("pair cert fail t=%d m=%d\n", t, As.m); }
   if (!ok) ++X.run.inexact;
-  tl.pws.assign(As.codes.begin(), As.codes.begin() + As.m);
-  tl.pws_t = t;
+  P.pws.assign(As.codes.begin(), As.codes.begin() + As.m);
+  P.pws_t = t;
   std::vector<double> uh(H), hx(R), hy(R);
   for (int d = 0; d < 2; ++d) {
     for (int k = 0; k < H; ++k) uh[k] = around(x[d * H + k], c.round_decimals);
-    rollout_nonlinear(tl.xt[d], uh.data(), tl.ag[d].spd, c.dt, c.L, H, hx.data(), hy.data());
-    double* ht = &tl.hat[(size_t)d * 2 * R];
+    rollout_nonlinear(ag[d]->xt, uh.data(), ag[d]->spd, c.dt, c.L, H, hx.data(), hy.data());
+    double* ht = &P.hat[(size_t)d * 2 * R];
     for (int k = 0; k < R; ++k) {
       ht[k] = hx[k];
       ht[R + k] = hy[k];
@@ -766,10 +784,11 @@ void z_step(Ctx& X, Tile& tl, int t, Work& W) {
   }
 }
 
-// dual update of the pair (oracle dual_update): plain casadi/main.py:161-162, PI :156-188
-void dual_update(const CpuCfg& c, Tile& tl, const double* dist) {
+// dual update of a pair (oracle dual_update): plain casadi/main.py:161-162, PI :156-188
+void dual_update(const CpuCfg& c, World& Wd, Pair& P, const double* dist) {
   const int R = c.H + 1;
-  const double* ps[2][2] = {{tl.ag[0].px.data(), tl.ag[0].py.data()}, {tl.ag[1].px.data(), tl.ag[1].py.data()}};
+  const Agent &a0 = Wd.ag[P.v[0]], &a1 = Wd.ag[P.v[1]];
+  const double* ps[2][2] = {{a0.px.data(), a0.py.data()}, {a1.px.data(), a1.py.data()}};
   double kP = 0.0;
   if (c.dual_mode != 0) {
     double dmin = dist[0];
@@ -777,10 +796,10 @@ void dual_update(const CpuCfg& c, Tile& tl, const double* dist) {
     kP = c.theta1 - c.theta2 / (1 + std::exp(-dmin));
   }
   for (int d = 0; d < 2; ++d) {
-    double* lam = &tl.lam[(size_t)d * 2 * R];
-    double* S = &tl.S[(size_t)d * 2 * R];
-    double* D = &tl.D[(size_t)d * 2 * R];
-    const double* hat = &tl.hat[(size_t)d * 2 * R];
+    double* lam = &P.lam[(size_t)d * 2 * R];
+    double* S = &P.S[(size_t)d * 2 * R];
+    double* D = &P.D[(size_t)d * 2 * R];
+    const double* hat = &P.hat[(size_t)d * 2 * R];
     for (int a = 0; a < 2; ++a)
       for (int k = 0; k < R; ++k) {
         const int i = a * R + k;
@@ -806,66 +825,99 @@ void dual_update(const CpuCfg& c, Tile& tl, const double* dist) {
   }
 }
 
-void begin_step(Ctx& X, Tile& tl) {
-  const CpuCfg& c = X.c;
+// seeds (casadi/main.py:48-49), the per-step reset of the pair state (:52-63; with warm_duals the
+// previous step's shifted one slot, optimizer.py:337-344 / oracle shift_horizon), safety distance
+void begin_step(const CpuCfg& c, World& Wd, Comp& C, bool first_step) {
   const int R = c.H + 1;
-  for (int v = 0; v < 2; ++v) {
-    tl.seeds[v][0] = around(tl.xt[v][0] + c.dt * tl.ag[v].spd * std::cos(tl.xt[v][2]), c.round_decimals);
-    tl.seeds[v][1] = around(tl.xt[v][1] + c.dt * tl.ag[v].spd * std::sin(tl.xt[v][2]), c.round_decimals);
+  for (int a : C.agents) {
+    Agent& A = Wd.ag[a];
+    A.seeds[0] = around(A.xt[0] + c.dt * A.spd * std::cos(A.xt[2]), c.round_decimals);
+    A.seeds[1] = around(A.xt[1] + c.dt * A.spd * std::sin(A.xt[2]), c.round_decimals);
   }
-  for (auto* a : {&tl.hat, &tl.lam, &tl.S, &tl.D, &tl.last}) a->assign((size_t)2 * 2 * R, 0.0);
-  tl.d_eff = c.tighten ? c.dis_thres + delay_norm(c, tl.xt[0], tl.ag[0].spd) + delay_norm(c, tl.xt[1], tl.ag[1].spd)
-                       : c.dis_thres;
-  tl.active = tl.seen = tl.flag = tl.alias = tl.done = false;
-  tl.dis_chk = NAN;
-  tl.iters = 0;
-  tl.resid.clear();
+  for (int e : C.pairs) {
+    Pair& P = Wd.pr[e];
+    for (auto* arr : {&P.hat, &P.lam, &P.S, &P.D, &P.last}) {
+      if (c.warm_duals && !first_step) {
+        for (int r = 0; r < 4; ++r) {
+          double* row = arr->data() + (size_t)r * R;
+          for (int k = 0; k < R - 1; ++k) row[k] = row[k + 1];     // drop slot 0, duplicate the last
+        }
+      } else {
+        arr->assign((size_t)2 * 2 * R, 0.0);
+      }
+    }
+    const Agent &a0 = Wd.ag[P.v[0]], &a1 = Wd.ag[P.v[1]];
+    P.d_eff = c.tighten ? c.dis_thres + delay_norm(c, a0.xt, a0.spd) + delay_norm(c, a1.xt, a1.spd) : c.dis_thres;
+    P.active = P.seen = false;
+    P.dis_chk = NAN;
+    P.rk = P.sk = 0.0;
+  }
+  C.flag = C.alias = C.done = false;
+  C.iters = 0;
+  C.resid.clear();
 }
 
-// one outer iteration up to the residuals: x-steps, collision test, z-step, dual update
-void iterate(Ctx& X, Tile& tl, int tile, int t, int it, Work& W) {
+// one outer iteration of a component up to its partials: x-steps, collision tests, pair QPs, dual
+// updates, residual terms (pair order), and [rk, sk, active pairs, checked pairs, failed checks]
+void iterate(Ctx& X, World& Wd, Comp& C, int t, int it, Work& W) {
   const CpuCfg& c = X.c;
-  const int H = c.H, R = H + 1;
-  tl.iters = it + 1;
-  for (int v = 0; v < 2; ++v) x_step(X, tl, v, 2 * tile + v, W);
-  const double thr = c.collide_sq_thres ? tl.d_eff * tl.d_eff : tl.d_eff;
-  bool col = false;
-  const Agent &a0 = tl.ag[0], &a1 = tl.ag[1];
-  for (int k = 0; k < R; ++k) {
-    const double dx = a0.px[k] - a1.px[k], dy = a0.py[k] - a1.py[k];
-    col |= (dx * dx + dy * dy) < thr;
+  const int R = c.H + 1;
+  C.iters = it + 1;
+  for (int a : C.agents) x_step(X, Wd, a, W);
+  double rk = 0.0, sk = 0.0, nact = 0.0, nseen = 0.0, nbad = 0.0;
+  for (int e : C.pairs) {
+    Pair& P = Wd.pr[e];
+    const Agent &a0 = Wd.ag[P.v[0]], &a1 = Wd.ag[P.v[1]];
+    const double thr = c.collide_sq_thres ? P.d_eff * P.d_eff : P.d_eff;
+    bool col = c.no_collision_gate != 0;
+    for (int k = 0; k < R && !col; ++k) {
+      const double dx = a0.px[k] - a1.px[k], dy = a0.py[k] - a1.py[k];
+      col = (dx * dx + dy * dy) < thr;
+    }
+    P.active = col;
+    if (col) {
+      z_step(X, Wd, e, t, W);
+      double dist[64 + 1];
+      for (int k = 0; k < R; ++k) {
+        const double dx = a0.px[k] - a1.px[k], dy = a0.py[k] - a1.py[k];
+        dist[k] = std::sqrt(dx * dx + dy * dy);
+      }
+      dual_update(c, Wd, P, dist);
+      P.dis_chk = dist[1];
+      P.seen = true;
+      // residuals (oracle pair_residuals): v1 side only, times 2
+      const double* hat0 = &P.hat[0];
+      const double* last0 = &P.last[0];
+      double r2 = 0.0, s2 = 0.0;
+      for (int k = 0; k < R; ++k) {
+        const double e1 = a0.px[k] - hat0[k], e2 = a0.py[k] - hat0[R + k];
+        r2 += e1 * e1 + e2 * e2;
+      }
+      for (int i = 0; i < 2 * R; ++i) {
+        const double ev = c.rho * (last0[i] - hat0[i]);
+        s2 += ev * ev;
+      }
+      P.rk = 2 * std::sqrt(r2);
+      P.sk = 2 * std::sqrt(s2);
+    }
+    if (P.seen) {
+      nseen += 1.0;
+      nbad += (P.dis_chk > P.d_eff) ? 0.0 : 1.0;
+    }
+    if (!P.active) continue;
+    nact += 1.0;
+    if (!C.alias) sk += P.sk;
+    rk += P.rk;
   }
-  tl.active = col;
-  tl.rk = tl.sk = 0.0;
-  if (!col) return;
-  z_step(X, tl, t, W);
-  double dist[64 + 1];
-  for (int k = 0; k < R; ++k) {
-    const double dx = a0.px[k] - a1.px[k], dy = a0.py[k] - a1.py[k];
-    dist[k] = std::sqrt(dx * dx + dy * dy);
-  }
-  dual_update(c, tl, dist);
-  tl.dis_chk = dist[1];
-  tl.seen = true;
-  // residuals (oracle pair_residuals): v1 side only, times 2
-  const double* hat0 = &tl.hat[0];
-  const double* last0 = &tl.last[0];
-  double r2 = 0.0, s2 = 0.0;
-  for (int k = 0; k < R; ++k) {
-    const double e1 = a0.px[k] - hat0[k], e2 = a0.py[k] - hat0[R + k];
-    r2 += e1 * e1 + e2 * e2;
-  }
-  for (int i = 0; i < 2 * R; ++i) {
-    const double e = c.rho * (last0[i] - hat0[i]);
-    s2 += e * e;
-  }
-  tl.rk = 2 * std::sqrt(r2);
-  tl.sk = tl.alias ? 0.0 : 2 * std::sqrt(s2);
+  C.part[0] = rk;
+  C.part[1] = sk;
+  C.part[2] = nact;
+  C.part[3] = nseen;
+  C.part[4] = nbad;
 }
 
 // stop rules of one termination group (casadi/main.py:115-118,174-181); part = summed partials
-void decide(const CpuCfg& c, Tile& tl, const double* part, bool& g_flag, bool& g_alias, bool& g_done) {
-  (void)tl;
+void decide(const CpuCfg& c, const double* part, bool& g_flag, bool& g_alias, bool& g_done) {
   const double rk = part[0], sk = part[1], n_act = part[2], n_seen = part[3], n_bad = part[4];
   if (n_act == 0 && !g_flag && !c.fixed_iters) {
     g_done = true;
@@ -880,35 +932,30 @@ void decide(const CpuCfg& c, Tile& tl, const double* part, bool& g_flag, bool& g
   if (c.alias_dual_residual) g_alias = true;
 }
 
-void partials(const CpuCfg& c, const Tile& tl, double* p) {
-  p[0] = tl.active ? tl.rk : 0.0;
-  p[1] = tl.active ? tl.sk : 0.0;
-  p[2] = tl.active ? 1.0 : 0.0;
-  p[3] = tl.seen ? 1.0 : 0.0;
-  p[4] = (tl.seen && !(tl.dis_chk > tl.d_eff)) ? 1.0 : 0.0;
-  (void)c;
-}
-
-void after_decide(const CpuCfg& c, Tile& tl, bool recorded, bool g_alias) {
+void after_decide(const CpuCfg& c, World& Wd, Comp& C, bool recorded, bool g_alias) {
   const int R = c.H + 1;
   if (recorded) {
-    tl.resid.push_back(tl.active ? tl.rk : 0.0);
-    tl.resid.push_back(tl.active ? tl.sk : 0.0);
+    C.resid.push_back(C.part[0]);
+    C.resid.push_back(C.part[1]);
   }
-  if (tl.done) return;
-  if (c.alias_dual_residual) tl.alias = g_alias;
-  else std::memcpy(tl.last.data(), tl.hat.data(), sizeof(double) * 2 * 2 * R);
+  if (C.done) return;
+  if (c.alias_dual_residual) {
+    C.alias = g_alias;
+  } else {
+    for (int e : C.pairs) std::memcpy(Wd.pr[e].last.data(), Wd.pr[e].hat.data(), sizeof(double) * 2 * 2 * R);
+  }
 }
 
-void end_step(const CpuCfg& c, Tile& tl) {
-  for (int v = 0; v < 2; ++v) {
-    // slot 1 of rollout_nonlinear (oracle propagate, casadi/main.py:185-192)
-    double* xt = tl.xt[v];
-    const double s = tl.ag[v].spd, th = xt[2];
+// propagation (oracle propagate, casadi/main.py:185-192): slot 1 of rollout_nonlinear
+void end_step(const CpuCfg& c, World& Wd, const Comp& C) {
+  for (int a : C.agents) {
+    Agent& A = Wd.ag[a];
+    double* xt = A.xt;
+    const double s = A.spd, th = xt[2];
     const double sk = std::sin(th), ck = std::cos(th);
     const double x1 = xt[0] + (-s * sk * th + (s * ck + s * th * sk)) * c.dt;
     const double y1 = xt[1] + (s * ck * th + (s * sk - s * th * ck)) * c.dt;
-    xt[2] = th + (s / c.L * tl.ag[v].u[0]) * c.dt;
+    xt[2] = th + (s / c.L * A.u[0]) * c.dt;
     xt[0] = x1;
     xt[1] = y1;
   }
@@ -920,32 +967,69 @@ extern "C" {
 
 int piadmm_cpu_cfg_size() { return (int)sizeof(CpuCfg); }
 
-// Runs n_steps MPC steps (t = t0 ...) of n_tiles two-agent components on `threads` OpenMP
-// threads.  Agents 2k, 2k+1 form tile k (candidate pair (2k, 2k+1)); ref is (2 n_tiles, 2, T).
-// Outputs (any may be null): xt_out (n_steps, N, 3), u_out (n_steps, N, H), iters_out
-// (n_steps, n_tiles), resid_out (n_steps, n_tiles, max_outer, 2; unused slots NaN),
+// Runs n_steps MPC steps (t = t0 ...) of N agents with the E candidate pairs `edges` (E x 2,
+// v1 < v2) on `threads` OpenMP threads, OpenMP over connected components (labelled in order of
+// their first agent, the oracle's Scenario.components(); agents and pairs of a component in
+// increasing index).  ref is (N, 2, T).  Outputs (any may be null): xt_out (n_steps, N, 3), u_out
+// (n_steps, N, H), iters_out (n_steps, C), resid_out (n_steps, C, max_outer, 2; unused slots NaN),
 // counters [x_qps, z_qps, x_hits, gi_steps, inexact].  seconds_out = wall time of the steps.
-int piadmm_cpu_run(const CpuCfg* cfg, int n_tiles, const double* spd, const double* xt0, const double* ref, int T,
-                   int t0, int n_steps, int threads, double* xt_out, double* u_out, int* iters_out, double* resid_out,
-                   double* seconds_out, long long* counters) {
+// Returns the number of components C (>= 1), or -1 on bad arguments.
+int piadmm_cpu_run_graph(const CpuCfg* cfg, int N, const double* spd, const double* xt0, const double* ref, int T,
+                         int E, const int* edges, int t0, int n_steps, int threads, double* xt_out, double* u_out,
+                         int* iters_out, double* resid_out, double* seconds_out, long long* counters) {
   const CpuCfg& c = *cfg;
-  const int H = c.H, N = 2 * n_tiles, MO = c.max_outer;
-  if (H < 3 || H > 63 || n_tiles < 1 || t0 + n_steps + H > T || MO < 1) return -1;
+  const int H = c.H, MO = c.max_outer;
+  if (H < 3 || H > 63 || N < 1 || E < 0 || t0 + n_steps + H > T || MO < 1) return -1;
+  if (c.dual_mode != 0 && c.dual_mode != 1) return -1;
   if (threads < 1) threads = 1;
-  std::vector<Tile> tiles(n_tiles);
-  for (int k = 0; k < n_tiles; ++k) {
-    Tile& tl = tiles[k];
-    for (int v = 0; v < 2; ++v) {
-      Agent& a = tl.ag[v];
-      a.spd = spd[2 * k + v];
-      agent_P(c, a.spd, 1, a.Pinv);
-      a.ws.init(H, H);
-      a.u.assign(H, 0.0);
-      a.px.assign(H + 1, 0.0);
-      a.py.assign(H + 1, 0.0);
-      for (int j = 0; j < 3; ++j) tl.xt[v][j] = xt0[(2 * k + v) * 3 + j];
+  World Wd;
+  Wd.ag.resize(N);
+  Wd.pr.resize(E);
+  std::vector<int> parent(N);
+  for (int a = 0; a < N; ++a) parent[a] = a;
+  auto find = [&](int a) {
+    while (parent[a] != a) a = parent[a] = parent[parent[a]];
+    return a;
+  };
+  std::vector<std::vector<std::pair<int, std::pair<int, int>>>> adj(N);   // (neighbour, (pair, dir))
+  for (int e = 0; e < E; ++e) {
+    const int v1 = edges[2 * e], v2 = edges[2 * e + 1];
+    if (v1 < 0 || v2 >= N || v1 >= v2) return -1;
+    Wd.pr[e].v[0] = v1;
+    Wd.pr[e].v[1] = v2;
+    adj[v1].push_back({v2, {e, 0}});
+    adj[v2].push_back({v1, {e, 1}});
+    const int ra = find(v1), rb = find(v2);
+    if (ra != rb) parent[std::max(ra, rb)] = std::min(ra, rb);
+  }
+  std::vector<int> cid(N, -1), root_id(N, -1);
+  for (int a = 0; a < N; ++a) {
+    const int r = find(a);
+    if (root_id[r] < 0) {
+      root_id[r] = (int)Wd.comps.size();
+      Wd.comps.emplace_back();
     }
-    pair_P(c, tl.ag[0].spd, tl.ag[1].spd, tl.Ppinv);
+    cid[a] = root_id[r];
+    Wd.comps[cid[a]].agents.push_back(a);
+  }
+  for (int e = 0; e < E; ++e) Wd.comps[cid[edges[2 * e]]].pairs.push_back(e);
+  const int C = (int)Wd.comps.size();
+  for (int a = 0; a < N; ++a) {
+    Agent& A = Wd.ag[a];
+    A.spd = spd[a];
+    std::sort(adj[a].begin(), adj[a].end());
+    for (const auto& x : adj[a]) A.nbr.push_back(x.second);
+    agent_P(c, A.spd, (int)A.nbr.size(), A.Pinv);
+    A.ws.init(H, H);
+    A.u.assign(H, 0.0);
+    A.px.assign(H + 1, 0.0);
+    A.py.assign(H + 1, 0.0);
+    for (int j = 0; j < 3; ++j) A.xt[j] = xt0[a * 3 + j];
+  }
+  for (int e = 0; e < E; ++e) {
+    Pair& P = Wd.pr[e];
+    pair_P(c, Wd.ag[P.v[0]].spd, Wd.ag[P.v[1]].spd, P.Ppinv);
+    for (auto* arr : {&P.hat, &P.lam, &P.S, &P.D, &P.last}) arr->assign((size_t)2 * 2 * (H + 1), 0.0);
   }
   std::vector<Run> runs(threads);
   for (auto& r : runs) r.c = c, r.H = H;
@@ -953,77 +1037,62 @@ int piadmm_cpu_run(const CpuCfg* cfg, int n_tiles, const double* spd, const doub
   for (int st = 0; st < n_steps; ++st) {
     const int t = t0 + st;
     if (!c.term_global || c.fixed_iters) {
-      // per-component termination (or fixed iterations): every tile runs its own loop
+      // per-component termination (or fixed iterations): every component runs its own loop
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
-      for (int k = 0; k < n_tiles; ++k) {
+      for (int k = 0; k < C; ++k) {
         Run& run = runs[omp_get_thread_num()];
         Ctx X{c, ref, T, run, t};
         thread_local Work W;
-        Tile& tl = tiles[k];
-        begin_step(X, tl);
+        Comp& Cm = Wd.comps[k];
+        begin_step(c, Wd, Cm, st == 0);
         bool gf = false, ga = false;
-        for (int it = 0; it < MO && !tl.done; ++it) {
-          iterate(X, tl, k, t, it, W);
-          double p[5];
-          partials(c, tl, p);
+        for (int it = 0; it < MO && !Cm.done; ++it) {
+          iterate(X, Wd, Cm, t, it, W);
           bool gd = false;
-          decide(c, tl, p, gf, ga, gd);
-          tl.done = gd;
-          after_decide(c, tl, gf, ga);
+          decide(c, Cm.part, gf, ga, gd);
+          Cm.done = gd;
+          after_decide(c, Wd, Cm, gf, ga);
         }
-        end_step(c, tl);
+        end_step(c, Wd, Cm);
       }
     } else {
-      // the reference's global scope: one stop decision per outer iteration over all tiles
-#pragma omp parallel for schedule(static) num_threads(threads)
-      for (int k = 0; k < n_tiles; ++k) {
-        Run& run = runs[omp_get_thread_num()];
-        Ctx X{c, ref, T, run, t};
-        begin_step(X, tiles[k]);
-      }
+      // the reference's global scope: one stop decision per outer iteration over all components
+      for (int k = 0; k < C; ++k) begin_step(c, Wd, Wd.comps[k], st == 0);
       bool gf = false, ga = false, gd = false;
       for (int it = 0; it < MO && !gd; ++it) {
-        double part[5] = {0, 0, 0, 0, 0};
-#pragma omp parallel num_threads(threads)
-        {
+#pragma omp parallel for schedule(dynamic, 4) num_threads(threads)
+        for (int k = 0; k < C; ++k) {
           Run& run = runs[omp_get_thread_num()];
           Ctx X{c, ref, T, run, t};
           thread_local Work W;
-          double p5[5] = {0, 0, 0, 0, 0};
-#pragma omp for schedule(dynamic, 4)
-          for (int k = 0; k < n_tiles; ++k) {
-            iterate(X, tiles[k], k, t, it, W);
-            double p[5];
-            partials(c, tiles[k], p);
-            for (int j = 0; j < 5; ++j) p5[j] += p[j];
-          }
-#pragma omp critical
-          for (int j = 0; j < 5; ++j) part[j] += p5[j];
+          iterate(X, Wd, Wd.comps[k], t, it, W);
         }
-        decide(c, tiles[0], part, gf, ga, gd);
-        for (int k = 0; k < n_tiles; ++k) {
-          tiles[k].done = gd;
-          after_decide(c, tiles[k], gf, ga);   // recorded unless no pair ever collided (gf)
+        double part[5] = {0, 0, 0, 0, 0};
+        for (int k = 0; k < C; ++k)                 // component order (the oracle's sum)
+          for (int j = 0; j < 5; ++j) part[j] += Wd.comps[k].part[j];
+        decide(c, part, gf, ga, gd);
+        for (int k = 0; k < C; ++k) {
+          Wd.comps[k].done = gd;
+          after_decide(c, Wd, Wd.comps[k], gf, ga);   // recorded unless no pair ever collided (gf)
         }
       }
 #pragma omp parallel for schedule(static) num_threads(threads)
-      for (int k = 0; k < n_tiles; ++k) end_step(c, tiles[k]);
+      for (int k = 0; k < C; ++k) end_step(c, Wd, Wd.comps[k]);
     }
-    if (xt_out || u_out || iters_out || resid_out) {
-      for (int k = 0; k < n_tiles; ++k) {
-        const Tile& tl = tiles[k];
-        for (int v = 0; v < 2; ++v) {
-          const int a = 2 * k + v;
-          if (xt_out)
-            for (int j = 0; j < 3; ++j) xt_out[((size_t)st * N + a) * 3 + j] = tl.xt[v][j];
-          if (u_out)
-            for (int j = 0; j < H; ++j) u_out[((size_t)st * N + a) * H + j] = tl.ag[v].u[j];
-        }
-        if (iters_out) iters_out[(size_t)st * n_tiles + k] = tl.iters;
-        if (resid_out) {
-          double* ro = resid_out + ((size_t)st * n_tiles + k) * MO * 2;
-          for (int i = 0; i < 2 * MO; ++i) ro[i] = (i < (int)tl.resid.size()) ? tl.resid[i] : NAN;
-        }
+    if (xt_out || u_out) {
+      for (int a = 0; a < N; ++a) {
+        if (xt_out)
+          for (int j = 0; j < 3; ++j) xt_out[((size_t)st * N + a) * 3 + j] = Wd.ag[a].xt[j];
+        if (u_out)
+          for (int j = 0; j < H; ++j) u_out[((size_t)st * N + a) * H + j] = Wd.ag[a].u[j];
+      }
+    }
+    for (int k = 0; k < C; ++k) {
+      const Comp& Cm = Wd.comps[k];
+      if (iters_out) iters_out[(size_t)st * C + k] = Cm.iters;
+      if (resid_out) {
+        double* ro = resid_out + ((size_t)st * C + k) * MO * 2;
+        for (int i = 0; i < 2 * MO; ++i) ro[i] = (i < (int)Cm.resid.size()) ? Cm.resid[i] : NAN;
       }
     }
   }
@@ -1040,7 +1109,23 @@ int piadmm_cpu_run(const CpuCfg* cfg, int n_tiles, const double* spd, const doub
     }
     std::memcpy(counters, s, sizeof(s));
   }
-  return 0;
+  return C;
+}
+
+// The tiled workload (agents 2k, 2k+1 and candidate pair (2k, 2k+1) = tile k; ref (2 n_tiles, 2, T)):
+// piadmm_cpu_run_graph on that graph.  Returns 0 or -1.
+int piadmm_cpu_run(const CpuCfg* cfg, int n_tiles, const double* spd, const double* xt0, const double* ref, int T,
+                   int t0, int n_steps, int threads, double* xt_out, double* u_out, int* iters_out, double* resid_out,
+                   double* seconds_out, long long* counters) {
+  if (n_tiles < 1) return -1;
+  std::vector<int> edges(2 * (size_t)n_tiles);
+  for (int k = 0; k < n_tiles; ++k) {
+    edges[2 * k] = 2 * k;
+    edges[2 * k + 1] = 2 * k + 1;
+  }
+  const int C = piadmm_cpu_run_graph(cfg, 2 * n_tiles, spd, xt0, ref, T, n_tiles, edges.data(), t0, n_steps, threads,
+                                     xt_out, u_out, iters_out, resid_out, seconds_out, counters);
+  return C == n_tiles ? 0 : -1;
 }
 
 }  // extern "C"

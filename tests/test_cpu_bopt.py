@@ -52,5 +52,45 @@ def test_bopt_threads_do_not_change_results():
 def test_bopt_rejects_what_it_does_not_cover():
     with pytest.raises(ValueError):
         cpu_bopt.run(config.casadi_old_pi(H=5), scenario.tiled(1, 5, n_steps=2), 1)
-    with pytest.raises(ValueError):
-        cpu_bopt.run(config.matlab_pi(H=5), scenario.crossing(3, 5, n_steps=2), 1)
+
+
+GRAPH_CASES = [
+    ("crossings", "matlab_pi", 12, {}, 24),
+    ("crossings", "matlab_pi", 12, {"term_global": 1}, 22),
+    ("chains+pair", "casadi_default", 10, {"warm_duals": 1}, 26),
+    ("crossings", "matlab_pi", 10, {"warm_duals": 1, "tighten": 1}, 22),
+]
+
+
+def graph_scenario(kind, H, n_steps):
+    if kind == "crossings":
+        return scenario.concat([scenario.crossing(4, H, n_steps=n_steps + 2, seed=k) for k in range(2)])
+    return scenario.concat([scenario.crossing(4, H, n_steps=n_steps + 2, seed=3, pairs="chain"),
+                            scenario.tiled(1, H, n_steps=n_steps + 2, seed=4),
+                            scenario.crossing(3, H, n_steps=n_steps + 2, seed=5, pairs="chain")])
+
+
+@pytest.mark.parametrize("kind,preset,H,kw,n_steps", GRAPH_CASES,
+                         ids=[f"{k}-{p}-H{h}-{'-'.join(w) or 'natural'}" for k, p, h, w, _ in GRAPH_CASES])
+def test_bopt_general_graph_matches_oracle(kind, preset, H, kw, n_steps):
+    """Any candidate graph (4-vehicle all-pairs crossings: agents in three pairs each; chains next
+    to a tile): the x-step's consensus sum over every candidate neighbour, pairs in index order,
+    per-component or global stop -- equal to the oracle, step by step."""
+    cfg = config.PRESETS[preset](H=H, **kw)
+    scn = graph_scenario(kind, H, n_steps)
+    r = cpu_bopt.run(cfg, scn, n_steps, threads=2)
+    assert r["counters"]["inexact"] == 0
+    orc = O.Oracle(cfg, scn)
+    C = orc.n_comp
+    assert r["iters"].shape == (n_steps, C)
+    for st in range(n_steps):
+        ro = orc.mpc_step()
+        np.testing.assert_array_equal(ro.iters, r["iters"][st])
+        np.testing.assert_allclose(r["u"][st], ro.u, rtol=0, atol=1e-8)
+        np.testing.assert_allclose(r["xt"][st], ro.xt, rtol=1e-8, atol=1e-8)
+        for k in range(C):
+            res = np.array(ro.resid[k], np.float64).reshape(-1, 2)
+            mine = r["resid"][st, k]
+            np.testing.assert_allclose(mine[:len(res)], res, rtol=1e-8, atol=1e-8)
+            assert np.all(np.isnan(mine[len(res):]))
+    assert r["counters"]["z_qps"] > 0

@@ -127,3 +127,23 @@ def test_gpu_equals_bopt_cpu_baseline_at_full_size(Solver, preset, H, tiles, n_s
             np.testing.assert_array_equal(rg.iters, rc["iters"][k])
             close(rg.u, rc["u"][k], rtol=0)
             close(rg.xt, rc["xt"][k])
+
+
+@pytest.mark.parametrize("kw,n_steps", [({"fixed_iters": 1, "term_global": 1}, 3), ({"term_global": 1}, 14)])
+def test_gpu_equals_bopt_on_the_crossing_workload(Solver, kw, n_steps):
+    """bench.py --crossing at its full size (64 four-vehicle all-pairs crossings, 256 agents, 384
+    candidate pairs, H30, matlab_pi, the reference's global scope) on the graph kernel equals the
+    B-opt CPU baseline on the same job (1e-8): the crossing's cpu_baseline times this exact work."""
+    from oracle import cpu_bopt
+    H = 30
+    cfg = config.matlab_pi(H=H, **kw)
+    scn = scenario.concat([scenario.crossing(4, H, n_steps=n_steps + 2, seed=k) for k in range(64)])
+    rc = cpu_bopt.run(cfg, scn, n_steps, threads=4)
+    assert rc["counters"]["inexact"] == 0 and rc["counters"]["z_qps"] > 0
+    with Solver(cfg, scn) as s:
+        for k in range(n_steps):
+            rg = s.mpc_step()
+            assert np.all(rg.status == 0)
+            np.testing.assert_array_equal(rg.iters, rc["iters"][k])
+            close(rg.u, rc["u"][k], rtol=0)
+            close(rg.xt, rc["xt"][k])

@@ -131,3 +131,43 @@ def test_fp32_admm_matrices_keep_answers(Solver, H, n):
     (15, 25) checks the 8-byte alignment of the second wave's fp32 region in LDS mode."""
     compare(Solver, config.matlab_pi(H=H, precision=1, tighten=int(H == 50)),
             scenario.tiled(2, H, n_steps=12, seed=H + 1), n)
+
+
+@pytest.mark.parametrize("kind", ["tiles", "crossings"])
+def test_device_decided_termination_equals_host_decision(Solver, monkeypatch, kind):
+    """Natural global termination without the in-kernel grid barrier (the path of every rank of
+    a multi-GPU job; PIADMM_NO_COOP=1 takes it on one rank): the stop rules run on the device
+    (k_decide after the all-reduced partials, chunks of iterations enqueued ahead, one host read
+    per chunk) and give the same job as one host decision per outer iteration
+    (PIADMM_HOST_DECIDE=1) -- steps of 1 to many outer iterations, fused and graph kernels."""
+    H = 20
+    cfg = config.matlab_pi(H=H, term_global=1)
+    if kind == "tiles":
+        scn = scenario.tiled(6, H, n_steps=24, perturb=True, seed=9)
+    else:
+        scn = scenario.concat([scenario.crossing(4, H, n_steps=24, seed=k) for k in range(3)])
+    monkeypatch.setenv("PIADMM_NO_COOP", "1")
+    s1 = Solver(cfg, scn)
+    monkeypatch.setenv("PIADMM_HOST_DECIDE", "1")
+    s2 = Solver(cfg, scn)
+    monkeypatch.delenv("PIADMM_HOST_DECIDE")
+    monkeypatch.delenv("PIADMM_NO_COOP")
+    its = []
+    try:
+        for _ in range(22):
+            r1, r2 = s1.mpc_step(), s2.mpc_step()
+            assert r1.global_iters == r2.global_iters
+            its.append(r1.global_iters)
+            np.testing.assert_array_equal(r1.iters, r2.iters)
+            np.testing.assert_allclose(r1.global_resid, r2.global_resid, rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(r1.xt, r2.xt, rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(r1.u, r2.u, rtol=1e-12, atol=1e-12)
+        s1.steps_async(22, 2)
+        s2.steps_async(22, 2)
+        s1.sync()
+        s2.sync()
+        np.testing.assert_allclose(s1.state()["xt"], s2.state()["xt"], rtol=1e-12, atol=1e-12)
+    finally:
+        s1.close()
+        s2.close()
+    assert len(set(its)) > 1            # steps of different lengths: chunks shorter and longer than needed
