@@ -41,6 +41,28 @@ enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL
                  ST_GI_FWD = 45, ST_GI_BWD, ST_GI_YPASS, ST_GI_DROP, ST_N_DROP, ST_N_APPEND, ST_N_WARMROW,
                  ST_SUM_M, ST_SUM_MEND, ST_N_GICALL, NSTAMP = 64 };
 
+// ============================================================ address spaces
+// The kernels' scratch pointers travel through structs that also carry HBM pointers, so the
+// compiler sees generic pointers and emits flat loads (TA path; waits on vmcnt AND lgkmcnt) for
+// what is LDS.  Code that knows a pointer is the wave's LDS scratch addresses it through an
+// address_space(3) view (ds_read / ds_write); in_lds() tells the two apart at run time where a
+// pointer is LDS in one mode and HBM in another (a uniform branch).
+typedef __attribute__((address_space(3))) double ldsd;
+__device__ __forceinline__ ldsd* lds_ptr(double* p) { return (ldsd*)p; }
+__device__ __forceinline__ const ldsd* lds_ptr(const double* p) { return (const ldsd*)p; }
+typedef __attribute__((address_space(1))) double gbld;      // HBM (global) view
+__device__ __forceinline__ gbld* gbl_ptr(double* p) { return (gbld*)p; }
+__device__ __forceinline__ const gbld* gbl_ptr(const double* p) { return (const gbld*)p; }
+// generic pointer into LDS? (device pass only; the host pass never runs device code)
+__device__ __forceinline__ bool in_lds(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)p);
+#else
+  (void)p;
+  return false;
+#endif
+}
+
 // ============================================================ wave primitives
 __device__ __forceinline__ int lid() { return (int)__lane_id(); }
 
@@ -68,6 +90,10 @@ __device__ __forceinline__ double rdl(double v, int k) {
   return __longlong_as_double((long long)r);
 }
 __device__ __forceinline__ int rdli(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+// A wave-uniform int the compiler cannot prove uniform (an active-set size carried in a VGPR) into
+// an SGPR: loop bounds, clamps and row offsets derived from it become scalar ops, and an LDS
+// address is one v_add instead of a min / mul_lo (quarter rate) / shift-add chain per element.
+__device__ __forceinline__ int unif(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // DPP move of a double (two 32-bit halves); lanes whose source is outside the row/wave read 0.
 template <int CTRL>
@@ -273,7 +299,8 @@ __device__ __forceinline__ void rollout(const double* xt3, double s, double u, c
 
 // ============================================================ in-wave dense kernels
 // In-place Gauss-Jordan inverse of an SPD matrix held in LDS (stride ld), lane = column.
-__device__ __forceinline__ void gj_invert(double* m, int n, int ld) {
+__device__ __forceinline__ void gj_invert(double* m_, int n, int ld) {
+  ldsd* m = lds_ptr(m_);            // every caller passes the wave's LDS scratch
   const int l = lid();
   const int lc = (l < n) ? l : n - 1;     // lanes >= n mirror column n-1 and never store
   constexpr int U = 8;

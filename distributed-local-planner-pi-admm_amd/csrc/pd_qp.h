@@ -54,6 +54,7 @@ struct QP {
   const double* Kcache;   // x-step: HBM copy of K_s^-1, loaded into K only when ADMM is needed
   mutable int csig;       // x-step: per-lane working-set signature of the cached X', G
   int* gws;               // pair: HBM warm working set of the dual active set (GI_WS ints)
+  bool gws_warm = true;   // pair: start from the stored set (false: cold start, the set is still saved)
   int tstep;              // MPC step index (warm-set bookkeeping)
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
@@ -414,7 +415,8 @@ __device__ __forceinline__ Gather4 s_gather(const QP<NV>& P, int ia, int ibd) {
 }
 
 // Solve L L' x = b (lane a holds b_a, a < m).  L lower in fac (stride ld), linv = 1/L_aa.
-__device__ __forceinline__ double chol_solve(const double* L, int ld, double linv, double b, int m) {
+__device__ __forceinline__ double chol_solve(const double* L_, int ld, double linv, double b, int m) {
+  const ldsd* L = lds_ptr(L_);      // the factor lives in the wave's LDS scratch
   const int l = lid();
   for (int k = 0; k < m; ++k) {       // forward, column-oriented
     const double Llk = (l > k && l < m) ? L[l * ld + k] : 0.0;
@@ -439,13 +441,14 @@ __device__ __forceinline__ double chol_solve(const double* L, int ld, double lin
 // it is dropped (zero column of L, linv = 0, so its multiplier solves to 0), as the
 // oracle's active-set solver does.  Returns false only on a non-finite pivot.
 constexpr double DEP_TOL = 1e-10;
-__device__ __forceinline__ bool chol_factor(double* fac, int ld, double sdiag, double delta, int m, double& linv) {
+__device__ __forceinline__ bool chol_factor(double* fac_, int ld, double sdiag, double delta, int m, double& linv) {
+  ldsd* fac = lds_ptr(fac_);        // the wave's LDS scratch
   const int l = lid();
   for (int k = 0; k < m; ++k) {
     double acc = 0.0;
     if (l >= k && l < m) {
-      const double* ri = fac + l * ld;
-      const double* rk = fac + k * ld;
+      const ldsd* ri = fac + l * ld;
+      const ldsd* rk = fac + k * ld;
       int j = 0;
       for (; j + 4 <= k; j += 4)
         acc += ri[j] * rk[j] + ri[j + 1] * rk[j + 1] + ri[j + 2] * rk[j + 2] + ri[j + 3] * rk[j + 3];
@@ -559,7 +562,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
         const double sv = gg[u].c[0] * tv[u][0] + gg[u].c[1] * tv[u][1] + gg[u].c[2] * tv[u][2] + gg[u].c[3] * tv[u][3];
         if (b < m && l <= b && l < m) {
           if (b == l) sdiag = sv;
-          else P.fac[l * ld + b] = sv;
+          else lds_ptr(P.fac)[l * ld + b] = sv;
         }
       }
     }
@@ -593,7 +596,8 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
     for (int b = 0; b < m; ++b) {
       const double lb = rdl(lamv, b);
       if (l < m) {
-        const double sab = (b == l) ? sdiag : (b > l ? P.fac[l * ld + b] : P.fac[b * ld + l]);
+        const ldsd* F = lds_ptr(P.fac);
+        const double sab = (b == l) ? sdiag : (b > l ? F[l * ld + b] : F[b * ld + l]);
         sl += sab * lb;
       }
     }
@@ -687,7 +691,7 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
 // a hit costs one fused pass over P^-1 and X' plus the x recovery.
 __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, const int* ids, const double* vb_b) {
   const int l = lid(), H = P.H, ld = P.fld;
-  double* fac = P.fac;
+  ldsd* fac = lds_ptr(P.fac);       // the wave's LDS scratch
   double* XT = P.XT;
   // S (upper triangle, lane a = row a) from the LDS P^-1
   unsigned long long t_s = STAMP_T();
@@ -717,14 +721,16 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   wsync();
   double linv = 0.0;
   // unshifted: a dependent working-set row (degenerate vertex) is dropped by chol_factor
-  if (!chol_factor(fac, ld, sdiag, 0.0, m, linv)) return false;
+  if (!chol_factor(P.fac, ld, sdiag, 0.0, m, linv)) return false;
   if (l < m) P.fdiag[64 + l] = linv;
   STAMP_ADD(ST_RED_CHOL, t_c);
   unsigned long long t_x = STAMP_T();
   // right-hand sides, one per lane: lane i < H -> row i of Y = P^-1 A_W', lane H -> b
+  // X', G, g: LDS (LDS mode) or HBM (big / graph mode) -- the same space for both tables
+  auto tables = [&](auto XTp, auto Gp) {
   const int li = (l <= H) ? l : H;
   const bool own = l <= H;
-  double* xr = XT + li * P.xld;
+  auto xr = XTp + li * P.xld;
   constexpr int XB = 4;
   for (int a0 = 0; a0 < m; a0 += XB) {
     int o[XB][2];
@@ -809,7 +815,7 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
         if (a0 + u < m && l < H) fac[(a0 + u) * ld + l] = cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1];
     }
     wsync();
-    const double* xj = XT + lc * P.xld;
+    const auto xj = XTp + lc * P.xld;
     constexpr int GB = 8;
     for (int i0 = 0; i0 < H; i0 += GB) {
       double acc[GB], pv[GB];
@@ -820,17 +826,17 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
       }
       for (int a = 0; a < m; ++a) {
         const double xja = xj[a];
-        const double* ya = fac + a * ld + i0;
+        const ldsd* ya = fac + a * ld + i0;
 #pragma unroll
         for (int u = 0; u < GB; ++u) acc[u] += ya[u] * xja;     // rows past H are never stored
       }
 #pragma unroll
       for (int u = 0; u < GB; ++u)
-        if (l < H && i0 + u < H) P.G[(i0 + u) * H + l] = pv[u] - acc[u];
+        if (l < H && i0 + u < H) Gp[(i0 + u) * H + l] = pv[u] - acc[u];
     }
     double gacc = 0.0;
-    for (int a = 0; a < m; ++a) gacc += fac[a * ld + lc] * XT[H * P.xld + a];
-    if (l < H) P.G[H * H + l] = gacc;
+    for (int a = 0; a < m; ++a) gacc += fac[a * ld + lc] * XTp[H * P.xld + a];
+    if (l < H) Gp[H * H + l] = gacc;
     if (P.gmem) gsync();
     else wsync();
   }
@@ -840,10 +846,10 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
     double s1 = 0.0, s2 = 0.0, t1 = 0.0, t2 = 0.0;
     const int la = (l < m) ? l : 0;
     for (int k = 0; k < H; ++k) {
-      const double gk = P.G[k * H + (l < H ? l : 0)];
-      const double xk = XT[k * P.xld + la];
-      if (l < H) P.G[k * H + l] = s2;
-      if (l < m) XT[k * P.xld + l] = t2;
+      const double gk = Gp[k * H + (l < H ? l : 0)];
+      const double xk = XTp[k * P.xld + la];
+      if (l < H) Gp[k * H + l] = s2;
+      if (l < m) XTp[k * P.xld + l] = t2;
       s1 += gk;
       s2 += s1;
       t1 += xk;
@@ -852,6 +858,9 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
     if (P.gmem) gsync();
     else wsync();
   }
+  };
+  if (in_lds(XT)) tables(lds_ptr(XT), lds_ptr(P.G));
+  else tables(gbl_ptr(XT), gbl_ptr(P.G));
   return true;
 }
 
@@ -1078,20 +1087,7 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
 // reaching the cap, a full set or the step limit return false and the caller falls back to
 // ADMM + PDAS; the result is certified by the same KKT test either way.
 
-// LDS-typed views: the QP struct's pointers are generic (LDS or HBM by mode), which makes the
-// compiler emit flat loads (TA path, vmcnt + lgkmcnt waits) for what is LDS -- the passes below
-// address the wave's scratch through address_space(3) pointers so they become ds_read / ds_write.
-typedef __attribute__((address_space(3))) double ldsd;
-__device__ __forceinline__ ldsd* lds_ptr(double* p) { return (ldsd*)p; }
-// generic pointer into LDS? (device pass only; the host pass never runs device code)
-__device__ __forceinline__ bool in_lds(const void* p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)p);
-#else
-  (void)p;
-  return false;
-#endif
-}
+// (LDS-typed views ldsd / lds_ptr / in_lds: pd_common.h)
 
 // The broadcast operand of an m-term pass: vbuf[a] = v (lanes a < m), 0 up to lane 63, so the
 // batched loads of a pass (never beyond lane 63: m <= 63, batches of 8 from multiples of 8) need
@@ -1105,8 +1101,9 @@ __device__ __forceinline__ void put_bcast(ldsd* vb, double v, int m) {
 // r = S^-1 v over the m active constraints (v, r at lanes a < m): lane = column of the symmetric
 // inverse (LDS, stride ld), v broadcast from LDS (vbuf: 64 doubles of the wave's vector buffer).
 constexpr int SINV_U = 8;
-__device__ __forceinline__ double sinv_gemv(double* Si_, int ld, double* vbuf_, double v, int m) {
+__device__ __forceinline__ double sinv_gemv(double* Si_, int ld_, double* vbuf_, double v, int m_) {
   const int l = lid();
+  const int m = unif(m_), ld = unif(ld_);
   ldsd* vb = lds_ptr(vbuf_);
   const ldsd* col = lds_ptr(Si_) + ((l < m) ? l : 0);
   put_bcast(vb, v, m);
@@ -1115,7 +1112,7 @@ __device__ __forceinline__ double sinv_gemv(double* Si_, int ld, double* vbuf_, 
     double sv[SINV_U], vv[SINV_U];
 #pragma unroll
     for (int u = 0; u < SINV_U; ++u) {
-      sv[u] = col[min(j0 + u, m - 1) * ld];
+      sv[u] = col[unif(min(j0 + u, m - 1) * ld)];
       vv[u] = vb[j0 + u];
     }
 #pragma unroll
@@ -1130,17 +1127,18 @@ __device__ __forceinline__ double sinv_gemv(double* Si_, int ld, double* vbuf_, 
 
 // z[v] -= sum_{a < m} coef_a Y[a][v] (lane = variable; coef at lanes a < m, broadcast from LDS).
 template <int NV, typename YP>
-__device__ __forceinline__ void y_axpy_t(YP Y, int H, ldsd* vb, int m, double* z) {
-  const int l = lid(), H2 = NV * H;
+__device__ __forceinline__ void y_axpy_t(YP Y, int H_, ldsd* vb, int m_, double* z) {
+  const int l = lid(), H = unif(H_), m = unif(m_), H2 = NV * H;
   const int lc = (l < H) ? l : 0;
+  const auto Yl = Y + lc;
   for (int a0 = 0; a0 < m; a0 += SINV_U) {
     double yv[SINV_U][NV], cv[SINV_U];
 #pragma unroll
     for (int u = 0; u < SINV_U; ++u) {
-      const int a = min(a0 + u, m - 1);
+      const int a = unif(min(a0 + u, m - 1));
       cv[u] = vb[a0 + u];
 #pragma unroll
-      for (int v = 0; v < NV; ++v) yv[u][v] = Y[a * H2 + v * H + lc];
+      for (int v = 0; v < NV; ++v) yv[u][v] = Yl[unif(a * H2 + v * H)];
     }
 #pragma unroll
     for (int u = 0; u < SINV_U; ++u)
@@ -1153,7 +1151,7 @@ __device__ __forceinline__ void y_axpy(double* Y, int H, double* vbuf_, double c
   ldsd* vb = lds_ptr(vbuf_);
   put_bcast(vb, coef, m);
   if (in_lds(Y)) y_axpy_t<NV>((const ldsd*)lds_ptr(Y), H, vb, m, z);
-  else y_axpy_t<NV>((const double*)Y, H, vb, m, z);   // big mode: the columns in HBM / L2
+  else y_axpy_t<NV>(gbl_ptr((const double*)Y), H, vb, m, z);   // big mode: the columns in HBM / L2
   wsync();
 }
 
@@ -1263,16 +1261,17 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     if (l < m) {
       const double rl = r * id;
       ldsd* col = Sil + l;
-      for (int j0 = 0; j0 < m; j0 += SINV_U) {
+      const int mu = unif(m), ldu = unif(ld);
+      for (int j0 = 0; j0 < mu; j0 += SINV_U) {
         double sv[SINV_U], rv[SINV_U];
 #pragma unroll
         for (int u = 0; u < SINV_U; ++u) {
-          sv[u] = col[min(j0 + u, m - 1) * ld];
+          sv[u] = col[unif(min(j0 + u, mu - 1) * ldu)];
           rv[u] = vbl[j0 + u];
         }
 #pragma unroll
         for (int u = 0; u < SINV_U; ++u)
-          if (j0 + u < m) col[(j0 + u) * ld] = sv[u] + rv[u] * rl;
+          if (j0 + u < mu) col[unif((j0 + u) * ldu)] = sv[u] + rv[u] * rl;
       }
       Sil[m * ld + l] = -rl;      // row m, column l
       Sil[l * ld + m] = -rl;      // row l, column m
@@ -1304,16 +1303,17 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     if (l < m && l != k) {
       const double cl = c / d;
       ldsd* col = Sil + l;
-      for (int j0 = 0; j0 < m; j0 += SINV_U) {
+      const int mu = unif(m), ldu = unif(ld);
+      for (int j0 = 0; j0 < mu; j0 += SINV_U) {
         double sv[SINV_U], cv[SINV_U];
 #pragma unroll
         for (int u = 0; u < SINV_U; ++u) {
-          sv[u] = col[min(j0 + u, m - 1) * ld];
+          sv[u] = col[unif(min(j0 + u, mu - 1) * ldu)];
           cv[u] = vbl[j0 + u];
         }
 #pragma unroll
         for (int u = 0; u < SINV_U; ++u)
-          if (j0 + u < m) col[(j0 + u) * ld] = sv[u] - cv[u] * cl;
+          if (j0 + u < mu) col[unif((j0 + u) * ldu)] = sv[u] - cv[u] * cl;
       }
     }
     wsync();
@@ -1400,7 +1400,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   start();
   bool warm = false;
   unsigned long long t_wb = STAMP_T();
-  if (P.gws) {
+  if (P.gws && P.gws_warm) {
     // ---- pair: the stored active set (this step's, or the previous step's shifted)
     const int gm = P.gws[0], gt = P.gws[1];
     const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
@@ -1760,7 +1760,11 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         }
       }
     } else {
-      ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+      // pair: one reduced solve on the previous solve's labels (a hit when the pair QP barely
+      // moved since); label moves are left to the dual active set, warm-started from the same
+      // active set -- each further PDAS step is a full Schur build + factorization (r03 stamps:
+      // 3.25 of them per step on a crossing, nearly all followed by the dual active set anyway)
+      ok = pdas<NV, XU>(P, lab, x, y, n_pdas, NV == 2 ? 1 : PDAS_STEPS);
     }
   }
   if constexpr (NV == 2) {

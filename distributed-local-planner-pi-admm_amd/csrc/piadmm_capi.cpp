@@ -392,6 +392,8 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   {
     const char* ps = std::getenv("PIADMM_PAIR_SOLVER");
     A.pair_gi = (ps && std::strcmp(ps, "admm") == 0) ? 0 : 1;
+    const char* pw = std::getenv("PIADMM_PAIR_WARM");
+    A.pair_warm = (pw && pw[0] == '0') ? 0 : 1;
     // PIADMM_X_SOLVER: "pdas" = one-step label moves + ADMM only; "gi" = the dual active set
     // warm-started from the labels after a failed reduced solve of them; "gi_warm" = the same,
     // except that an MPC step's first x-QP skips that reduced solve (a table rebuild, ~20 us,

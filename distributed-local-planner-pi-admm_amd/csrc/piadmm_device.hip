@@ -261,6 +261,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     qe.ycap = A.pair_gi ? ((Ke ? 4 : 2) * H * H) / (2 * H) : 0;
     qe.y_in_k = true;
     qe.gws = A.gi_ws + (size_t)e * GI_WS;
+    qe.gws_warm = A.pair_warm != 0;
     qe.tstep = t;
     // Ke doubles as the H x 2H staging of the per-scenario pair tables; with fp32 images in
     // LDS mode the fp32 region (2H^2 doubles of space) takes that role

@@ -246,6 +246,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
   qe.ycap = A.pair_gi ? (W.ylds ? GYCAP : min(WAVE, A.ke_stride / (2 * H))) : 0;
   qe.y_in_k = W.ylds == nullptr;
   qe.gws = A.gi_ws + (size_t)e * GI_WS;
+  qe.gws_warm = A.pair_warm != 0;
   qe.tstep = t;
   qe.csig = -1;
   if (l == 0) W.zfs[0] = -1;

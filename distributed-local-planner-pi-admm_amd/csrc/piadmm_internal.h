@@ -33,6 +33,7 @@ struct DevArgs {
   piadmm_config_t cfg;
   int N, E, C, T;
   int pair_gi;              // 1: pair QPs try the dual active set first (env PIADMM_PAIR_SOLVER)
+  int pair_warm;            // 1: the pair's dual active set starts from its last active set (PIADMM_PAIR_WARM=0: cold)
   int x_gi;                 // x-step working-set changes by the dual active set (1); the step's first x-QP
                             // without the labels' reduced solve (2), started cold (3); all cold (4); PIADMM_X_SOLVER
   // scenario (read-only during a step)
