@@ -65,6 +65,10 @@ WORKLOADS = {
     "x4": dict(tiles=64, H=30, preset="matlab_pi", max_outer=100, tighten=0, scaling="weak", kind="crossing",
                desc="256 agents x H30 per GPU (64 four-vehicle all-pairs crossings, 384 candidate pairs), "
                     "matlab_pi preset"),
+    "ch": dict(tiles=1024, H=30, preset="matlab_pi", max_outer=100, tighten=0, scaling="weak", kind="chain",
+               cpu_steps=2,
+               desc="1024 agents x H30 per GPU in ONE connected chain (1023 candidate pairs; the component spans "
+                    "256 workgroups of 4 agents), matlab_pi preset"),
 }
 
 
@@ -128,6 +132,8 @@ def make_scenario(wl: dict, n_steps: int, rank: int = 0):
     if wl.get("kind") == "crossing":
         return scenario.concat([scenario.crossing(4, wl["H"], n_steps=n_steps, seed=1000 * rank + k)
                                 for k in range(wl["tiles"])])
+    if wl.get("kind") == "chain":
+        return scenario.crossing(wl["tiles"], wl["H"], n_steps=n_steps, seed=1000 * rank + 1, pairs="chain")
     return scenario.tiled(wl["tiles"], wl["H"], n_steps=n_steps, perturb=True, seed=1000 * rank)
 
 
@@ -145,19 +151,22 @@ def cpu_baseline(wl: dict, budget_s: float, K: int) -> dict:
     n_tiles, H = wl["tiles"], wl["H"]
     cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=1, max_outer=wl["max_outer"], tighten=wl["tighten"],
                                         term_global=1)
-    crossing = wl.get("kind") == "crossing"
+    kind = wl.get("kind", "tiles")
+    K = wl.get("cpu_steps", K)      # a bounded sample of the job's steps (a single-component chain
+                                    # runs on one host thread: OpenMP is over components)
     bopt = pool = None
     try:
         from oracle import cpu_bopt
         scn = make_scenario(wl, K)
-        bopt = cpu_bopt.time_baseline(cfg, n_tiles, (0.6 if not crossing else 1.0) * budget_s, n_steps=K, scn=scn,
-                                      desc=f"{n_tiles} four-vehicle crossings" if crossing else None)
+        desc = {"crossing": f"{n_tiles} four-vehicle crossings", "chain": f"one {n_tiles}-agent chain"}.get(kind)
+        bopt = cpu_bopt.time_baseline(cfg, n_tiles, (0.6 if kind == "tiles" else 1.0) * budget_s, n_steps=K, scn=scn,
+                                      desc=desc)
         r = cpu_bopt.run(cfg.replace(fixed_iters=0), scn, K, bopt["cores"])
         bopt["natural_ms_per_step"] = 1e3 * r["seconds"] / K
         bopt["natural_outer_iters_per_step"] = float(r["iters"][:, 0].mean())
     except Exception as e:          # noqa: BLE001 -- report the NumPy pool alone
         print(f"bench.py: B-opt CPU baseline failed ({e})", file=sys.stderr)
-    if not crossing:                # the NumPy pool parallelises over two-vehicle tiles
+    if kind == "tiles":             # the NumPy pool parallelises over two-vehicle tiles
         try:
             from oracle import cpu_parallel
             pool = cpu_parallel.time_baseline(cfg, n_tiles, 0.4 * budget_s)
@@ -227,7 +236,9 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
         cnt = solver.counters()
         spl, C = solver.steps_per_launch(), max(solver.C, 1)
         N = int(shard.owned.sum()) if shard is not None else solver.N
-        xchg = shard is not None and shard.n_slots > 0
+        # pairs across ranks (an X and a Z launch per outer iteration), or one component split over
+        # workgroups (the same two launches, no exchange)
+        xchg = (shard is not None and shard.n_slots > 0) or wl.get("kind") == "chain"
     finally:
         solver.close()
     if dist is not None:
@@ -243,7 +254,7 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
         n_launch = 2 * int(job_iters) + K
     else:
         n_launch = -(-K // spl) if spl > 1 else int(job_iters) + K
-    graph = xchg or wl.get("kind") == "crossing"
+    graph = xchg or wl.get("kind") in ("crossing", "chain")
     return dict(wall=wall, ev_ms=ev_ms, job_iters=job_iters, n_launch=n_launch, spl=spl, N=N, C=C, xchg=xchg,
                 kernel="pd::k_graph_step" if graph else "pd::k_mpc_step"), cnt
 
@@ -262,6 +273,7 @@ def main():
     g.add_argument("--config5", action="store_true", help="BASELINE configs[4]: H=50 with delay tightening")
     g.add_argument("--strong", action="store_true", help="BASELINE configs[3]: 1024 agents sharded over N GPUs")
     g.add_argument("--crossing", action="store_true", help="coupling-heavy: 64 four-vehicle all-pairs crossings")
+    g.add_argument("--chain", action="store_true", help="one connected 1024-agent chain (component over workgroups)")
     ap.add_argument("--split", choices=("components", "interleaved"), default="components",
                     help="--strong: whole tiles per rank, or every tile across two ranks (boundary exchange)")
     args = ap.parse_args()
@@ -275,7 +287,8 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    key = "c2" if args.config2 else "c5" if args.config5 else "c4" if args.strong else "x4" if args.crossing else "c3"
+    key = ("c2" if args.config2 else "c5" if args.config5 else "c4" if args.strong else "x4" if args.crossing
+           else "ch" if args.chain else "c3")
     wl = WORKLOADS[key]
     # the CPU baseline first, on the host cores, before this process touches the GPU (its worker
     # pool is started with the spawn method)
@@ -303,7 +316,7 @@ def main():
     avg_launch_s = (m["ev_ms"] / 1e3) / m["n_launch"]
     bytes_launch = algorithmic_bytes(cnt, H) / m["n_launch"]
     achieved = bytes_launch / avg_launch_s / 1e9
-    wname = f"{'crossing4x' if wl.get('kind') == 'crossing' else 'tiled'}{wl['tiles']}_H{H}_{wl['preset']}_fixed{M}" + (
+    wname = f"{ {'crossing': 'crossing4x', 'chain': 'chain'}.get(wl.get('kind'), 'tiled')}{wl['tiles']}_H{H}_{wl['preset']}_fixed{M}" + (
         "_tight" if wl["tighten"] else "")
     traffic = latest_profile("traffic", wname) if not args.natural else None
     traffic_launch = traffic["hbm_bytes_per_step"] * K / m["n_launch"] if traffic else None
@@ -323,6 +336,8 @@ def main():
         "dtype": "f64",
         "data": (f"synthetic: seeded four-vehicle all-pairs crossings (lanes 0, 1 = the reference's 2-vehicle "
                  f"intersection; {agents_job} agents in the job)" if wl.get("kind") == "crossing" else
+                 f"synthetic: one seeded {agents_job}-vehicle chain on the crossing's lanes (candidate pairs (k, k+1))"
+                 if wl.get("kind") == "chain" else
                  f"synthetic: seeded tiles of the reference 2-vehicle intersection ({agents_job} agents in the job)"),
         "config": {
             "workload": wl["desc"] + ", " + (

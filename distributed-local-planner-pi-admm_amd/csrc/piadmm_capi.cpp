@@ -48,6 +48,10 @@ struct piadmm_ctx {
   // boundary exchange buffer per outer iteration
   bool xchg = false;
   int n_slots = 0;
+  // a connected component larger than the workgroup block (term_global) split over several
+  // workgroups: the graph kernel's X and Z phases as separate launches (like a sharded job's,
+  // without the exchange: every agent's positions are in this handle's memory)
+  bool split = false;
   double* d_xrecv = nullptr;
   // host all-reduce transport (piadmm_set_allreduce): used when there is no RCCL communicator
   piadmm_allreduce_fn xfn = nullptr;
@@ -308,6 +312,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   HIPCHK(h, hipStreamSynchronize(h->stream));
   free_all(h);
   h->step_open = false;
+  h->split = false;
   h->comp_ptr.assign(1, 0);
   h->comp_edge.clear();
   std::vector<int> nbr(N, 0);
@@ -345,6 +350,35 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
       const int r = find(a);
       if (id_of[r] < 0) id_of[r] = C++;
       comp[a] = id_of[r];
+    }
+    // Components of more than `block` agents (PIADMM_GRAPH_BLOCK, default 4; 0: never) span
+    // several workgroups under the global scope: blocks of `block` consecutive agents (in index
+    // order, numbered by first agent), a pair owned by the block of its first agent.  The x-step
+    // of an agent reads the hat / lam of pairs other blocks own and a pair reads positions of
+    // agents other blocks own, so the X and Z phases run as separate launches (the kernel boundary
+    // orders them); the stop test sums the blocks' partials (one job-wide decision).
+    h->split = false;
+    if (h->cfg.term_global && !sharded) {
+      int block = 4;
+      if (const char* gb = std::getenv("PIADMM_GRAPH_BLOCK")) block = std::atoi(gb);
+      if (block > 0) {
+        std::vector<int> csize(C, 0);
+        for (int a = 0; a < N; ++a) ++csize[comp[a]];
+        bool any = false;
+        for (int k = 0; k < C; ++k) any |= csize[k] > block;
+        if (any) {
+          std::vector<int> seen(C, 0), cur(C, -1), nb;
+          int NB = 0;
+          for (int a = 0; a < N; ++a) {
+            const int k = comp[a];
+            if (seen[k] % block == 0) cur[k] = NB++;     // a new block of component k
+            ++seen[k];
+            comp[a] = cur[k];
+          }
+          C = NB;
+          h->split = true;
+        }
+      }
     }
     g_aptr.assign(C + 1, 0);
     g_eptr.assign(C + 1, 0);
@@ -561,7 +595,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   {
     const char* nc = std::getenv("PIADMM_NO_COOP");
     h->coop = h->cfg.term_global && !h->cfg.fixed_iters && !(nc && nc[0] == '1') && !h->xchg &&
-              (A.graph ? pd::graph_coop_fits(A, h->cfg.device) : pd::coop_fits(A, h->cfg.device));
+              !h->split && (A.graph ? pd::graph_coop_fits(A, h->cfg.device) : pd::coop_fits(A, h->cfg.device));
     (void)hipGetLastError();   // a refused query must not surface as the next launch's error
   }
   h->have_scn = true;
@@ -650,14 +684,20 @@ static int32_t devstop_step(piadmm_handle_t h, int32_t tk, bool sync_outputs) {
   hipStream_t s = h->stream;
   const int M = c.max_outer;
   const size_t nx = h->xchg ? (size_t)h->n_slots * 3 * (c.H + 1) : 0;
+  const bool phases = h->xchg || h->split;      // X and Z phases as separate launches
   HIPCHK(h, hipMemsetAsync(h->a.gctl, 0, 4 * sizeof(int), s));
   if (!h->a.graph) LAUNCH(h, pd::launch_pair_deff(h->a, s));
   int it = 0, K = std::max(1, std::min(h->chunk_guess, M));
   while (true) {
     const int n = std::min(K, M - it);
     for (int j = 0; j < n; ++j, ++it) {
-      const int f = (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | pd::F_DEVSTOP;
-      if (h->xchg) {
+      int f = (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | pd::F_DEVSTOP;
+      if (it == 0 && h->split) {
+        // the blocks of a split component reset their pairs before any block's x-step reads them
+        LAUNCH(h, launch_step(h->a, tk, 1, 0, 0, pd::F_FIRST | pd::F_GLOBAL | pd::F_INITONLY, s));
+        f &= ~pd::F_FIRST;
+      }
+      if (phases) {
         LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f | pd::F_XONLY, s));
         if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
         LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, pd::F_GLOBAL | pd::F_DEVSTOP | pd::F_ZONLY, s));
@@ -704,7 +744,12 @@ static int32_t run_steps_xchg(piadmm_handle_t h, int32_t t, int32_t n, bool sync
     h->ghist.assign((size_t)2 * M, NAN);
     int flag = 0, nit = 0, nanlast = 0;
     for (int it = 0; it < M; ++it) {
-      LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | pd::F_XONLY, s));
+      int f = (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | pd::F_XONLY;
+      if (it == 0 && h->split) {   // (see devstop_step)
+        LAUNCH(h, launch_step(h->a, tk, 1, 0, 0, pd::F_FIRST | pd::F_GLOBAL | pd::F_INITONLY, s));
+        f &= ~pd::F_FIRST;
+      }
+      LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f, s));
       if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
       LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, pd::F_GLOBAL | pd::F_ZONLY, s));
       nit = it + 1;
@@ -779,7 +824,7 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
   const piadmm_config_t& c = h->cfg;
   hipStream_t s = h->stream;
   const int M = c.max_outer;
-  if (h->xchg) return run_steps_xchg(h, t, n, sync_outputs);
+  if (h->xchg || h->split) return run_steps_xchg(h, t, n, sync_outputs);
   if (!c.term_global) {
     LAUNCH(h, launch_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST, s));
     return PIADMM_OK;
@@ -886,7 +931,9 @@ int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_o
 int32_t piadmm_outer_iter(piadmm_handle_t h, int32_t t, int32_t it, int32_t* stop_out) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
-  if (h->xchg) return fail(h, PIADMM_E_STATE, "host stepping of a sharded graph is not supported");
+  if (h->xchg || h->split)
+    return fail(h, PIADMM_E_STATE, "host stepping of a sharded graph or of components split over workgroups "
+                                   "is not supported");
   const piadmm_config_t& c = h->cfg;
   if (it < 0 || it >= c.max_outer) return fail(h, PIADMM_E_ARG, "it must be in [0, max_outer)");
   if (t < 0 || t + c.H + 1 > h->T) return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
@@ -970,7 +1017,7 @@ int32_t piadmm_n_components(piadmm_handle_t h) { return h && h->have_scn ? h->C 
 
 int32_t piadmm_steps_per_launch(piadmm_handle_t h) {
   if (!h || !h->have_scn) return 0;
-  if (h->xchg) return 1;
+  if (h->xchg || h->split) return 1;
   if (h->cfg.term_global && !h->cfg.fixed_iters) return (h->coop && !h->comm && !h->xfn) ? h->step_cap : 1;
   return h->step_cap;
 }

@@ -568,6 +568,16 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
     for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
     if (coop && ci == 0)
       for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) A.ghist[(size_t)slot * 2 * M + i] = NAN;
+    if (flags & F_INITONLY) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        A.cst[(size_t)ci * 4 + 0] = 0;
+        A.cst[(size_t)ci * 4 + 1] = 0;
+        A.cst[(size_t)ci * 4 + 3] = 0;
+        A.iters[ci] = 0;
+      }
+      return;
+    }
   }
   int flag = first ? 0 : A.cst[(size_t)ci * 4 + 0];
   int aliased = first ? 0 : A.cst[(size_t)ci * 4 + 1];

@@ -190,6 +190,9 @@ constexpr int F_ZONLY = 64;
 // with the all-reduce and k_decide between them, and the host reads the stop state once per
 // chunk; the LAST launch takes its iteration count and NANLAST from A.gctl.
 constexpr int F_DEVSTOP = 128;
+// With F_FIRST: only the step init (seeds, per-step pair reset), no iteration -- a component split
+// over workgroups resets the pairs its blocks own before ANY block's first x-step reads them.
+constexpr int F_INITONLY = 256;
 
 int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 // candidate-pair detection (piadmm_detect.hip)

@@ -85,6 +85,14 @@ SYMBOLS = [
                                           _P(ctypes.c_uint8)]),
     ("piadmm_set_allreduce", c_i32, [_H, ctypes.c_void_p, ctypes.c_void_p]),
     ("piadmm_candidate_pairs", c_i32, [_H, _dp, _dp, c_i32, _ip, c_i32, _ip, _P(ctypes.c_float)]),
+    ("piadmm_obca_create", c_i32, [c_i32, _P(_H)]),
+    ("piadmm_obca_destroy", c_i32, [_H]),
+    ("piadmm_obca_last_error", ctypes.c_char_p, [_H]),
+    ("piadmm_obca_solve", c_i32, [_H, _dp, c_i32, _dp, _ip]),
+    ("piadmm_obca_upload", c_i32, [_H, _dp, c_i32]),
+    ("piadmm_obca_run", c_i32, [_H, c_i32]),
+    ("piadmm_obca_time", c_i32, [_H, c_i32, _P(ctypes.c_float)]),
+    ("piadmm_obca_download", c_i32, [_H, _dp, _ip, c_i32]),
 ]
 
 # piadmm_allreduce_fn: int32_t (*)(void* ctx, double* buf, int64_t n)

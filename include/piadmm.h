@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PIADMM_ABI_VERSION 4
+#define PIADMM_ABI_VERSION 5
 
 enum {
   PIADMM_OK = 0,
@@ -240,6 +240,44 @@ int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double
 /* Diagnostic builds (-DPIADMM_STAMPS, libpiadmm_stamps.so) only: per-component
  * cycle sums of the kernel phases (C x 32 uint64); PIADMM_E_STATE otherwise. */
 int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n);
+
+/* ---- OBCA local subproblem ------------------------------------------
+ * Replaces the vehicle side of the OBCA-ADMM planner: OBCAOptimizer.local_initialize,
+ * local_build_model, local_generate_constrain, local_generate_variable, local_generate_object and
+ * local_solve (Distributed_planner/decentralized/optimizer.py:40-201) -- one CasADi/IPOPT NLP per
+ * vehicle per ADMM iterate (decentralized_overtaking_ADMM.py:49-63) -- with a batched SQP on the
+ * device: n independent local NLPs (kinematic bicycle, N_horz 8, OBCA dual-distance constraints
+ * against the other vehicle's exchanged halfspaces), one wavefront each, one launch.
+ *
+ * recs: n x PIADMM_OBCA_REC fp64 records, each
+ *   init[5] | ref[8][5] (ref_traj[veh][t_step + k]) | A_o[7][4][2] | b_o[7][4] | lamb_ij_o[7][4]
+ *   (bar_state.A/b/lamb_ij of the OTHER vehicle) | lamb_bar[7][9] | Z_bar[7][9] (this vehicle's) |
+ *   rho, min_dis, max_x, max_y, r, q, prob (0/1: util.py:48-68 or :70-101 halfspaces),
+ *   max_sqp_iters | pad.
+ * out: n x PIADMM_OBCA_OUT fp64: X[8][5] | U[7][2] | Lambda[7][4] (local_solve's x_opt..steer_opt,
+ *   a_opt, steerate_opt, lambda_loc, :183-201) | multipliers y_a[7] y_b[7][2] y_n[7] y_x[7][5]
+ *   pi[7][5] y_u[14] y_l[28] | cost | pad.
+ * status3: n x 3 int32: PIADMM_OBCA_* status, SQP iterations, QP active-set steps.
+ * The NLP is the reference's as written; the solver is not IPOPT. */
+#define PIADMM_OBCA_REC 296
+#define PIADMM_OBCA_OUT 224
+#define PIADMM_OBCA_CONVERGED 0
+#define PIADMM_OBCA_MAX_ITER 1
+#define PIADMM_OBCA_QP_INFEASIBLE 2
+#define PIADMM_OBCA_LINESEARCH_FAIL 3
+#define PIADMM_OBCA_HESSIAN_FAIL 4
+
+typedef struct piadmm_obca_s* piadmm_obca_t;
+int32_t piadmm_obca_create(int32_t device, piadmm_obca_t* out);
+int32_t piadmm_obca_destroy(piadmm_obca_t h);
+const char* piadmm_obca_last_error(piadmm_obca_t h);
+/* upload + one launch + download (synchronous) */
+int32_t piadmm_obca_solve(piadmm_obca_t h, const double* recs, int32_t n, double* out, int32_t* status3);
+/* resident batch: upload once, launch (async on the handle's stream), time, download */
+int32_t piadmm_obca_upload(piadmm_obca_t h, const double* recs, int32_t n);
+int32_t piadmm_obca_run(piadmm_obca_t h, int32_t repeats);
+int32_t piadmm_obca_time(piadmm_obca_t h, int32_t repeats, float* ms_per_launch);
+int32_t piadmm_obca_download(piadmm_obca_t h, double* out, int32_t* status3, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -180,3 +180,60 @@ def test_global_pi_on_a_crossing(Solver):
     """Three vehicles, every pair a candidate: each agent's P sums two adaptive penalties."""
     cfg = config.casadi_old_pi(H=12, fixed_iters=1, max_outer=6)
     compare(Solver, cfg, scenario.crossing(3, 12, n_steps=8, seed=2), 5)
+
+
+@pytest.mark.parametrize("fixed", [0, 1])
+def test_component_split_over_workgroups(Solver, monkeypatch, fixed):
+    """A connected component larger than the workgroup block (term_global) spans several
+    workgroups: blocks of 4 agents, a pair owned by the block of its first agent, the X and Z
+    phases as separate launches.  A 24-vehicle chain (one component) equals the same job on one
+    workgroup (PIADMM_GRAPH_BLOCK=0) to 1e-10 and the oracle to 1e-8 -- steps with 1 to 23 outer
+    iterations, natural and fixed termination."""
+    H = 12
+    cfg = config.matlab_pi(H=H, term_global=1, fixed_iters=fixed, max_outer=30 if fixed else 100)
+    scn = scenario.crossing(24, H, n_steps=24, seed=1, pairs="chain")
+    s1 = Solver(cfg, scn)
+    monkeypatch.setenv("PIADMM_GRAPH_BLOCK", "0")
+    s2 = Solver(cfg, scn)
+    monkeypatch.delenv("PIADMM_GRAPH_BLOCK")
+    orc = O.Oracle(cfg, scn)
+    try:
+        assert s1.C == 6 and s2.C == 1 and s1.steps_per_launch() == 1
+        # (beyond step 12 the job's stop test becomes borderline -- rk within rounding of eps --
+        # and the blocks' summation order of the residual partials may resolve it differently)
+        for k in range(12):
+            r1, r2, ro = s1.mpc_step(), s2.mpc_step(), orc.mpc_step()
+            assert np.all(r1.status == 0)
+            assert r1.global_iters == r2.global_iters == int(ro.iters[0])
+            np.testing.assert_allclose(r1.xt, r2.xt, rtol=1e-10, atol=1e-10, err_msg=f"step {k}")
+            np.testing.assert_allclose(r1.u, r2.u, rtol=1e-10, atol=1e-10, err_msg=f"step {k}")
+            n = r1.global_iters
+            np.testing.assert_allclose(r1.global_resid[:n], r2.global_resid[:n], rtol=1e-9, atol=1e-12)
+            close(r1.xt, ro.xt)
+            close(r1.u, ro.u)
+    finally:
+        s1.close()
+        s2.close()
+
+
+def test_large_connected_graph_split(Solver, monkeypatch):
+    """256 agents in ONE connected chain at the bench horizon (H30, fixed 100 outer iterations,
+    the bench's mode): 64 workgroups of 4 agents equal the single-workgroup job to 1e-10."""
+    H = 30
+    cfg = config.matlab_pi(H=H, term_global=1, fixed_iters=1)
+    scn = scenario.crossing(256, H, n_steps=4, seed=2, pairs="chain")
+    s1 = Solver(cfg, scn)
+    monkeypatch.setenv("PIADMM_GRAPH_BLOCK", "0")
+    s2 = Solver(cfg, scn)
+    monkeypatch.delenv("PIADMM_GRAPH_BLOCK")
+    try:
+        assert s1.C == 64 and s2.C == 1
+        for k in range(2):
+            r1, r2 = s1.mpc_step(), s2.mpc_step()
+            assert np.all(r1.status == 0)
+            np.testing.assert_allclose(r1.xt, r2.xt, rtol=1e-10, atol=1e-10)
+            np.testing.assert_allclose(r1.u, r2.u, rtol=1e-10, atol=1e-10)
+            np.testing.assert_allclose(r1.global_resid, r2.global_resid, rtol=1e-9, atol=1e-12)
+    finally:
+        s1.close()
+        s2.close()
