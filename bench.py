@@ -17,6 +17,9 @@ intersection, inputs resident in HBM before the timed region):
                exchange buffer per outer iteration)
   --crossing   coupling-heavy: 64 four-vehicle all-pairs crossings (256 agents, 384 candidate
                pairs, H30) on the graph kernel -- pairs stay active for many outer iterations
+  --chain      one connected 1024-agent chain (one component split over workgroups)
+  --obca       the OBCA local subproblem: 4096 local NLPs of the overtaking
+               scenario per GPU, batched SQP, local NLP solves/s
 
 One "step" = one MPC step of the full loop (x-step QPs of all agents, collision graph, pair
 z-step QPs, PI + back-calculation dual update, residuals) plus propagation; the library's MPC
@@ -259,6 +262,107 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
                 kernel="pd::k_graph_step" if graph else "pd::k_mpc_step"), cnt
 
 
+def _obca_chunk(recs):
+    """worker: the NumPy SQP oracle on a chunk of records (CPU baseline of --obca)."""
+    sys.path.insert(0, ROOT)
+    from oracle import obca_oracle as O
+    n_conv = 0
+    for rec in recs:
+        p, opt = O.from_record(rec)
+        n_conv += int(O.solve_local(p, opt).status == O.CONVERGED)
+    return len(recs), n_conv
+
+
+def obca_cpu_baseline(recs, budget_s: float) -> dict:
+    """The OBCA oracle (oracle/obca_oracle.py: NumPy, the kernel's algorithm) over a process
+    pool on the host cores, on a bounded sample of the batch; run before the GPU is touched."""
+    import multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from oracle import hostinfo
+    hi = hostinfo.host_cpu()
+    cores = max(1, min(16, hi["threads"]))
+    # calibrate: one worker's rate on a few problems, then a sample sized for ~budget_s
+    t0 = time.perf_counter()
+    _obca_chunk(recs[:8])
+    per = (time.perf_counter() - t0) / 8
+    n = int(min(len(recs), max(cores * 4, budget_s * cores / max(per, 1e-6))))
+    sample = recs[:n]
+    chunks = [sample[i::cores] for i in range(cores)]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(cores) as pool:
+        t0 = time.perf_counter()
+        res = pool.map(_obca_chunk, chunks)
+        dt = time.perf_counter() - t0
+    done = sum(r[0] for r in res)
+    return {"value": done / dt, "unit": "local_nlp_solves/s", "cores": cores, "kind": "port",
+            "sample": f"first {done} problems of the batch (SQP oracle, NumPy fp64) over a {cores}-process pool, "
+                      f"{dt:.1f} s", "host": hostinfo.describe(hi),
+            "converged": sum(r[1] for r in res)}
+
+
+def main_obca(args, world, rank, local_rank):
+    """--obca: the OBCA local subproblem, a batch of local NLPs of the
+    two-vehicle overtaking scenario per GPU; one step = one batched SQP launch over the batch."""
+    from piadmm import obca
+    n = args.obca_batch
+    recs = obca.scenario_batch(n, seed=rank)
+    cpu = obca_cpu_baseline(recs, args.cpu_budget) if (rank == 0 and world == 1 and not args.no_cpu) else None
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from piadmm.solver import device_count
+    b = obca.OBCABatch(local_rank % max(device_count(), 1))
+    try:
+        b.upload(recs)
+        if args.warmup > 0:
+            b.time(args.warmup)
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        ev_ms = b.time(args.steps)           # hipEvents around the K launches on the handle's stream
+        wall = time.perf_counter() - t0
+        if dist is not None:
+            dist.barrier()
+        res = b.download(n)
+    finally:
+        b.close()
+    if dist is not None:
+        import torch
+        tt = torch.tensor([wall, ev_ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, ev_ms = float(tt[0]), float(tt[1])
+    K = args.steps
+    value = n * K * world / wall
+    bytes_launch = n * (obca.REC * 8 + obca.OUT * 8 + 12)
+    achieved = bytes_launch / (ev_ms / 1e3) / 1e9
+    line = {
+        "metric": "OBCA local NLP solves/s (batched SQP, two-vehicle overtaking, N_horz 8)",
+        "value": value, "unit": "local_nlp_solves/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
+        "ms_per_step": wall / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: local problems of the reference's two-vehicle overtaking scenario (every MPC step, "
+                "both vehicles, three bar_state variants; piadmm.obca.scenario_batch)",
+        "config": {"workload": f"{n} OBCA local NLPs per GPU (82 variables, 35 dynamics equalities, 7 x (5a, 5b, "
+                               f"norm)), one wavefront each, one launch per step",
+                   "problems_per_gpu": n, "converged": int((res.status == 0).sum()),
+                   "sqp_iters_mean": float(res.iters.mean()), "qp_steps_mean": float(res.qp_steps.mean()),
+                   "parallelism": f"independent problems per GPU ({world} GPU(s)), no collective"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": "obca::k_obca_sqp",
+                     "avg_launch_ms": ev_ms, "algorithmic_bytes_per_launch": bytes_launch,
+                     "note": "latency bound: 520 doubles of HBM traffic per problem, the SQP state stays in LDS; "
+                             "see DESIGN.md section 9"},
+        "cpu_baseline": cpu,
+    }
+    if cpu is not None:
+        line["speedup_vs_cpu_baseline"] = value / cpu["value"]
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -274,6 +378,8 @@ def main():
     g.add_argument("--strong", action="store_true", help="BASELINE configs[3]: 1024 agents sharded over N GPUs")
     g.add_argument("--crossing", action="store_true", help="coupling-heavy: 64 four-vehicle all-pairs crossings")
     g.add_argument("--chain", action="store_true", help="one connected 1024-agent chain (component over workgroups)")
+    g.add_argument("--obca", action="store_true", help="OBCA local subproblem: a batch of local NLPs (SQP)")
+    ap.add_argument("--obca-batch", type=int, default=4096, help="--obca: local problems per GPU")
     ap.add_argument("--split", choices=("components", "interleaved"), default="components",
                     help="--strong: whole tiles per rank, or every tile across two ranks (boundary exchange)")
     args = ap.parse_args()
@@ -287,6 +393,8 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.obca:
+        return main_obca(args, world, rank, local_rank)
     key = ("c2" if args.config2 else "c5" if args.config5 else "c4" if args.strong else "x4" if args.crossing
            else "ch" if args.chain else "c3")
     wl = WORKLOADS[key]

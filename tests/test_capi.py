@@ -23,7 +23,7 @@ def test_library_is_built_for_gfx950():
     lib = _lib.load()
     info = lib.piadmm_build_info().decode()
     assert "gfx950" in info
-    assert lib.piadmm_abi_version() == 4
+    assert lib.piadmm_abi_version() == 5
 
 
 def test_exports_every_declared_symbol():
