@@ -42,6 +42,8 @@ constexpr int ROWS_T = 21;            // per stage: state lo/hi x5, (5a) lo/hi, 
 constexpr int NROW = ROWS_T * NT + 2 * NUV;   // 175
 constexpr int REC = PIADMM_OBCA_REC, OUT = PIADMM_OBCA_OUT;
 constexpr int MAXACT = NZ;
+constexpr int NZP = NZ + 1;         // padded LDS row stride of the 28 x 28 matrices (odd: no bank conflicts
+                                     // when each lane walks its own row)
 
 // VehicleConfig (veh_config.py:7-27), OBCAOptimizer (optimizer.py:10-37)
 constexpr double LENGTH = 3.5, WIDTH = 2.0, LF = 1.5, LR = 1.0;
@@ -68,18 +70,20 @@ struct Ws {
   double gX[NH][NX], gL[NT][NL];
   double ga_v[NT], ga_g[NT][9], gb_v[NT][2], gb_J[NT][2][9], gn_v[NT], gn_g[NT][NL];
   double sv[NH][NX];
-  double K[NT][9][NZ];        // [dX_t; dLam_t] = K_t z + k0_t  (stage t = index + 1)
+  // [dX_t; dLam_t] = K_t z + k0_t with z = (dU, zeta) and K_t = [[T_t, 0], [-pmv_t (x) T_t[3], N_t]]
+  // (N_t = the null space of dm/dLam at zeta block t): K is never stored
+  double T[NT][NX][NUV];      // dX_t = T_t dU + s_t  (stage t = index + 1)
+  double pmv[NT][NL];         // P m_theta
   double k0[NT][9];
   double Pm[NT][NL][2];
-  double WK[9][NZ];
-  double Hq[NZ][NZ], gq[NZ];
-  double Hm[NZ][NZ];          // modified Hessian, then its Cholesky factor
-  double J[NZ][NZ], R[NZ][NZ];
+  double gq[NZ];
+  double Hm[NZ][NZP];         // modified Hessian, then its Cholesky factor; warm-solve scratch
+  double J[NZ][NZP];          // the condensed Hessian Hq until the QP, then J = L^-T
+  double R[NZ][NZP];          // W_t G_t during the assembly, Ga during the modification, then R
   double garow[NT][NZ], gnrow[NT][NZ];
   double din[NROW], uin[NROW];
-  double x[NZ], d[NZ], zd[NZ], rd[NZ], u[MAXACT + 1], dd[NZ];
+  double x[NZ], d[NZ], npv[NZ], u[MAXACT + 1], dd[NZ];
   double dX[NH][NX], dU[NT][NU], dL[NT][NL];
-  double red[64];
   int act[MAXACT + 1], pact[NROW];
   int nact, npact;
   int flag;
@@ -109,6 +113,21 @@ __device__ __forceinline__ void wargmin(double& v, int& i) {
 }
 
 #define SYNC() __syncthreads()
+
+// diagnostic build (-DPIADMM_STAMPS, libpiadmm_stamps.so): per-problem cycle sums of the SQP phases
+// and event counts, lane 0's clock; never the measured library
+constexpr int NSTAMP = 16;
+enum { ST_LIN, ST_COND, ST_HESS, ST_ROWS, ST_MOD, ST_GI, ST_REC, ST_LS, ST_INIT, ST_OUT,
+       ST_N_CHOL, ST_N_ADD, ST_N_DROP, ST_N_TRIAL, ST_N_SQP, ST_TOTAL };
+#ifdef PIADMM_STAMPS
+#define OST_DECL unsigned long long st_acc[NSTAMP] = {}; unsigned long long st_last = clock64(), st_t0 = st_last;
+#define OST(slot) do { if (threadIdx.x == 0) { unsigned long long _n = clock64(); st_acc[slot] += _n - st_last; st_last = _n; } } while (0)
+#define OCNT(slot, v) do { if (threadIdx.x == 0) st_acc[slot] += (v); } while (0)
+#else
+#define OST_DECL
+#define OST(slot) do { } while (0)
+#define OCNT(slot, v) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // geometry and dynamics (util.py:12-101, optimizer.py:75-100); same closed forms as the oracle
@@ -255,28 +274,29 @@ __device__ void cost_viol(Ws& S, const double (*X)[NX], const double (*U)[NU], c
 }
 
 // ---------------------------------------------------------------------------------------------
-// dense Cholesky of Hm in place (lower); returns true if positive definite
-// ---------------------------------------------------------------------------------------------
-__device__ bool chol(Ws& S) {
+// dense Cholesky (lower, in place) of the leading n x n block of M, lane i owning row i: per
+// column a pivot read, the column scaled by its owners, then each owner updates its own row
+// (the same operation order per entry as the right-looking form); false if a pivot is <= thr^2
+// (thr = 0: not positive).
+__device__ bool chol_n(double (*M)[NZP], int n, double thr) {
   int lane = threadIdx.x;
-  for (int j = 0; j < NZ; ++j) {
+  for (int j = 0; j < n; ++j) {
     SYNC();
-    double piv = S.Hm[j][j];
+    double piv = M[j][j];
     if (!(piv > 0.0)) { SYNC(); return false; }
     double l = sqrt(piv);
+    if (!(l > thr)) { SYNC(); return false; }
+    double lij = 0.0;
+    if (lane > j && lane < n) { lij = M[lane][j] / l; M[lane][j] = lij; }
+    if (lane == j) M[j][j] = l;
     SYNC();
-    if (lane == 0) S.Hm[j][j] = l;
-    if (lane > j && lane < NZ) S.Hm[lane][j] /= l;
-    SYNC();
-    // trailing update: rows i > j, cols k in (j, i]
-    for (int e = lane; e < NZ * NZ; e += 64) {
-      int i = e / NZ, k = e % NZ;
-      if (i > j && k > j && k <= i) S.Hm[i][k] -= S.Hm[i][j] * S.Hm[k][j];
-    }
+    if (lane > j && lane < n)
+      for (int k = j + 1; k <= lane; ++k) M[lane][k] -= lij * M[k][j];
   }
   SYNC();
   return true;
 }
+__device__ __forceinline__ bool chol(Ws& S) { return chol_n(S.Hm, NZ, 0.0); }
 
 // row c of the constraint matrix (C z >= din) dotted with v (28)
 __device__ double row_dot(const Ws& S, int c, const double* v) {
@@ -285,16 +305,24 @@ __device__ double row_dot(const Ws& S, int c, const double* v) {
     return (c & 1) ? -v[j] : v[j];
   }
   int ti = c / ROWS_T, r = c % ROWS_T;
-  const double* a;
-  double sgn = 1.0;
-  if (r < 10) { a = S.K[ti][r >> 1]; sgn = (r & 1) ? -1.0 : 1.0; }
-  else if (r == 10) a = S.garow[ti];
-  else if (r == 11) { a = S.garow[ti]; sgn = -1.0; }
-  else if (r == 12) { a = S.gnrow[ti]; sgn = -1.0; }
-  else { int q = r - 13; a = S.K[ti][5 + (q >> 1)]; sgn = (q & 1) ? -1.0 : 1.0; }
+  if (r < 10) {                       // state rows: T_t only
+    const double* a = S.T[ti][r >> 1];
+    double s = 0.0;
+    for (int k = 0; k < NUV; ++k) s += a[k] * v[k];
+    return (r & 1) ? -s : s;
+  }
+  if (r >= 13) {                      // Lambda rows: -pmv T_t[3] dU + N zeta_t
+    int q = r - 13, j = q >> 1;
+    const double* a = S.T[ti][3];
+    double s = 0.0;
+    for (int k = 0; k < NUV; ++k) s += a[k] * v[k];
+    s = -S.pmv[ti][j] * s + v[NUV + 2 * ti + (j & 1)];
+    return (q & 1) ? -s : s;
+  }
+  const double* a = (r == 12) ? S.gnrow[ti] : S.garow[ti];
   double s = 0.0;
   for (int k = 0; k < NZ; ++k) s += a[k] * v[k];
-  return sgn * s;
+  return (r == 10) ? s : -s;
 }
 __device__ double row_elem(const Ws& S, int c, int k) {
   if (c >= ROWS_T * NT) {
@@ -302,38 +330,52 @@ __device__ double row_elem(const Ws& S, int c, int k) {
     return (k == j) ? ((c & 1) ? -1.0 : 1.0) : 0.0;
   }
   int ti = c / ROWS_T, r = c % ROWS_T;
-  if (r < 10) return ((r & 1) ? -1.0 : 1.0) * S.K[ti][r >> 1][k];
+  if (r < 10) return (k < NUV) ? ((r & 1) ? -1.0 : 1.0) * S.T[ti][r >> 1][k] : 0.0;
   if (r == 10) return S.garow[ti][k];
   if (r == 11) return -S.garow[ti][k];
   if (r == 12) return -S.gnrow[ti][k];
-  int q = r - 13;
-  return ((q & 1) ? -1.0 : 1.0) * S.K[ti][5 + (q >> 1)][k];
+  int q = r - 13, j = q >> 1;
+  double e = (k < NUV) ? -S.pmv[ti][j] * S.T[ti][3][k] : ((k == NUV + 2 * ti + (j & 1)) ? 1.0 : 0.0);
+  return (q & 1) ? -e : e;
+}
+
+// the dU part of K_t, row i (i < 9), column a < NUV
+__device__ __forceinline__ double gval(const Ws& S, int ti, int i, int a) {
+  return (i < 5) ? S.T[ti][i][a] : -S.pmv[ti][i - 5] * S.T[ti][3][a];
+}
+__device__ __forceinline__ double wval(const Ws& S, int t, int i, int j) {
+  return (i < 5) ? (j < 5 ? S.Wxx[t][i][j] : S.Wxl[t][i][j - 5]) : (j < 5 ? S.Wxl[t][j][i - 5] : S.Wll[t][i - 5][j - 5]);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Goldfarb-Idnani on min 1/2 z'Hz + gq'z, C z >= din (no equalities); H = L L' in S.Hm.
 // Returns 0 ok, 2 infeasible, 1 step limit; S.x = solution, S.uin = multipliers (dense).
 // ---------------------------------------------------------------------------------------------
+// Lane ownership inside the active-set updates: lane i owns row i of J (every Givens rotation of a
+// J column pair is row-local), lane c owns column c of R during a drop's rotations; rotation
+// parameters are uniform (computed by every lane from LDS / a shuffle), so the rotation chains run
+// without barriers.
 __device__ void gi_drop(Ws& S, int k) {
   int lane = threadIdx.x;
-  int q = S.nact;
   SYNC();
-  // remove column k of R (shift left)
+  int q = S.nact;
+  // remove column k of R (row-owned shift)
   if (lane < NZ) {
     for (int j = k; j < q - 1; ++j) S.R[lane][j] = S.R[lane][j + 1];
     S.R[lane][q - 1] = 0.0;
   }
   SYNC();
   for (int j = k; j < q - 1; ++j) {
-    double a = S.R[j][j], b = S.R[j + 1][j];
+    // column j is lane j's: its (R[j][j], R[j+1][j]) after the previous rotations
+    double aj = (lane < NZ) ? S.R[j][lane] : 0.0;
+    double bj = (lane < NZ) ? S.R[j + 1][lane] : 0.0;
+    double a = __shfl(aj, j, 64), b = __shfl(bj, j, 64);
     double h = hypot(a, b);
-    SYNC();
     if (h != 0.0) {
       double cs = a / h, sn = b / h;
       if (lane >= j && lane < q - 1) {
-        double rj = S.R[j][lane], rj1 = S.R[j + 1][lane];
-        S.R[j][lane] = cs * rj + sn * rj1;
-        S.R[j + 1][lane] = -sn * rj + cs * rj1;
+        S.R[j][lane] = cs * aj + sn * bj;
+        S.R[j + 1][lane] = -sn * aj + cs * bj;
       }
       if (lane < NZ) {
         double Jj = S.J[lane][j], Jj1 = S.J[lane][j + 1];
@@ -341,8 +383,8 @@ __device__ void gi_drop(Ws& S, int k) {
         S.J[lane][j + 1] = -sn * Jj + cs * Jj1;
       }
     }
-    SYNC();
   }
+  SYNC();
   if (lane == 0) {
     for (int j = k; j < q - 1; ++j) { S.act[j] = S.act[j + 1]; S.u[j] = S.u[j + 1]; }
     S.nact = q - 1;
@@ -354,88 +396,183 @@ __device__ void gi_drop(Ws& S, int k) {
 __device__ int gi_add(Ws& S, int p, int& steps) {
   int lane = threadIdx.x;
   double up = 0.0;
-  double bp = S.din[p];
+  const double bp = S.din[p];
+  SYNC();
+  if (lane < NZ) S.npv[lane] = row_elem(S, p, lane);
+  SYNC();
+  const double npl = (lane < NZ) ? S.npv[lane] : 0.0;
   while (true) {
     if (++steps > 500) return -1;
-    int q = S.nact;
+    const int q = S.nact;
+    // d = J' n_p (lane j)
+    double dj = 0.0;
+    if (lane < NZ)
+      for (int i = 0; i < NZ; ++i) dj += S.J[i][lane] * S.npv[i];
+    if (lane < NZ) S.d[lane] = dj;
     SYNC();
-    // d = J' n_p
-    if (lane < NZ) {
-      double s = 0.0;
-      for (int i = 0; i < NZ; ++i) s += S.J[i][lane] * row_elem(S, p, i);
-      S.d[lane] = s;
-      S.dd[lane] = s;
-    }
-    SYNC();
-    // z = J[:, q:] d[q:]
-    if (lane < NZ) {
-      double s = 0.0;
-      for (int j = q; j < NZ; ++j) s += S.J[lane][j] * S.d[j];
-      S.zd[lane] = s;
-    }
-    // r = R^-1 d[:q] (back substitution)
+    // z = J[:, q:] d[q:] (lane i)
+    double zi = 0.0;
+    if (lane < NZ)
+      for (int j = q; j < NZ; ++j) zi += S.J[lane][j] * S.d[j];
+    // r = R^-1 d[:q]: back substitution on the lanes' registers (lane k ends with r_k)
+    double ddk = (lane < q) ? dj : 0.0, rk = 0.0;
     for (int j = q - 1; j >= 0; --j) {
-      SYNC();
-      double rj = S.dd[j] / S.R[j][j];
-      SYNC();
-      if (lane == 0) S.rd[j] = rj;
-      if (lane < j) S.dd[lane] -= S.R[lane][j] * rj;
+      double rj = __shfl(ddk, j, 64) / S.R[j][j];
+      if (lane == j) rk = rj;
+      if (lane < j) ddk -= S.R[lane][j] * rj;
     }
-    SYNC();
     // partial step t1 over active rows with r_k > 1e-13 max(1, max|r|)
-    double rmax = 1.0;
-    {
-      double v = (lane < q) ? fabs(S.rd[lane]) : 0.0;
-      rmax = fmax(1.0, wmax(v));
-    }
+    const double rmax = fmax(1.0, wmax(lane < q ? fabs(rk) : 0.0));
     double t1v = INFINITY;
     int l = -1;
-    if (lane < q && S.rd[lane] > 1e-13 * rmax) { t1v = S.u[lane] / S.rd[lane]; l = lane; }
+    if (lane < q && rk > 1e-13 * rmax) { t1v = S.u[lane] / rk; l = lane; }
     wargmin(t1v, l);
-    double t1 = (l >= 0) ? t1v : INFINITY;
+    const double t1 = (l >= 0) ? t1v : INFINITY;
     // full step t2
-    double zn = wsum(lane < NZ ? S.zd[lane] * row_elem(S, p, lane) : 0.0);
-    double dd2 = wsum(lane < NZ ? S.d[lane] * S.d[lane] : 0.0);
-    double sx = row_dot(S, p, S.x) - bp;
-    double t2 = (zn > 1e-12 * dd2) ? -sx / zn : INFINITY;
-    double t = fmin(t1, t2);
+    const double xl = (lane < NZ) ? S.x[lane] : 0.0;
+    const double zn = wsum(zi * npl);
+    const double dd2 = wsum(dj * dj);
+    const double sx = wsum(npl * xl) - bp;
+    const double t2 = (zn > 1e-12 * dd2) ? -sx / zn : INFINITY;
+    const double t = fmin(t1, t2);
     if (t == INFINITY) return 0;
     if (t2 == INFINITY) {
-      SYNC();
-      if (lane < q) S.u[lane] -= t * S.rd[lane];
+      if (lane < q) S.u[lane] -= t * rk;
       up += t;
-      SYNC();
       gi_drop(S, l);
       continue;
     }
-    SYNC();
-    if (lane < NZ) S.x[lane] += t * S.zd[lane];
-    if (lane < q) S.u[lane] -= t * S.rd[lane];
+    if (lane < NZ) S.x[lane] = xl + t * zi;
+    if (lane < q) S.u[lane] -= t * rk;
     up += t;
-    SYNC();
     if (t == t2) {
-      for (int j = NZ - 1; j > q; --j) {
-        double a = S.d[j - 1], b = S.d[j];
-        SYNC();
-        if (b != 0.0) {
-          double h = hypot(a, b);
-          double cs = a / h, sn = b / h;
+      // one Householder reflection of J[:, q:] zeroing d[q+1..] (uniform v, each lane its own row)
+      double alpha = S.d[q];
+      if (q < NZ - 1) {
+        double ss = 0.0;
+        for (int j = q + 1; j < NZ; ++j) ss += S.d[j] * S.d[j];
+        if (ss > 0.0) {
+          const double a0 = S.d[q];
+          const double sig = sqrt(a0 * a0 + ss);
+          alpha = (a0 > 0.0) ? -sig : sig;
+          const double v0 = a0 - alpha;
+          const double beta = 1.0 / (sig * (sig + fabs(a0)));     // 2 / v'v
           if (lane < NZ) {
-            double Jj = S.J[lane][j - 1], Jj1 = S.J[lane][j];
-            S.J[lane][j - 1] = cs * Jj + sn * Jj1;
-            S.J[lane][j] = -sn * Jj + cs * Jj1;
+            double sv = S.J[lane][q] * v0;
+            for (int j = q + 1; j < NZ; ++j) sv += S.J[lane][j] * S.d[j];
+            sv *= beta;
+            S.J[lane][q] -= sv * v0;
+            for (int j = q + 1; j < NZ; ++j) S.J[lane][j] -= sv * S.d[j];
           }
-          if (lane == 0) { S.d[j - 1] = h; S.d[j] = 0.0; }
         }
-        SYNC();
       }
-      if (lane <= q) S.R[lane][q] = S.d[lane];
+      if (lane < q) S.R[lane][q] = S.d[lane];
+      if (lane == q) S.R[q][q] = alpha;
+      SYNC();
       if (lane == 0) { S.act[q] = p; S.u[q] = up; S.nact = q + 1; }
       SYNC();
       return 1;
     }
     gi_drop(S, l);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// warm equality solve (oracle warm_eqp): the previous SQP iteration's active rows W as the QP's
+// active set.  Y = L^-1 A_W' (= J' A_W'), S = Y'Y, lam = S^-1 (d_W + Y'y0), z = L^-T (Y lam - y0),
+// two refinement steps on d_W - A_W z; certified iff lam >= 0 and every row holds -- then z is
+// THE minimiser of the strictly convex QP.  Scratch: A_W and then S in Hm (the factor of H is
+// no longer needed once J is formed), Y in R (zeroed again before a fallback).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double s_solve(Ws& S, int m, double v) {
+  // S.Hm holds Ls (m x m lower); lane k < m carries component k of the right-hand side
+  int lane = threadIdx.x;
+  for (int j = 0; j < m; ++j) {
+    double yj = __shfl(v, j, 64) / S.Hm[j][j];
+    if (lane == j) v = yj;
+    if (lane > j && lane < m) v -= S.Hm[lane][j] * yj;
+  }
+  for (int j = m - 1; j >= 0; --j) {
+    double xj = __shfl(v, j, 64) / S.Hm[j][j];
+    if (lane == j) v = xj;
+    if (lane < j) v -= S.Hm[j][lane] * xj;
+  }
+  return v;
+}
+
+__device__ bool warm_eqp(Ws& S) {
+  const int lane = threadIdx.x;
+  const int m = S.npact;
+  for (int e = lane; e < m * NZ; e += 64) S.Hm[e / NZ][e % NZ] = row_elem(S, S.pact[e / NZ], e % NZ);
+  SYNC();
+  for (int e = lane; e < NZ * m; e += 64) {
+    int i = e / m, k = e % m;
+    double s = 0.0;
+    for (int j = 0; j < NZ; ++j) s += S.J[j][i] * S.Hm[k][j];
+    S.R[i][k] = s;
+  }
+  SYNC();
+  for (int e = lane; e < m * m; e += 64) {
+    int k = e / m, l = e % m;
+    double s = 0.0;
+    for (int i = 0; i < NZ; ++i) s += S.R[i][k] * S.R[i][l];
+    S.Hm[k][l] = s;
+  }
+  SYNC();
+  const double dmax = wmax(lane < m ? S.Hm[lane][lane] : 0.0);
+  if (!chol_n(S.Hm, m, 1e-7 * sqrt(dmax))) return false;
+  // lam
+  double lam = 0.0;
+  if (lane < m) {
+    lam = S.din[S.pact[lane]];
+    for (int i = 0; i < NZ; ++i) lam += S.R[i][lane] * S.dd[i];
+  }
+  lam = s_solve(S, m, lam);
+  // w = Y lam - y0  (lane i), kept in S.d
+  double wi = 0.0;
+  for (int k = 0; k < m; ++k) {
+    double lk = __shfl(lam, k, 64);
+    if (lane < NZ) wi += S.R[lane][k] * lk;
+  }
+  if (lane < NZ) { wi -= S.dd[lane]; S.d[lane] = wi; }
+  for (int rep = 0; rep < 2; ++rep) {
+    SYNC();
+    if (lane < NZ) {
+      double z = 0.0;
+      for (int j = 0; j < NZ; ++j) z += S.J[lane][j] * S.d[j];
+      S.x[lane] = z;
+    }
+    SYNC();
+    double r = (lane < m) ? S.din[S.pact[lane]] - row_dot(S, S.pact[lane], S.x) : 0.0;
+    double dl = s_solve(S, m, r);
+    if (lane < m) lam += dl;
+    for (int k = 0; k < m; ++k) {
+      double dk = __shfl(dl, k, 64);
+      if (lane < NZ) wi += S.R[lane][k] * dk;
+    }
+    SYNC();
+    if (lane < NZ) S.d[lane] = wi;
+  }
+  const double lmax = fmax(1.0, wmax(lane < m ? fabs(lam) : 0.0));
+  const int neg = __any(lane < m && lam < -1e-12 * lmax);
+  if (neg) { SYNC(); return false; }
+  SYNC();
+  if (lane < NZ) {
+    double z = 0.0;
+    for (int j = 0; j < NZ; ++j) z += S.J[lane][j] * S.d[j];
+    S.x[lane] = z;
+  }
+  SYNC();
+  int bad = 0;
+  for (int c = lane; c < NROW; c += 64) {
+    double sc = row_dot(S, c, S.x) - S.din[c];
+    bad |= (sc < -1e-11 * (1.0 + fabs(S.din[c])));
+  }
+  if (__any(bad)) { SYNC(); return false; }
+  if (lane < m) { S.act[lane] = S.pact[lane]; S.u[lane] = fmax(lam, 0.0); }
+  if (lane == 0) S.nact = m;
+  SYNC();
+  return true;
 }
 
 __device__ int gi_solve(Ws& S, int& steps) {
@@ -460,12 +597,15 @@ __device__ int gi_solve(Ws& S, int& steps) {
     S.dd[lane] = s;
   }
   SYNC();
+  if (S.npact > 0 && warm_eqp(S)) {
+    steps = 0;
+  } else {
   if (lane < NZ) {
     double s = 0.0;
     for (int j = 0; j < NZ; ++j) s += S.J[lane][j] * S.dd[j];
     S.x[lane] = -s;
   }
-  for (int e = lane; e < NZ * NZ; e += 64) (&S.R[0][0])[e] = 0.0;
+  for (int e = lane; e < NZ * NZ; e += 64) S.R[e / NZ][e % NZ] = 0.0;
   if (lane == 0) S.nact = 0;
   SYNC();
   while (true) {
@@ -481,6 +621,7 @@ __device__ int gi_solve(Ws& S, int& steps) {
     if (ok < 0) return 1;
     if (ok == 0) return 2;
   }
+  }
   SYNC();
   for (int c = lane; c < NROW; c += 64) S.uin[c] = 0.0;
   SYNC();
@@ -494,8 +635,10 @@ __device__ int gi_solve(Ws& S, int& steps) {
 // the SQP
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs, int n,
-                                                 double* __restrict__ out, int* __restrict__ ist) {
+                                                 double* __restrict__ out, int* __restrict__ ist,
+                                                 unsigned long long* __restrict__ stamps) {
   __shared__ Ws S;
+  OST_DECL
   const int lane = threadIdx.x;
   const int pb = blockIdx.x;
   if (pb >= n) return;
@@ -543,17 +686,9 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
   for (int e = lane; e < NT * NL; e += 64) (&S.yl[0][0])[e] = 0.0;
   if (lane < NT) { S.ya[lane] = 0.0; S.yn[lane] = 0.0; S.yb[lane][0] = S.yb[lane][1] = 0.0; }
   if (lane < NUV) S.yu[lane] = 0.0;
-  // constant parts of K: X rows' zeta columns 0; Lambda rows' zeta columns = N at block t-1
-  for (int e = lane; e < NT * 9 * NZ; e += 64) (&S.K[0][0][0])[e] = 0.0;
-  SYNC();
-  if (lane < NT) {
-    int ti = lane;
-    const double NN[4][2] = {{1, 0}, {0, 1}, {1, 0}, {0, 1}};
-    for (int i = 0; i < 4; ++i)
-      for (int cc = 0; cc < 2; ++cc) S.K[ti][5 + i][NUV + 2 * ti + cc] = NN[i][cc];
-  }
   SYNC();
 
+  OST(ST_INIT);
   double mu = 0.0;
   int qp_total = 0;
   int status = PIADMM_OBCA_MAX_ITER;
@@ -621,19 +756,20 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) S.Wll[t][i][j] = (i == j ? S.rho : 0.0) + H[5 + i][5 + j] - yn * Hn[i][j];
     }
-    // ---- condense: K_t[0:5][0:14] = T_t, s_t ----
+    OST(ST_LIN);
+    // ---- condense: T_t, s_t ----
     if (lane < NX) S.sv[0][lane] = S.init[lane] - S.X[0][lane];
     SYNC();
     for (int k = 0; k < NT; ++k) {
-      // T_{k+1} = A_k T_k + B_k E_k  (T_0 = 0); K index k holds T_{k+1}
+      // T_{k+1} = A_k T_k + B_k E_k  (T_0 = 0); index k holds T_{k+1}
       for (int e = lane; e < NX * NUV; e += 64) {
         int i = e / NUV, j = e % NUV;
         double s = 0.0;
         if (k > 0)
-          for (int m = 0; m < NX; ++m) s += S.A[k][i][m] * S.K[k - 1][m][j];
+          for (int m = 0; m < NX; ++m) s += S.A[k][i][m] * S.T[k - 1][m][j];
         if (j == 2 * k && i == 2) s += DT;
         if (j == 2 * k + 1 && i == 4) s += DT;
-        S.K[k][i][j] = s;
+        S.T[k][i][j] = s;
       }
       if (lane < NX) {
         double s = 0.0;
@@ -642,7 +778,7 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       }
       SYNC();
     }
-    // ---- (5b) elimination: Lambda rows of K and k0 ----
+    // ---- (5b) elimination: P m_theta and k0 ----
     if (lane < NT) {
       int ti = lane;
       double P[4][2], pm[4], pr[4];
@@ -659,53 +795,63 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       }
       for (int i = 0; i < 5; ++i) S.k0[ti][i] = S.sv[ti + 1][i];
       for (int i = 0; i < 4; ++i) S.k0[ti][5 + i] = pr[i];
-      for (int i = 0; i < 4; ++i) S.red[ti * 4 + i] = pm[i];   // P m_theta, used below
+      for (int i = 0; i < 4; ++i) S.pmv[ti][i] = pm[i];
     }
     SYNC();
-    for (int e = lane; e < NT * 4 * NUV; e += 64) {
-      int ti = e / (4 * NUV), rem = e % (4 * NUV), i = rem / NUV, j = rem % NUV;
-      S.K[ti][5 + i][j] = -S.red[ti * 4 + i] * S.K[ti][3][j];
-    }
-    // ---- condensed Hessian and gradient ----
+    OST(ST_COND);
+    // ---- condensed Hessian and gradient by blocks: UU += G_t' W_t G_t, U zeta_t += G_t' W_t N,
+    //      zeta_t zeta_t += N' W_ll N; gq += K_t' (W_t k0_t + g_t) ----
     for (int e = lane; e < NZ * NZ; e += 64) {
       int a = e / NZ, b = e % NZ;
-      (&S.Hq[0][0])[e] = (a == b && a < NUV) ? 2 * S.rr : 0.0;
+      S.J[a][b] = (a == b && a < NUV) ? 2 * S.rr : 0.0;
     }
     if (lane < NZ) S.gq[lane] = lane < NUV ? 2 * S.rr * (&S.U[0][0])[lane] : 0.0;
     SYNC();
     for (int ti = 0; ti < NT; ++ti) {
-      int t = ti + 1;
-      // WK = W_t K_t (9 x 28)
-      for (int e = lane; e < 9 * NZ; e += 64) {
-        int i = e / NZ, a = e % NZ;
-        double s = 0.0;
-        for (int j = 0; j < 9; ++j) {
-          double wij = (i < 5) ? (j < 5 ? S.Wxx[t][i][j] : S.Wxl[t][i][j - 5])
-                               : (j < 5 ? S.Wxl[t][j][i - 5] : S.Wll[t][i - 5][j - 5]);
-          s += wij * S.K[ti][j][a];
+      const int t = ti + 1;
+      // R[i][0..13] = (W_t G_t)[i][:], R[i][14 + c] = (W_t N)[i][c]; dd[i] = (W_t k0_t + g_t)[i]
+      for (int e = lane; e < 9 * 16; e += 64) {
+        int i = e >> 4, a = e & 15;
+        double v = 0.0;
+        if (a < NUV) {
+          for (int j = 0; j < 9; ++j) v += wval(S, t, i, j) * gval(S, ti, j, a);
+        } else {
+          int c = a - NUV;
+          v = wval(S, t, i, 5 + c) + wval(S, t, i, 7 + c);
         }
-        S.WK[i][a] = s;
+        S.R[i][a] = v;
+      }
+      if (lane >= 48 && lane < 57) {
+        int i = lane - 48;
+        double v = (i < 5) ? S.gX[t][i] : S.gL[ti][i - 5];
+        for (int j = 0; j < 9; ++j) v += wval(S, t, i, j) * S.k0[ti][j];
+        S.dd[i] = v;
       }
       SYNC();
-      for (int e = lane; e < NZ * NZ; e += 64) {
-        int a = e / NZ, b = e % NZ;
-        double s = 0.0;
-        for (int i = 0; i < 9; ++i) s += S.K[ti][i][a] * S.WK[i][b];
-        S.Hq[a][b] += s;
+      for (int e = lane; e < NUV * NUV; e += 64) {
+        int a = e / NUV, b = e % NUV;
+        double v = 0.0;
+        for (int i = 0; i < 9; ++i) v += gval(S, ti, i, a) * S.R[i][b];
+        S.J[a][b] += v;
       }
-      if (lane < NZ) {
-        // gq += K_t' (W_t k0_t + g_t)
-        double s = 0.0;
-        for (int i = 0; i < 9; ++i) {
-          double v = (i < 5) ? S.gX[t][i] : S.gL[ti][i - 5];
-          for (int j = 0; j < 9; ++j) {
-            double wij = (i < 5) ? (j < 5 ? S.Wxx[t][i][j] : S.Wxl[t][i][j - 5])
-                                 : (j < 5 ? S.Wxl[t][j][i - 5] : S.Wll[t][i - 5][j - 5]);
-            v += wij * S.k0[ti][j];
-          }
-          s += S.K[ti][i][lane] * v;
-        }
-        S.gq[lane] += s;
+      if (lane < 2 * NUV) {
+        int a = lane >> 1, c = lane & 1;
+        double v = 0.0;
+        for (int i = 0; i < 9; ++i) v += gval(S, ti, i, a) * S.R[i][NUV + c];
+        S.J[a][NUV + 2 * ti + c] += v;
+        S.J[NUV + 2 * ti + c][a] += v;
+      } else if (lane < 2 * NUV + 4) {
+        int c1 = (lane - 2 * NUV) >> 1, c2 = (lane - 2 * NUV) & 1;
+        S.J[NUV + 2 * ti + c1][NUV + 2 * ti + c2] += S.R[5 + c1][NUV + c2] + S.R[7 + c1][NUV + c2];
+      }
+      if (lane >= 32 && lane < 32 + NUV) {
+        int a = lane - 32;
+        double v = 0.0;
+        for (int i = 0; i < 9; ++i) v += gval(S, ti, i, a) * S.dd[i];
+        S.gq[a] += v;
+      } else if (lane >= 48 && lane < 50) {
+        int c = lane - 48;
+        S.gq[NUV + 2 * ti + c] += S.dd[5 + c] + S.dd[7 + c];
       }
       SYNC();
     }
@@ -713,20 +859,26 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
     for (int e = lane; e < NZ * NZ; e += 64) {
       int a = e / NZ, b = e % NZ;
       if (a < b) {
-        double v = 0.5 * (S.Hq[a][b] + S.Hq[b][a]);
-        S.Hq[a][b] = v;
-        S.Hq[b][a] = v;
+        double v = 0.5 * (S.J[a][b] + S.J[b][a]);
+        S.J[a][b] = v;
+        S.J[b][a] = v;
       }
     }
+    OST(ST_HESS);
     // ---- constraint rows ----
     for (int e = lane; e < NT * NZ; e += 64) {
       int ti = e / NZ, a = e % NZ;
-      double s = 0.0;
-      for (int i = 0; i < 9; ++i) s += S.ga_g[ti][i] * S.K[ti][i][a];
-      S.garow[ti][a] = s;
-      double g = 0.0;
-      for (int j = 0; j < 4; ++j) g += S.gn_g[ti][j] * S.K[ti][5 + j][a];
-      S.gnrow[ti][a] = g;
+      double sa = 0.0, sn = 0.0;
+      if (a < NUV) {
+        for (int i = 0; i < 9; ++i) sa += S.ga_g[ti][i] * gval(S, ti, i, a);
+        for (int j = 0; j < 4; ++j) sn += S.gn_g[ti][j] * gval(S, ti, 5 + j, a);
+      } else if (((a - NUV) >> 1) == ti) {
+        int c = (a - NUV) & 1;
+        sa = S.ga_g[ti][5 + c] + S.ga_g[ti][7 + c];
+        sn = S.gn_g[ti][c] + S.gn_g[ti][2 + c];
+      }
+      S.garow[ti][a] = sa;
+      S.gnrow[ti][a] = sn;
     }
     for (int c = lane; c < NROW; c += 64) {
       double dv;
@@ -760,19 +912,24 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       S.din[c] = dv;
     }
     SYNC();
+    OST(ST_ROWS);
     // ---- Hessian modification ----
-    for (int e = lane; e < NZ * NZ; e += 64) (&S.Hm[0][0])[e] = (&S.Hq[0][0])[e];
+    for (int e = lane; e < NZ * NZ; e += 64) S.Hm[e / NZ][e % NZ] = S.J[e / NZ][e % NZ];
     bool pd = chol(S);
+    OCNT(ST_N_CHOL, 1);
     if (!pd && S.npact > 0) {
-      // Ga = sum over previous active rows of a a' / |a|^2  (in R, free until the QP)
-      for (int e = lane; e < NZ * NZ; e += 64) (&S.R[0][0])[e] = 0.0;
+      // sigma/2 sum_k (a_k'z - d_k)^2 over the previous QP's active rows, normalised (zero and
+      // stationary on their face: a QP solution keeping them active is unchanged):
+      // Ga = sum a a' (in R, free until the QP), gav = sum d a (in npv)
+      for (int e = lane; e < NZ * NZ; e += 64) S.R[e / NZ][e % NZ] = 0.0;
+      if (lane < NZ) S.npv[lane] = 0.0;
       SYNC();
       for (int k = 0; k < S.npact; ++k) {
         int c = S.pact[k];
         double a = (lane < NZ) ? row_elem(S, c, lane) : 0.0;
         double nn = wsum(a * a);
         double inv = 1.0 / fmax(sqrt(nn), 1e-300);
-        if (lane < NZ) S.dd[lane] = a * inv;
+        if (lane < NZ) { S.dd[lane] = a * inv; S.npv[lane] += (S.din[c] * inv) * (a * inv); }
         SYNC();
         for (int e = lane; e < NZ * NZ; e += 64) {
           int i = e / NZ, j = e % NZ;
@@ -780,22 +937,24 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
         }
         SYNC();
       }
-      double hm = wmax(lane < NZ ? fabs(S.Hq[lane][lane]) : 0.0);
+      double hm = wmax(lane < NZ ? fabs(S.J[lane][lane]) : 0.0);
       double sig = 1e-4 * hm;
       for (int a = 0; a < 8; ++a) {
-        for (int e = lane; e < NZ * NZ; e += 64) (&S.Hm[0][0])[e] = (&S.Hq[0][0])[e] + sig * (&S.R[0][0])[e];
+        for (int e = lane; e < NZ * NZ; e += 64) S.Hm[e / NZ][e % NZ] = S.J[e / NZ][e % NZ] + sig * S.R[e / NZ][e % NZ];
         pd = chol(S);
+        OCNT(ST_N_CHOL, 1);
         if (pd) break;
         sig *= 10.0;
       }
       if (!pd) {
         // H0 = Hq + sig_last Ga (sig was multiplied once more after the last try)
         sig /= 10.0;
-        for (int e = lane; e < NZ * NZ; e += 64) (&S.R[0][0])[e] = (&S.Hq[0][0])[e] + sig * (&S.R[0][0])[e];
-        SYNC();
+        for (int e = lane; e < NZ * NZ; e += 64) S.R[e / NZ][e % NZ] = S.J[e / NZ][e % NZ] + sig * S.R[e / NZ][e % NZ];
       }
+      if (lane < NZ) S.gq[lane] -= sig * S.npv[lane];
+      SYNC();
     } else if (!pd) {
-      for (int e = lane; e < NZ * NZ; e += 64) (&S.R[0][0])[e] = (&S.Hq[0][0])[e];
+      for (int e = lane; e < NZ * NZ; e += 64) S.R[e / NZ][e % NZ] = S.J[e / NZ][e % NZ];
       SYNC();
     }
     if (!pd) {
@@ -805,18 +964,23 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
         tau = (tau == 0.0) ? 1e-6 : tau * 10.0;
         for (int e = lane; e < NZ * NZ; e += 64) {
           int i = e / NZ, j = e % NZ;
-          double h = (&S.R[0][0])[e];
-          (&S.Hm[0][0])[e] = (i == j) ? h + tau * fmax(fabs(h), 1e-12) : h;
+          double h = S.R[i][j];
+          S.Hm[i][j] = (i == j) ? h + tau * fmax(fabs(h), 1e-12) : h;
         }
         pd = chol(S);
+        OCNT(ST_N_CHOL, 1);
         if (pd) break;
       }
       if (!pd) { status = PIADMM_OBCA_HESSIAN_FAIL; break; }
     }
+    OST(ST_MOD);
     // ---- QP ----
     int steps = 0;
     int qst = gi_solve(S, steps);
     qp_total += steps;
+    OCNT(ST_N_ADD, S.nact);
+    OST(ST_GI);
+    OCNT(ST_N_SQP, 1);
     if (qst != 0) { status = (qst == 2) ? PIADMM_OBCA_QP_INFEASIBLE : PIADMM_OBCA_MAX_ITER; break; }
     if (lane == 0) {
       int m = 0;
@@ -829,10 +993,11 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
     if (lane < NX) S.dX[0][lane] = S.sv[0][lane];
     for (int e = lane; e < NT * 9; e += 64) {
       int ti = e / 9, i = e % 9;
-      double s = S.k0[ti][i];
-      for (int a = 0; a < NZ; ++a) s += S.K[ti][i][a] * S.x[a];
-      if (i < 5) S.dX[ti + 1][i] = s;
-      else S.dL[ti][i - 5] = s;
+      int ir = (i < 5) ? i : 3;
+      double s = 0.0;
+      for (int a = 0; a < NUV; ++a) s += S.T[ti][ir][a] * S.x[a];
+      if (i < 5) S.dX[ti + 1][i] = S.k0[ti][i] + s;
+      else S.dL[ti][i - 5] = S.k0[ti][i] - S.pmv[ti][i - 5] * s + S.x[NUV + 2 * ti + ((i - 5) & 1)];
     }
     // ---- QP multipliers -> NLP multipliers ----
     if (lane < NT) {
@@ -877,6 +1042,7 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       }
       SYNC();
     }
+    OST(ST_REC);
     // ---- convergence test ----
     double f0, viol;
     cost_viol(S, S.X, S.U, S.L, f0, viol);
@@ -922,6 +1088,7 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       SYNC();
       double fn, vn;
       cost_viol(S, S.Xn, S.Un, S.Ln, fn, vn);
+      OCNT(ST_N_TRIAL, 1);
       if (fn + mu * vn <= phi0 + 1e-4 * alpha * D) { ok = true; break; }
       alpha *= 0.5;
       SYNC();
@@ -937,6 +1104,7 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
     }
     if (lane < NT * NL) (&S.yl[0][0])[lane] += alpha * ((&S.nyl[0][0])[lane] - (&S.yl[0][0])[lane]);
     if (lane < NUV) S.yu[lane] += alpha * (S.nyu[lane] - S.yu[lane]);
+    OST(ST_LS);
     if (lane < NT) {
       S.ya[lane] += alpha * (S.nya[lane] - S.ya[lane]);
       S.yn[lane] += alpha * (S.nyn[lane] - S.yn[lane]);
@@ -964,6 +1132,14 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
     ist[(size_t)pb * 3 + 1] = (it < max_iter) ? it + 1 : max_iter;
     ist[(size_t)pb * 3 + 2] = qp_total;
   }
+#ifdef PIADMM_STAMPS
+  OST(ST_OUT);
+  if (lane == 0 && stamps) {
+    st_acc[ST_N_DROP] = (unsigned long long)qp_total;
+    st_acc[ST_TOTAL] = clock64() - st_t0;
+    for (int k = 0; k < NSTAMP; ++k) stamps[(size_t)pb * NSTAMP + k] = st_acc[k];
+  }
+#endif
 }
 
 }  // namespace obca
@@ -978,6 +1154,7 @@ struct piadmm_obca_s {
   double* d_rec = nullptr;
   double* d_out = nullptr;
   int* d_ist = nullptr;
+  unsigned long long* d_stamps = nullptr;
   int cap = 0, n = 0;
   std::string err;
 };
@@ -996,7 +1173,12 @@ int fail(piadmm_obca_t h, int code, const std::string& msg) {
 int ensure(piadmm_obca_t h, int n) {
   if (n <= h->cap) return 0;
   if (h->d_rec) { (void)hipFree(h->d_rec); (void)hipFree(h->d_out); (void)hipFree(h->d_ist); }
-  h->d_rec = nullptr; h->d_out = nullptr; h->d_ist = nullptr; h->cap = 0;
+  if (h->d_stamps) (void)hipFree(h->d_stamps);
+  h->d_rec = nullptr; h->d_out = nullptr; h->d_ist = nullptr; h->d_stamps = nullptr; h->cap = 0;
+#ifdef PIADMM_STAMPS
+  OHIP(h, hipMalloc(&h->d_stamps, (size_t)n * obca::NSTAMP * sizeof(unsigned long long)));
+  OHIP(h, hipMemset(h->d_stamps, 0, (size_t)n * obca::NSTAMP * sizeof(unsigned long long)));
+#endif
   OHIP(h, hipMalloc(&h->d_rec, (size_t)n * obca::REC * sizeof(double)));
   OHIP(h, hipMalloc(&h->d_out, (size_t)n * obca::OUT * sizeof(double)));
   OHIP(h, hipMalloc(&h->d_ist, (size_t)n * 3 * sizeof(int)));
@@ -1016,7 +1198,8 @@ int check_recs(piadmm_obca_t h, const double* recs, int n) {
 }
 
 int launch(piadmm_obca_t h) {
-  hipLaunchKernelGGL(obca::k_obca_sqp, dim3(h->n), dim3(64), 0, h->stream, h->d_rec, h->n, h->d_out, h->d_ist);
+  hipLaunchKernelGGL(obca::k_obca_sqp, dim3(h->n), dim3(64), 0, h->stream, h->d_rec, h->n, h->d_out, h->d_ist,
+                     h->d_stamps);
   OHIP(h, hipGetLastError());
   return 0;
 }
@@ -1097,6 +1280,14 @@ int32_t piadmm_obca_download(piadmm_obca_t h, double* out, int32_t* status3, int
   OHIP(h, hipMemcpyAsync(out, h->d_out, (size_t)n * obca::OUT * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   OHIP(h, hipMemcpyAsync(status3, h->d_ist, (size_t)n * 3 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   OHIP(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int32_t piadmm_obca_debug_stamps(piadmm_obca_t h, uint64_t* out, int32_t n) {
+  if (!h) return PIADMM_E_ARG;
+  if (!h->d_stamps) return fail(h, PIADMM_E_STATE, "not a stamps build (make stamps)");
+  if (n != h->n * obca::NSTAMP) return fail(h, PIADMM_E_ARG, "obca_debug_stamps: n must be 16 x the batch");
+  OHIP(h, hipMemcpy(out, h->d_stamps, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -93,6 +93,7 @@ SYMBOLS = [
     ("piadmm_obca_run", c_i32, [_H, c_i32]),
     ("piadmm_obca_time", c_i32, [_H, c_i32, _P(ctypes.c_float)]),
     ("piadmm_obca_download", c_i32, [_H, _dp, _ip, c_i32]),
+    ("piadmm_obca_debug_stamps", c_i32, [_H, _P(ctypes.c_uint64), c_i32]),
 ]
 
 # piadmm_allreduce_fn: int32_t (*)(void* ctx, double* buf, int64_t n)

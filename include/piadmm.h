@@ -278,6 +278,9 @@ int32_t piadmm_obca_upload(piadmm_obca_t h, const double* recs, int32_t n);
 int32_t piadmm_obca_run(piadmm_obca_t h, int32_t repeats);
 int32_t piadmm_obca_time(piadmm_obca_t h, int32_t repeats, float* ms_per_launch);
 int32_t piadmm_obca_download(piadmm_obca_t h, double* out, int32_t* status3, int32_t n);
+/* Diagnostic builds (-DPIADMM_STAMPS) only: per-problem cycle sums of the SQP phases and event
+ * counts of the last launch (n = 16 x batch uint64); PIADMM_E_STATE otherwise. */
+int32_t piadmm_obca_debug_stamps(piadmm_obca_t h, uint64_t* out, int32_t n);
 
 #ifdef __cplusplus
 }
