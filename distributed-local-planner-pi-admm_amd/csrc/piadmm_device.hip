@@ -7,7 +7,7 @@
 // and propagation.  Components are independent; the only inter-workgroup step is
 // the grid barrier of the reference's global stopping test (cooperative launch).
 //
-// Wave layout: wave w solves agent w's x-step; wave 0 also owns the pair.
+// Wave layout: wave w < 2 solves agent w's x-step; wave 2 owns the pair.
 // Lane k <-> time/variable index k (H <= 63).  All arithmetic is fp64.
 //
 // Every QP answer is the exact minimiser, certified by a complete KKT test:
@@ -31,131 +31,154 @@ struct CompLds {
   double *pos, *xt, *seed, *u, *hat, *lam, *S, *D, *last, *sc;
 };
 
+// What every wave of a component's workgroup knows about the launch (uniform values).
+struct StepCtx {
+  int H, H1, ci, w, l, a0, na, e, t, it0, it_end, slot;
+  bool first, last_launch, global, coop, skip, big, f32;
+  double deff, thr;
+  CompLds S;
+  double* resid;
+  double* vec_all;
+  WaveMem wm;
+};
 
-// One launch runs outer iterations [it0, it1) of MPC step t for every component (one
-// workgroup each).  The fused mode is one launch (0, max_outer, FIRST | LAST); the global
-// termination mode (term_global, reference quirk B9) runs one launch per outer iteration,
-// with the per-step state carried in HBM between launches (restore / save below) and the
-// stop decision taken by the host from all-reduced partials, then a LAST launch with no
-// iterations for the outputs and the propagation.
-template <bool BIG>
-__device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
-                                              int& nbar) {
-  extern __shared__ double lds[];
-  __shared__ int s_int[NW * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
+// The outer loop's control state.  Every wave keeps its own copy and updates it from the same
+// LDS values behind the same barriers, so all copies agree (the waves take identical branches).
+struct LoopCtl {
+  int flag, aliased, iters, gflag;
+  bool stopped, nanlast, act;
+  double dis_chk;
+};
+
+// collision graph (casadi/main.py:110-118), computed by every wave from this iteration's positions
+__device__ __forceinline__ bool collide(const StepCtx& X, const double* pos) {
+  if (X.e < 0 || X.na != 2) return false;
+  bool hit = false;
+  if (X.l <= X.H) {
+    const double dx = pos[0 * X.H1 + X.l] - pos[2 * X.H1 + X.l];
+    const double dy = pos[1 * X.H1 + X.l] - pos[3 * X.H1 + X.l];
+    hit = (dx * dx + dy * dy) < X.thr;
+  }
+  return wany(hit);
+}
+
+// The end of an outer iteration in every wave (casadi/main.py:164-181; MATLAB :191-210), after
+// barrier B when the pair's z-step ran: the residuals in S.sc, the component's stop test, and --
+// single rank, natural global termination -- the in-kernel stop test over all components behind
+// a grid barrier.  Returns true when the component's step ends here.
+__device__ __forceinline__ bool iter_tail(const DevArgs& A, const StepCtx& X, LoopCtl& L, int it, int& nbar) {
   const piadmm_config_t& c = A.cfg;
-  const int H = c.H, H1 = H + 1;
-  const int ci = blockIdx.x;
-  const int w = threadIdx.x >> 6, l = lid();
-  const int a0 = A.comp_ptr[ci];
-  const int na = A.comp_ptr[ci + 1] - a0;
-  const int e = A.comp_edge[ci];
+  const CompLds& S = X.S;
+  const double rk = L.act ? S.sc[0] : 0.0;
+  const double sk = L.act ? S.sc[1] : 0.0;
+  if (L.act) L.dis_chk = S.sc[2];
+  if (!c.fixed_iters && !X.global && rk <= c.eps_pri && sk <= c.eps_dual &&
+      (!c.term_dist_check || L.dis_chk > X.deff)) {
+    L.stopped = true;
+    return true;
+  }
+  if (X.coop && !c.fixed_iters) {
+    // global termination over all components, in-kernel (single rank): per-component partials,
+    // one grid barrier, every workgroup sums them in the same order and applies the host's stop
+    // rules (piadmm_capi.cpp run_steps) identically.  Double-buffered by the parity of the
+    // launch's barrier count (iterations and steps), so one barrier per iteration suffices;
+    // agent-scope atomic accesses keep the partials out of the non-coherent per-CU cache.
+    unsigned long long t_gb = STAMP_T();
+    double* part = A.gpart + (size_t)(nbar & 1) * A.C * 5;
+    ++nbar;
+    const int ci = X.ci;
+    if (threadIdx.x == 0) {
+      const bool seen = (X.e >= 0) && (L.dis_chk == L.dis_chk);
+      const double pv[5] = {rk, sk, (X.e >= 0 && L.act) ? 1.0 : 0.0, seen ? 1.0 : 0.0,
+                            (seen && !(L.dis_chk > X.deff)) ? 1.0 : 0.0};
+#pragma unroll
+      for (int q = 0; q < 5; ++q)
+        __hip_atomic_store(&part[ci * 5 + q], pv[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    cooperative_groups::this_grid().sync();
+    {
+      // the first NT threads load (components tid, tid + NT, ...), then five threads sum the
+      // per-thread partials in thread order: a fixed order, identical in every workgroup and equal
+      // to k_term_partials' (the host-decided path)
+      constexpr int NT = NW * WAVE;
+      double v[5] = {0, 0, 0, 0, 0};
+      if ((int)threadIdx.x < NT)
+        for (int k = threadIdx.x; k < A.C; k += NT)
+#pragma unroll
+          for (int q = 0; q < 5; ++q)
+            v[q] += __hip_atomic_load(&part[k * 5 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double* red = X.vec_all;         // the waves' vector buffers are free between QP solves
+      if ((int)threadIdx.x < NT)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) red[q * NT + threadIdx.x] = v[q];
+      __syncthreads();
+      if (threadIdx.x < 5) {
+        double tot = 0.0;
+        for (int k = 0; k < NT; ++k) tot += red[threadIdx.x * NT + k];
+        S.sc[16 + threadIdx.x] = tot;
+      }
+    }
+    __syncthreads();
+    const double trk = S.sc[16], tsk = S.sc[17], tact = S.sc[18], tseen = S.sc[19], tbad = S.sc[20];
+    __syncthreads();
+    STAMP_ADD(ST_TERM, t_gb);
+    if (tact == 0.0 && L.gflag == 0) {       // no pair collides anywhere: stop (:115-116)
+      L.nanlast = true;
+      L.stopped = true;
+      return true;
+    }
+    L.gflag = 1;
+    if (ci == 0 && threadIdx.x == 0) {
+      A.ghist[((size_t)X.slot * c.max_outer + it) * 2 + 0] = trk;
+      A.ghist[((size_t)X.slot * c.max_outer + it) * 2 + 1] = tsk;
+    }
+    const bool dist_ok = tseen > 0.0 && tbad == 0.0;
+    if (trk <= c.eps_pri && tsk <= c.eps_dual && (!c.term_dist_check || dist_ok)) {
+      L.stopped = true;
+      return true;
+    }
+  }
+  if (c.alias_dual_residual) L.aliased = 1;
+  return false;
+}
 
-  // ---- LDS carve (lds_bytes() in piadmm_internal.h)
-  constexpr bool big = BIG;      // H > HMAX (launch_mpc_step picks the instantiation)
-  const bool f32 = c.precision == 1;   // ADMM matrices in fp32 (lds_bytes: half the space)
-  double *Kx = nullptr, *Gx = nullptr, *Ke = nullptr, *scr, *xfac_all, *xt_all = nullptr, *vec_all;
-  float* Kef = nullptr;
+// Work counters of one wave (summed over the workgroup's waves in the epilogue).
+struct WaveCnt {
+  int xqp = 0, zqp = 0, admm_x = 0, admm_z = 0, pdas_x = 0, pdas_z = 0, inexact = 0, gi = 0;
+  bool warm = false;
+};
+
+// -------------------------------------------------------------------- agent waves (0, 1)
+// Wave w < na solves agent a0 + w's x-step every outer iteration (casadi/main.py:81-106); its
+// QP state (tables, labels, warm ADMM state) stays in this wave's registers and LDS regions for
+// the whole step.  The pair's state never lives here: the pair wave owns it.
+template <bool BIG>
+__device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
+  extern __shared__ double lds[];
+  const piadmm_config_t& c = A.cfg;
+  const int H = X.H, H1 = X.H1, w = X.w, l = X.l, ci = X.ci, e = X.e, t = X.t;
+  const bool big = BIG, f32 = X.f32, first = X.first;
+  const CompLds& S = X.S;
+  // ---- this wave's LDS regions (lds_bytes() in piadmm_internal.h)
+  double *Kx = nullptr, *Gx = nullptr, *xfac, *xt_all = nullptr;
   float* Kxf = nullptr;
   if (!big) {
     double* p = lds;
     if (f32) { Kxf = (float*)p; p += kxf_words(H); }     // 2 x H*H fp32 agent K_s^-1 (even per wave)
     else { Kx = p; p += 2 * H * H; }                     // 2 x H*H   agent K_s^-1
     Gx = p; p += 2 * (H * H + H);                        // 2 x (H*H+H) agent polish G | g
-    if (f32) { Kef = (float*)p; p += 2 * H * H; }        // 4*H*H fp32 pair K_s^-1
-    else { Ke = p; p += 4 * H * H; }                     // 4*H*H     pair K_s^-1
-    scr = p;                                             // 64 x LD   pair scratch (wave 0)
-    xfac_all = scr + 64 * LD;                            // NW x HMAX x (HMAX+1)
-    xt_all = xfac_all + NW * HMAX * (HMAX + 1);          // NW x (HMAX+1) x XLD
-    vec_all = xt_all + NW * (HMAX + 1) * XLD;            // NW x 512
+    p += f32 ? 2 * H * H : 4 * H * H;                    // pair K_s^-1 (the pair wave's)
+    p += 64 * LD;                                        // pair scratch (the pair wave's)
+    xfac = p + w * HMAX * (HMAX + 1);                    // NW x HMAX x (HMAX+1)
+    xt_all = p + NW * HMAX * (HMAX + 1);                 // NW x (HMAX+1) x XLD
   } else {
-    Ke = (e >= 0) ? A.Ke_g + (size_t)e * 4 * H * H : nullptr;   // HBM / L2 (built in place)
-    scr = lds;                                           // 64 x LD   pair scratch (wave 0)
-    xfac_all = scr + 64 * LD;                            // NW x xrows(H) x (xrows+1)
-    vec_all = xfac_all + NW * xrows(H) * (xrows(H) + 1); // NW x 512
+    xfac = lds + 64 * LD + w * xrows(H) * (xrows(H) + 1);   // NW x xrows(H) x (xrows+1)
   }
-  double* fdiag_all = vec_all + NW * 512;                // NW x 256
-  CompLds S;
-  S.pos = fdiag_all + NW * 256;
-  S.xt = S.pos + 8 * H1;   // pos_old double-buffered by outer-iteration parity
-  S.seed = S.xt + 6;
-  S.u = S.seed + 4;
-  S.hat = S.u + 2 * H;
-  S.lam = S.hat + 4 * H1;
-  S.S = S.lam + 4 * H1;
-  S.D = S.S + 4 * H1;
-  S.last = S.D + 4 * H1;
-  S.sc = S.last + 4 * H1;
-  if (big && f32) Kef = (float*)(S.sc + 32);             // big mode: fp32 image of the pair K_s^-1
-  WaveMem wm{vec_all + w * 512, s_int + w * 272};
-  double* xfac = big ? xfac_all + w * xrows(H) * (xrows(H) + 1) : xfac_all + w * HMAX * (HMAX + 1);
-  double* xdiag = fdiag_all + w * 256;
-  double* zdiag = xdiag + 128;
-  int* xids = wm.ib;
-  int* zids = wm.ib + 128;
-  int* xfs = wm.ib + 256;
-  int* zfs = wm.ib + 257;
-  if (l == 0) {
-    xfs[0] = -1;
-    zfs[0] = -1;
-  }
+  double* xdiag = X.vec_all + NWT * 512 + w * 128;       // NWT x 128 factor diagonals
+  int* xids = X.wm.ib;
+  int* xfs = X.wm.ib + 256;
+  if (l == 0) xfs[0] = -1;
 
-  const bool first = (flags & F_FIRST) != 0;
-  const bool last_launch = (flags & F_LAST) != 0;
-  const bool global = (flags & F_GLOBAL) != 0;
-  const bool coop = (flags & F_COOP) != 0;   // global stop decided in-kernel (cooperative launch)
-  // a component whose step already ended in an earlier launch of this step (per-component stop,
-  // host-stepped by piadmm_outer_iter) runs no further iteration: its state is only carried
-  const bool skip = !first && A.cst[(size_t)ci * 4 + 3] != 0;
-  const int it_end = skip ? it0 : it1;
-  bool stopped = skip;
-  int gflag = 0;                             // coop: some pair ever collided (casadi/main.py:115)
-  bool nanlast = (flags & F_NANLAST) != 0;
-  // ---- seeds (casadi/main.py:48-49) and zero per-step state (:52-63)
-  if ((int)threadIdx.x < na) {
-    const int a = a0 + threadIdx.x;
-    const double x = A.xt[3 * a], y = A.xt[3 * a + 1], th = A.xt[3 * a + 2], s = A.spd[a];
-    S.xt[3 * threadIdx.x + 0] = x;
-    S.xt[3 * threadIdx.x + 1] = y;
-    S.xt[3 * threadIdx.x + 2] = th;
-    S.seed[2 * threadIdx.x + 0] = around(x + c.dt * s * cos(th), c.round_decimals);
-    S.seed[2 * threadIdx.x + 1] = around(y + c.dt * s * sin(th), c.round_decimals);
-  }
-  for (int i = threadIdx.x; i < 32; i += blockDim.x) S.sc[i] = 0.0;
-  {
-    double* const edge_lds[5] = {S.hat, S.lam, S.S, S.D, S.last};
-    double* const edge_hbm[5] = {A.hat, A.lam, A.Sacc, A.Dacc, A.last};
-    if (first) {
-      for (int i = threadIdx.x; i < 8 * H1; i += blockDim.x) S.pos[i] = 0.0;
-      // casadi/main.py:52-63 resets hat, lam (and the PI accumulators) every MPC step; with
-      // warm_duals they continue from the previous step shifted by one slot (a12)
-      for (int k = 0; k < 5; ++k)
-        for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) {
-          double v = 0.0;
-          if (e >= 0 && c.warm_duals) {
-            const int r = i / H1, tt = i - r * H1;
-            v = edge_hbm[k][(size_t)e * 4 * H1 + r * H1 + min(tt + 1, H)];
-          }
-          edge_lds[k][i] = v;
-        }
-    } else {
-      // state of the previous launch of this step
-      for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
-        S.pos[((it0 - 1) & 1) * 4 * H1 + i] = (i < na * 2 * H1) ? A.pos_old[(size_t)a0 * 2 * H1 + i] : 0.0;
-      for (int i = threadIdx.x; i < na * H; i += blockDim.x) S.u[i] = A.u[(size_t)a0 * H + i];
-      for (int k = 0; k < 5; ++k)
-        for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
-          edge_lds[k][i] = (e >= 0) ? edge_hbm[k][(size_t)e * 4 * H1 + i] : 0.0;
-    }
-  }
-  __syncthreads();
-  // pair safety distance (a13 tightening from the step's start states, else dis_thres)
-  double deff = c.dis_thres;
-  if (e >= 0 && c.tighten && na == 2)
-    deff = c.dis_thres + delay_norm(c, S.xt[2], A.spd[a0]) + delay_norm(c, S.xt[5], A.spd[a0 + 1]);
-  unsigned long long t_k = STAMP_T();
-
-  // ---- per-step QP setup (registers of the owning wave stay live for the whole step)
   QP<1> qx;
   double xs_x[1] = {0.0}, zs_x[2] = {0.0, 0.0}, ys_x[2] = {0.0, 0.0};
   signed char lab_x[2] = {0, 0};
@@ -164,9 +187,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   int nnb = 0;
   Geo gx;
   double cx_own = 0.0, cy_own = 0.0;
-  if (w < na) {
+  const bool own = w < X.na;
+  if (own) {
     unsigned long long t0 = STAMP_T();
-    const int a = a0 + w;
+    const int a = X.a0 + w;
     gx = make_geo(S.xt + 3 * w, A.spd[a], c);
     affine_c(gx, c.dt, H, cx_own, cy_own);
     qp_common(c, H, A.rho_x[a], qx);
@@ -175,7 +199,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     qx.kf32 = !big && f32;                        // big mode: the x-step K stays fp64 in HBM
     qx.Pinv = A.Pinv_x + (size_t)a * H * H;    // L2-resident; read only when W changes
     qx.G = big ? A.Gx_g + (size_t)a * (H * H + H) : Gx + w * (H * H + H);
-    qx.vb = wm.vb;
+    qx.vb = X.wm.vb;
     qx.fac = xfac;
     qx.XT = big ? A.XT_g + (size_t)a * H1 * XLDG : xt_all + w * (HMAX + 1) * XLD;
     qx.xld = big ? XLDG : XLD;
@@ -219,6 +243,180 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     }
     STAMP_ADD(ST_SETUP_X, t0);
   }
+  __syncthreads();
+
+  const bool nonlin_pos = c.pos_model != 0;
+  // the own agent's start state and speed in registers for the per-iteration rollout
+  double rl_x0 = 0.0, rl_y0 = 0.0, rl_th0 = 0.0, rl_s = 0.0, rl_sl = 0.0;
+  if (own) {
+    rl_x0 = S.xt[3 * w + 0];
+    rl_y0 = S.xt[3 * w + 1];
+    rl_th0 = S.xt[3 * w + 2];
+    rl_s = A.spd[X.a0 + w];
+    rl_sl = rl_s / c.L;
+  }
+  // reference positions of the own agent at time lanes (fixed for the step)
+  double rx_own = 0.0, ry_own = 0.0;
+  if (own && l <= H) {
+    const double* rp = A.ref + (size_t)(X.a0 + w) * 2 * A.T;
+    rx_own = rp[t + l];
+    ry_own = rp[A.T + t + l];
+  }
+  // the x-step's consensus term (cx - hat + lam) of the own direction in registers: hat and lam
+  // change only in a z-step, after which it is reloaded (behind the second barrier)
+  const bool cpl = own && nnb > 0 && e >= 0 && l <= H;
+  double cpx = 0.0, cpy = 0.0;
+  auto load_cp = [&]() {
+    if (cpl) {
+      const int d = w;   // agent local 0 owns hat_{v1 v2} (dir 0), agent 1 dir 1
+      cpx = cx_own - S.hat[(d * 2 + 0) * H1 + l] + S.lam[(d * 2 + 0) * H1 + l];
+      cpy = cy_own - S.hat[(d * 2 + 1) * H1 + l] + S.lam[(d * 2 + 1) * H1 + l];
+    }
+  };
+  load_cp();
+  for (int it = X.it0; it < X.it_end; ++it) {
+    L.iters = it + 1;
+    // this iteration's pos_old buffer: a wave may start the next iteration's x-step while
+    // another still reads this one's positions (no second barrier without a z-step)
+    double* const pos = S.pos + (it & 1) * 4 * H1;
+    // -------- x-step (casadi/main.py:81-106)
+    if (own) {
+      unsigned long long t_xs = STAMP_T();
+      const bool tl = l <= H;
+      double vx = 2.0 * c.Pnorm * (cx_own - rx_own), vy = 2.0 * c.Pnorm * (cy_own - ry_own);
+      if (cpl) {
+        vx = vx + c.rho * cpx;
+        vy = vy + c.rho * cpy;
+      }
+      const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
+      const double wsh = shdn(wt, 1);
+      qx.wq = (l < H) ? wsh : 0.0;
+      qx.qvalid = false;
+      STAMP_ADD(ST_XQ, t_xs);
+      double ustar[1];
+      unsigned long long t_q = STAMP_T();
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+                               qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && it == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
+      STAMP_ADD(ST_XQP, t_q);
+      status_x |= stx;
+      ++n.xqp;
+      n.inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
+      warm_x = true;
+      unsigned long long t_rd = STAMP_T();
+      const double u = around(ustar[0], c.round_decimals);
+      STAMP_ADD(ST_ROUND, t_rd);
+      double px, py, pth;
+      unsigned long long t_r = STAMP_T();
+      rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+      STAMP_ADD(ST_XROLL, t_r);
+      if (l <= H) {
+        pos[(w * 2 + 0) * H1 + l] = px;
+        pos[(w * 2 + 1) * H1 + l] = py;
+      }
+      if (l < H) S.u[w * H + l] = u;
+      STAMP_ADD(ST_XSTEP, t_xs);
+    }
+    unsigned long long t_sa = STAMP_T();
+    __syncthreads();                                     // A: every agent's positions
+    STAMP_ADD(ST_SYNC_A, t_sa);
+    L.act = collide(X, pos);
+    if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
+      L.stopped = true;
+      break;
+    }
+    L.flag = 1;
+    // (the pair wave runs the z-step and records the residuals now)
+    unsigned long long t_sb = STAMP_T();
+    if (__builtin_expect(L.act, 0)) {
+      __syncthreads();                                   // B: hat, lam, S, D, last, S.sc
+      load_cp();
+    }
+    STAMP_ADD(ST_SYNC_B, t_sb);
+    if (iter_tail(A, X, L, it, nbar)) break;
+  }
+  n.warm = own && warm_x;
+  // ---- the agent's state of this launch and, in the last launch, outputs and propagation
+  // (casadi/main.py:185-192)
+  if (own) {
+    const int a = X.a0 + w;
+    // the last executed iteration's buffer (a skipped launch: the buffer its state was restored to)
+    const double* posl = S.pos + ((X.skip ? X.it0 - 1 : L.iters - 1) & 1) * 4 * H1;
+    for (int i = l; i < 2 * H1; i += WAVE) A.pos_old[(size_t)a * 2 * H1 + i] = posl[w * 2 * H1 + i];
+    const double u = (l < H) ? S.u[w * H + l] : 0.0;
+    if (l < H) A.u[(size_t)a * H + l] = u;
+    if (l == 0) {
+      A.status[a] = status_x;
+      A.rho_x[a] = qx.rho;
+    }
+    if (__builtin_expect(A.xcache_rho[a] != qx.rho, 0)) {   // adaptive rho rebuilt K_s^-1: refresh the cache
+      double* Kc = A.Kx_cache + (size_t)a * H * H;
+      if (qx.kf32) {
+        for (int i = l; i < H * H; i += WAVE) Kc[i] = (double)qx.Kf[i];   // the fp32 image
+      } else if (qx.K != Kc) {
+        for (int i = l; i < H * H; i += WAVE) Kc[i] = qx.K[i];
+      }
+      if (l == 0) A.xcache_rho[a] = qx.rho;
+    }
+    if (!X.last_launch) {
+      if (qx.wraw) warm_to_scaled(qx, xs_x, zs_x, ys_x);
+      double* qs = A.qs_x + (size_t)a * 5 * WAVE;
+      signed char* ql = A.ql_x + (size_t)a * 2 * WAVE;
+      qs[l] = xs_x[0];
+      qs[WAVE + l] = zs_x[0];
+      qs[2 * WAVE + l] = zs_x[1];
+      qs[3 * WAVE + l] = ys_x[0];
+      qs[4 * WAVE + l] = ys_x[1];
+      ql[l] = lab_x[0];
+      ql[WAVE + l] = lab_x[1];
+    } else {
+      double px, py, pth;
+      rollout(S.xt + 3 * w, A.spd[a], u, c, H, true, px, py, pth);
+      if (l == 1) {
+        A.xt[3 * a + 0] = px;
+        A.xt[3 * a + 1] = py;
+        A.xt[3 * a + 2] = pth;
+      }
+      if (l == 0) A.warm_ok[a] = 1;
+      if (l < HCAP) {
+        signed char* lb = A.lab_x + (size_t)a * 2 * HCAP;
+        lb[l] = lab_x[0];
+        lb[HCAP + l] = lab_x[1];
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------------------- the pair wave (2)
+// Wave PW owns the component's pair (when it has one): the per-step pair setup (concurrent with
+// the agents' setups), the z-step QP, the hat rollouts, the dual update and the residuals
+// (casadi/main.py:121-181).  Its QP state stays in this wave's registers for the whole step.
+template <bool BIG>
+__device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
+  extern __shared__ double lds[];
+  const piadmm_config_t& c = A.cfg;
+  const int H = X.H, H1 = X.H1, l = X.l, ci = X.ci, e = X.e, t = X.t;
+  const bool big = BIG, f32 = X.f32, first = X.first;
+  const CompLds& S = X.S;
+  // ---- the pair's LDS regions (lds_bytes() in piadmm_internal.h)
+  double *Ke = nullptr, *scr;
+  float* Kef = nullptr;
+  if (!big) {
+    double* p = lds;
+    p += f32 ? kxf_words(H) : 2 * H * H;                 // agent K_s^-1 (the agent waves')
+    p += 2 * (H * H + H);                                // agent polish G | g (the agent waves')
+    if (f32) { Kef = (float*)p; p += 2 * H * H; }        // 4*H*H fp32 pair K_s^-1
+    else { Ke = p; p += 4 * H * H; }                     // 4*H*H     pair K_s^-1
+    scr = p;                                             // 64 x LD   pair scratch
+  } else {
+    Ke = (e >= 0) ? A.Ke_g + (size_t)e * 4 * H * H : nullptr;   // HBM / L2 (built in place)
+    scr = lds;                                           // 64 x LD   pair scratch
+    if (f32) Kef = (float*)(S.sc + 32);                  // big mode: fp32 image of the pair K_s^-1
+  }
+  double* zdiag = X.vec_all + NWT * 512 + PW * 128;
+  int* zids = X.wm.ib + 128;
+  int* zfs = X.wm.ib + 257;
+  if (l == 0) zfs[0] = -1;
+
   QP<2> qe;
   double xs_e[2] = {0.0, 0.0}, zs_e[5] = {0, 0, 0, 0, 0}, ys_e[5] = {0, 0, 0, 0, 0};
   signed char lab_e[5] = {0, 0, 0, 0, 0};
@@ -226,10 +424,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   int status_e = 0;
   Geo ge1, ge2;
   double c1x = 0.0, c1y = 0.0, c2x = 0.0, c2y = 0.0;
-  if (w == 0 && e >= 0) {
+  if (e >= 0) {
     unsigned long long t0 = STAMP_T();
-    ge1 = make_geo(S.xt + 0, A.spd[a0], c);
-    ge2 = make_geo(S.xt + 3, A.spd[a0 + 1], c);
+    ge1 = make_geo(S.xt + 0, A.spd[X.a0], c);
+    ge2 = make_geo(S.xt + 3, A.spd[X.a0 + 1], c);
     affine_c(ge1, c.dt, H, c1x, c1y);
     affine_c(ge2, c.dt, H, c2x, c2y);
     qe.H = H;
@@ -247,7 +445,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     qe.Kf = Kef;
     qe.kf32 = f32;
     qe.Pinv = A.tab_e + (size_t)e * 8 * H * H;
-    qe.vb = wm.vb;
+    qe.vb = X.wm.vb;
     qe.fac = scr;
     qe.fdiag = zdiag;
     qe.ib = zids;
@@ -265,7 +463,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     qe.tstep = t;
     // Ke doubles as the H x 2H staging of the per-scenario pair tables; with fp32 images in
     // LDS mode the fp32 region (2H^2 doubles of space) takes that role
-    setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke ? Ke : (double*)Kef, deff);
+    setup_pair(A, e, qe, ge1, ge2, c1x, c1y, c2x, c2y, S.seed, scr, Ke ? Ke : (double*)Kef, X.deff);
     if (!first) {
       const double* qs = A.qs_e + (size_t)e * 12 * WAVE;
       const signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
@@ -287,111 +485,20 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   }
   __syncthreads();
 
-  const bool nonlin_pos = c.pos_model != 0;
-  const double thr = c.collide_sq_thres ? deff * deff : deff;
-  int flag = first ? 0 : A.cst[(size_t)ci * 4 + 0];
-  int aliased = first ? 0 : A.cst[(size_t)ci * 4 + 1];
-  int iters = skip ? A.iters[ci] : it0;
-  int n_xqp = 0, n_zqp = 0, n_admm_x = 0, n_admm_z = 0, n_pdas_x = 0, n_pdas_z = 0, n_inexact = 0, n_gi = 0;
-  bool act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
-  double dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
-  double* resid = A.resid + ((size_t)slot * A.C + ci) * c.max_outer * 2;   // slot: step of the launch
-  if (first)
-    for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
-  if (coop && ci == 0)
-    for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) A.ghist[(size_t)slot * 2 * c.max_outer + i] = NAN;
-  // the own agent's start state and speed in registers for the per-iteration rollout
-  double rl_x0 = 0.0, rl_y0 = 0.0, rl_th0 = 0.0, rl_s = 0.0, rl_sl = 0.0;
-  if (w < na) {
-    rl_x0 = S.xt[3 * w + 0];
-    rl_y0 = S.xt[3 * w + 1];
-    rl_th0 = S.xt[3 * w + 2];
-    rl_s = A.spd[a0 + w];
-    rl_sl = rl_s / c.L;
-  }
-  // reference positions of the own agent at time lanes (fixed for the step)
-  double rx_own = 0.0, ry_own = 0.0;
-  if (w < na && l <= H) {
-    const double* rp = A.ref + (size_t)(a0 + w) * 2 * A.T;
-    rx_own = rp[t + l];
-    ry_own = rp[A.T + t + l];
-  }
-
-  // the x-step's consensus term (cx - hat + lam) of the own direction in registers: hat and lam
-  // change only in a z-step, after which it is reloaded (behind the second barrier)
-  const bool cpl = w < na && nnb > 0 && e >= 0 && l <= H;
-  double cpx = 0.0, cpy = 0.0;
-  auto load_cp = [&]() {
-    if (cpl) {
-      const int d = w;   // agent local 0 owns hat_{v1 v2} (dir 0), agent 1 dir 1
-      cpx = cx_own - S.hat[(d * 2 + 0) * H1 + l] + S.lam[(d * 2 + 0) * H1 + l];
-      cpy = cy_own - S.hat[(d * 2 + 1) * H1 + l] + S.lam[(d * 2 + 1) * H1 + l];
-    }
-  };
-  load_cp();
-  for (int it = it0; it < it_end; ++it) {
-    iters = it + 1;
-    // this iteration's pos_old buffer: a wave may start the next iteration's x-step while
-    // the other still reads this one's positions (no second barrier without a z-step)
+  for (int it = X.it0; it < X.it_end; ++it) {
+    L.iters = it + 1;
     double* const pos = S.pos + (it & 1) * 4 * H1;
-    // -------- x-step: every agent of the component (casadi/main.py:81-106)
-    if (w < na) {
-      unsigned long long t_xs = STAMP_T();
-      const bool tl = l <= H;
-      double vx = 2.0 * c.Pnorm * (cx_own - rx_own), vy = 2.0 * c.Pnorm * (cy_own - ry_own);
-      if (cpl) {
-        vx = vx + c.rho * cpx;
-        vy = vy + c.rho * cpy;
-      }
-      const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
-      const double wsh = shdn(wt, 1);
-      qx.wq = (l < H) ? wsh : 0.0;
-      qx.qvalid = false;
-      STAMP_ADD(ST_XQ, t_xs);
-      double ustar[1];
-      unsigned long long t_q = STAMP_T();
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
-                               qx.fld, ustar, n_admm_x, n_pdas_x, n_gi, (A.x_gi >= 2 && first && it == it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
-      STAMP_ADD(ST_XQP, t_q);
-      status_x |= stx;
-      ++n_xqp;
-      n_inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
-      warm_x = true;
-      unsigned long long t_rd = STAMP_T();
-      const double u = around(ustar[0], c.round_decimals);
-      STAMP_ADD(ST_ROUND, t_rd);
-      double px, py, pth;
-      unsigned long long t_r = STAMP_T();
-      rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
-      STAMP_ADD(ST_XROLL, t_r);
-      if (l <= H) {
-        pos[(w * 2 + 0) * H1 + l] = px;
-        pos[(w * 2 + 1) * H1 + l] = py;
-      }
-      if (l < H) S.u[w * H + l] = u;
-      STAMP_ADD(ST_XSTEP, t_xs);
-    }
     unsigned long long t_sa = STAMP_T();
-    __syncthreads();
+    __syncthreads();                                     // A: every agent's positions
     STAMP_ADD(ST_SYNC_A, t_sa);
-    // -------- collision graph (casadi/main.py:110-118), computed by every wave
-    act = false;
-    if (e >= 0 && na == 2) {
-      bool hit = false;
-      if (l <= H) {
-        const double dx = pos[0 * H1 + l] - pos[2 * H1 + l];
-        const double dy = pos[1 * H1 + l] - pos[3 * H1 + l];
-        hit = (dx * dx + dy * dy) < thr;
-      }
-      act = wany(hit);
-    }
-    if (!act && flag == 0 && !c.fixed_iters && !global) {   // no edge ever: stop (:115-116)
-      stopped = true;
+    L.act = collide(X, pos);
+    if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
+      L.stopped = true;
       break;
     }
-    flag = 1;
+    L.flag = 1;
     // -------- z-step + dual update on the colliding pair (casadi/main.py:121-162)
-    if (__builtin_expect(act && w == 0, 0)) {     // cold: about once per MPC step
+    if (__builtin_expect(L.act, 0)) {     // cold: about once per MPC step
       unsigned long long t_z = STAMP_T();
       const bool tl = l <= H;
       double bx[2], by[2];
@@ -411,17 +518,17 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       // (big mode, two columns per lane, in HBM)
       const int ste = qp_solve<2, BIG>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
                                big ? Ke : scr, big ? 2 * H : LD, uh,
-                               n_admm_z, n_pdas_z, n_gi);
+                               n.admm_z, n.pdas_z, n.gi);
       STAMP_ADD(ST_ZQP, t_zq);
       status_e |= ste;
-      ++n_zqp;
-      n_inexact += (ste & PIADMM_QP_INEXACT) ? 1 : 0;
+      ++n.zqp;
+      n.inexact += (ste & PIADMM_QP_INEXACT) ? 1 : 0;
       warm_e = true;
       // hat positions: nonlinear rollout of the rounded pair controls (:153-158)
       double hx[2], hy[2], hth;
       for (int v = 0; v < 2; ++v) {
         const double uv = (l < H) ? around(uh[v], c.round_decimals) : 0.0;
-        rollout(S.xt + 3 * v, A.spd[a0 + v], uv, c, H, true, hx[v], hy[v], hth);
+        rollout(S.xt + 3 * v, A.spd[X.a0 + v], uv, c, H, true, hx[v], hy[v], hth);
       }
       // dual update (plain :161-162 / PI + anti-windup MATLAB :156-188)
       double px[2], py[2];
@@ -482,208 +589,41 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       ss = wsum(ss);
       if (l == 0) {
         S.sc[0] = 2.0 * sqrt(rr);
-        S.sc[1] = aliased ? 0.0 : 2.0 * sqrt(ss);
+        S.sc[1] = L.aliased ? 0.0 : 2.0 * sqrt(ss);
         S.sc[2] = rdl(dist, 1);
       }
       STAMP_ADD(ST_ZSTEP, t_z);
     }
-    // -------- termination (casadi/main.py:164-181; MATLAB :191-210).  Wave 0 (which wrote
-    // S.sc) records the residuals and, unless the component stops, last_iter_hat_pos before
-    // the barrier; after it every wave takes the same stop decision from S.sc.  One barrier per
-    // half-iteration: S.sc is rewritten only after the next iteration's first barrier.
-    if (w == 0) {
+    // -------- residual record (casadi/main.py:164-181; MATLAB :191-210): this wave wrote S.sc;
+    // it records the residuals and, unless the component stops, last_iter_hat_pos before barrier
+    // B.  S.sc is rewritten only after the next iteration's barrier A.
+    {
       unsigned long long t_tw = STAMP_T();
       wsync();
-      const double rk0 = act ? S.sc[0] : 0.0;
-      const double sk0 = act ? S.sc[1] : 0.0;
-      const double dc0 = act ? S.sc[2] : dis_chk;
+      const double rk0 = L.act ? S.sc[0] : 0.0;
+      const double sk0 = L.act ? S.sc[1] : 0.0;
+      const double dc0 = L.act ? S.sc[2] : L.dis_chk;
       if (l == 0) {
-        resid[2 * it + 0] = rk0;
-        resid[2 * it + 1] = sk0;
+        X.resid[2 * it + 0] = rk0;
+        X.resid[2 * it + 1] = sk0;
       }
-      const bool stop0 = !c.fixed_iters && !global && rk0 <= c.eps_pri && sk0 <= c.eps_dual &&
-                         (!c.term_dist_check || dc0 > deff);
+      const bool stop0 = !c.fixed_iters && !X.global && rk0 <= c.eps_pri && sk0 <= c.eps_dual &&
+                         (!c.term_dist_check || dc0 > X.deff);
       // last_iter_hat_pos = hat_pos_old: only a z-step changes hat, so the copy is needed
       // only after one (S.last already equals hat otherwise)
-      if (__builtin_expect(act && !stop0 && !c.alias_dual_residual, 0))
+      if (__builtin_expect(L.act && !stop0 && !c.alias_dual_residual, 0))
         for (int i = l; i < 4 * H1; i += WAVE) S.last[i] = S.hat[i];
       STAMP_ADD(ST_TERMW, t_tw);
     }
-    // second barrier only after a z-step (it wrote hat, lam, S, D, last and S.sc); without
-    // one every wave takes the stop decision from its registers (rk = sk = 0)
     unsigned long long t_sb = STAMP_T();
-    if (__builtin_expect(act, 0)) {
-      __syncthreads();
-      load_cp();
-    }
+    if (__builtin_expect(L.act, 0)) __syncthreads();     // B
     STAMP_ADD(ST_SYNC_B, t_sb);
-    const double rk = act ? S.sc[0] : 0.0;
-    const double sk = act ? S.sc[1] : 0.0;
-    if (act) dis_chk = S.sc[2];
-    if (!c.fixed_iters && !global && rk <= c.eps_pri && sk <= c.eps_dual &&
-        (!c.term_dist_check || dis_chk > deff)) {
-      stopped = true;
-      break;
-    }
-    if (coop && !c.fixed_iters) {
-      // -------- global termination over all components, in-kernel (single rank): the
-      // partials of k_term_partials, one grid barrier, every workgroup sums them in the same
-      // order and applies the host's stop rules (piadmm_capi.cpp run_steps) identically.
-      // Double-buffered by the parity of the launch's barrier count (iterations and steps),
-      // so one barrier per iteration suffices; agent-scope atomic accesses keep the
-      // partials out of the non-coherent per-CU cache.
-      unsigned long long t_gb = STAMP_T();
-      double* part = A.gpart + (size_t)(nbar & 1) * A.C * 5;
-      ++nbar;
-      if (threadIdx.x == 0) {
-        const bool seen = (e >= 0) && (dis_chk == dis_chk);
-        const double pv[5] = {rk, sk, (e >= 0 && act) ? 1.0 : 0.0, seen ? 1.0 : 0.0,
-                              (seen && !(dis_chk > deff)) ? 1.0 : 0.0};
-#pragma unroll
-        for (int q = 0; q < 5; ++q)
-          __hip_atomic_store(&part[ci * 5 + q], pv[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      cooperative_groups::this_grid().sync();
-      {
-        // all threads load (components tid, tid + 128, ...), then five threads sum the
-        // per-thread partials in thread order: a fixed order, identical in every workgroup
-        double v[5] = {0, 0, 0, 0, 0};
-        for (int k = threadIdx.x; k < A.C; k += blockDim.x)
-#pragma unroll
-          for (int q = 0; q < 5; ++q)
-            v[q] += __hip_atomic_load(&part[k * 5 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        double* red = vec_all;           // the waves' vector buffers are free between QP solves
-#pragma unroll
-        for (int q = 0; q < 5; ++q) red[q * NW * WAVE + threadIdx.x] = v[q];
-        __syncthreads();
-        if (threadIdx.x < 5) {
-          double tot = 0.0;
-          for (int k = 0; k < NW * WAVE; ++k) tot += red[threadIdx.x * NW * WAVE + k];
-          S.sc[16 + threadIdx.x] = tot;
-        }
-      }
-      __syncthreads();
-      const double trk = S.sc[16], tsk = S.sc[17], tact = S.sc[18], tseen = S.sc[19], tbad = S.sc[20];
-      __syncthreads();
-      STAMP_ADD(ST_TERM, t_gb);
-      if (tact == 0.0 && gflag == 0) {       // no pair collides anywhere: stop (:115-116)
-        nanlast = true;
-        stopped = true;
-        break;
-      }
-      gflag = 1;
-      if (ci == 0 && threadIdx.x == 0) {
-        A.ghist[((size_t)slot * c.max_outer + it) * 2 + 0] = trk;
-        A.ghist[((size_t)slot * c.max_outer + it) * 2 + 1] = tsk;
-      }
-      const bool dist_ok = tseen > 0.0 && tbad == 0.0;
-      if (trk <= c.eps_pri && tsk <= c.eps_dual && (!c.term_dist_check || dist_ok)) {
-        stopped = true;
-        break;
-      }
-    }
-    if (c.alias_dual_residual) aliased = 1;
+    if (iter_tail(A, X, L, it, nbar)) break;
   }
-  __syncthreads();
-  STAMP_ADD(ST_KERNEL, t_k);
-  unsigned long long t_epi = STAMP_T();
-
-  // ---- work counters (accumulated across launches; one workgroup owns row ci)
-  {
-    __shared__ int s_cnt[NW][8];
-    if (l == 0) {
-      s_cnt[w][0] = n_xqp; s_cnt[w][1] = n_zqp; s_cnt[w][2] = n_admm_x; s_cnt[w][3] = n_admm_z;
-      s_cnt[w][4] = n_pdas_x; s_cnt[w][5] = n_pdas_z; s_cnt[w][6] = n_inexact; s_cnt[w][7] = 0;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long* cn = A.counters + (size_t)ci * 8;
-      cn[0] += (unsigned long long)(skip ? 0 : iters - it0);
-      for (int k = 0; k < 6; ++k) {
-        unsigned long long sum = 0;
-        for (int ww = 0; ww < NW; ++ww) sum += (unsigned long long)s_cnt[ww][k];
-        cn[k + 1] += sum;
-      }
-      unsigned long long inex = 0;
-      for (int ww = 0; ww < NW; ++ww) inex += (unsigned long long)s_cnt[ww][6];
-      cn[7] += inex;
-    }
-  }
-  // ---- state of this launch (every launch) and outputs / propagation (LAST, casadi/main.py:185-192)
-  if (threadIdx.x == 0) {
-    A.iters[ci] = iters;
-    if (e >= 0) {
-      A.edge_active[e] = act ? 1 : 0;
-      A.dischk[e] = dis_chk;
-    }
-    A.cst[(size_t)ci * 4 + 0] = flag;
-    A.cst[(size_t)ci * 4 + 1] = aliased;
-    A.cst[(size_t)ci * 4 + 3] = stopped ? 1 : 0;
-    if (coop && ci == 0) A.giters[slot] = iters;
-    if (nanlast && iters > 0 && !skip) {      // global stop at the collision test of this iteration
-      resid[2 * (iters - 1) + 0] = NAN;
-      resid[2 * (iters - 1) + 1] = NAN;
-    }
-  }
-  {
-    __shared__ int s_warm;
-    if (threadIdx.x == 0) s_warm = 0;
-    __syncthreads();
-    if (l == 0 && w < na && warm_x) atomicOr(&s_warm, 1 << w);
-    if (l == 0 && w == 0 && e >= 0 && warm_e) atomicOr(&s_warm, 4);
-    __syncthreads();
-    if (threadIdx.x == 0) A.cst[(size_t)ci * 4 + 2] = s_warm;
-  }
-  if (w < na) {
-    const int a = a0 + w;
-    // the last executed iteration's buffer (a skipped launch: the buffer its state was restored to)
-    const double* posl = S.pos + ((skip ? it0 - 1 : iters - 1) & 1) * 4 * H1;
-    for (int i = l; i < 2 * H1; i += WAVE) A.pos_old[(size_t)a * 2 * H1 + i] = posl[w * 2 * H1 + i];
-    const double u = (l < H) ? S.u[w * H + l] : 0.0;
-    if (l < H) A.u[(size_t)a * H + l] = u;
-    if (l == 0) {
-      A.status[a] = status_x;
-      A.rho_x[a] = qx.rho;
-    }
-    if (__builtin_expect(A.xcache_rho[a] != qx.rho, 0)) {   // adaptive rho rebuilt K_s^-1: refresh the cache
-      double* Kc = A.Kx_cache + (size_t)a * H * H;
-      if (qx.kf32) {
-        for (int i = l; i < H * H; i += WAVE) Kc[i] = (double)qx.Kf[i];   // the fp32 image
-      } else if (qx.K != Kc) {
-        for (int i = l; i < H * H; i += WAVE) Kc[i] = qx.K[i];
-      }
-      if (l == 0) A.xcache_rho[a] = qx.rho;
-    }
-    if (!last_launch) {
-      if (qx.wraw) warm_to_scaled(qx, xs_x, zs_x, ys_x);
-      double* qs = A.qs_x + (size_t)a * 5 * WAVE;
-      signed char* ql = A.ql_x + (size_t)a * 2 * WAVE;
-      qs[l] = xs_x[0];
-      qs[WAVE + l] = zs_x[0];
-      qs[2 * WAVE + l] = zs_x[1];
-      qs[3 * WAVE + l] = ys_x[0];
-      qs[4 * WAVE + l] = ys_x[1];
-      ql[l] = lab_x[0];
-      ql[WAVE + l] = lab_x[1];
-    } else {
-      double px, py, pth;
-      rollout(S.xt + 3 * w, A.spd[a], u, c, H, true, px, py, pth);
-      if (l == 1) {
-        A.xt[3 * a + 0] = px;
-        A.xt[3 * a + 1] = py;
-        A.xt[3 * a + 2] = pth;
-      }
-      if (l == 0) A.warm_ok[a] = 1;
-      if (l < HCAP) {
-        signed char* lb = A.lab_x + (size_t)a * 2 * HCAP;
-        lb[l] = lab_x[0];
-        lb[HCAP + l] = lab_x[1];
-      }
-    }
-  }
-  if (w == 0 && e >= 0) {
+  n.warm = e >= 0 && warm_e;
+  if (e >= 0) {
     if (l == 0) A.rho_e[e] = qe.rho;
-    if (!last_launch) {
+    if (!X.last_launch) {
       if (qe.wraw) warm_to_scaled(qe, xs_e, zs_e, ys_e);
       double* qs = A.qs_e + (size_t)e * 12 * WAVE;
       signed char* ql = A.ql_e + (size_t)e * 5 * WAVE;
@@ -697,13 +637,183 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
         ql[s * WAVE + l] = lab_e[s];
       }
     }
+    if (l == 0) A.status[A.N + e] = status_e;
+  }
+}
+
+// One launch runs outer iterations [it0, it1) of MPC step t for every component (one
+// workgroup each).  The fused mode is one launch (0, max_outer, FIRST | LAST); the global
+// termination mode (term_global, reference quirk B9) runs one launch per outer iteration,
+// with the per-step state carried in HBM between launches (restore / save below) and the
+// stop decision taken by the host from all-reduced partials, then a LAST launch with no
+// iterations for the outputs and the propagation.
+// Wave layout: waves 0 and 1 run the agents' x-steps (agent_part), wave 2 the pair
+// (pair_part); the two loops take the same barriers and stop decisions.
+template <bool BIG>
+__device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
+                                              int& nbar) {
+  extern __shared__ double lds[];
+  __shared__ int s_int[NWT * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
+  const piadmm_config_t& c = A.cfg;
+  StepCtx X;
+  X.H = c.H;
+  X.H1 = c.H + 1;
+  X.ci = blockIdx.x;
+  X.w = threadIdx.x >> 6;
+  X.l = lid();
+  X.t = t;
+  X.slot = slot;
+  X.a0 = A.comp_ptr[X.ci];
+  X.na = A.comp_ptr[X.ci + 1] - X.a0;
+  X.e = A.comp_edge[X.ci];
+  X.big = BIG;
+  X.f32 = c.precision == 1;
+  const int H = X.H, H1 = X.H1, ci = X.ci, e = X.e, na = X.na, a0 = X.a0;
+
+  // ---- LDS carve (lds_bytes() in piadmm_internal.h): the matrix regions are carved by the parts
+  double* vec_all;
+  if (!BIG) {
+    vec_all = lds + (X.f32 ? kxf_words(H) : 2 * H * H) + 2 * (H * H + H) + (X.f32 ? 2 * H * H : 4 * H * H) +
+              64 * LD + NW * HMAX * (HMAX + 1) + NW * (HMAX + 1) * XLD;   // NWT x 512
+  } else {
+    vec_all = lds + 64 * LD + NW * xrows(H) * (xrows(H) + 1);             // NWT x 512
+  }
+  X.vec_all = vec_all;
+  double* fdiag_all = vec_all + NWT * 512;               // NWT x 128
+  CompLds& S = X.S;
+  S.pos = fdiag_all + NWT * 128;
+  S.xt = S.pos + 8 * H1;   // pos_old double-buffered by outer-iteration parity
+  S.seed = S.xt + 6;
+  S.u = S.seed + 4;
+  S.hat = S.u + 2 * H;
+  S.lam = S.hat + 4 * H1;
+  S.S = S.lam + 4 * H1;
+  S.D = S.S + 4 * H1;
+  S.last = S.D + 4 * H1;
+  S.sc = S.last + 4 * H1;
+  X.wm = WaveMem{vec_all + X.w * 512, s_int + X.w * 272};
+
+  X.first = (flags & F_FIRST) != 0;
+  X.last_launch = (flags & F_LAST) != 0;
+  X.global = (flags & F_GLOBAL) != 0;
+  X.coop = (flags & F_COOP) != 0;   // global stop decided in-kernel (cooperative launch)
+  X.it0 = it0;
+  const bool first = X.first;
+  // a component whose step already ended in an earlier launch of this step (per-component stop,
+  // host-stepped by piadmm_outer_iter) runs no further iteration: its state is only carried
+  X.skip = !first && A.cst[(size_t)ci * 4 + 3] != 0;
+  X.it_end = X.skip ? it0 : it1;
+  // ---- seeds (casadi/main.py:48-49) and zero per-step state (:52-63)
+  if ((int)threadIdx.x < na) {
+    const int a = a0 + threadIdx.x;
+    const double x = A.xt[3 * a], y = A.xt[3 * a + 1], th = A.xt[3 * a + 2], s = A.spd[a];
+    S.xt[3 * threadIdx.x + 0] = x;
+    S.xt[3 * threadIdx.x + 1] = y;
+    S.xt[3 * threadIdx.x + 2] = th;
+    S.seed[2 * threadIdx.x + 0] = around(x + c.dt * s * cos(th), c.round_decimals);
+    S.seed[2 * threadIdx.x + 1] = around(y + c.dt * s * sin(th), c.round_decimals);
+  }
+  for (int i = threadIdx.x; i < 32; i += blockDim.x) S.sc[i] = 0.0;
+  {
+    double* const edge_lds[5] = {S.hat, S.lam, S.S, S.D, S.last};
+    double* const edge_hbm[5] = {A.hat, A.lam, A.Sacc, A.Dacc, A.last};
+    if (first) {
+      for (int i = threadIdx.x; i < 8 * H1; i += blockDim.x) S.pos[i] = 0.0;
+      // casadi/main.py:52-63 resets hat, lam (and the PI accumulators) every MPC step; with
+      // warm_duals they continue from the previous step shifted by one slot (a12)
+      for (int k = 0; k < 5; ++k)
+        for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) {
+          double v = 0.0;
+          if (e >= 0 && c.warm_duals) {
+            const int r = i / H1, tt = i - r * H1;
+            v = edge_hbm[k][(size_t)e * 4 * H1 + r * H1 + min(tt + 1, H)];
+          }
+          edge_lds[k][i] = v;
+        }
+    } else {
+      // state of the previous launch of this step
+      for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
+        S.pos[((it0 - 1) & 1) * 4 * H1 + i] = (i < na * 2 * H1) ? A.pos_old[(size_t)a0 * 2 * H1 + i] : 0.0;
+      for (int i = threadIdx.x; i < na * H; i += blockDim.x) S.u[i] = A.u[(size_t)a0 * H + i];
+      for (int k = 0; k < 5; ++k)
+        for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
+          edge_lds[k][i] = (e >= 0) ? edge_hbm[k][(size_t)e * 4 * H1 + i] : 0.0;
+    }
+  }
+  __syncthreads();
+  // pair safety distance (a13 tightening from the step's start states, else dis_thres)
+  X.deff = c.dis_thres;
+  if (e >= 0 && c.tighten && na == 2)
+    X.deff = c.dis_thres + delay_norm(c, S.xt[2], A.spd[a0]) + delay_norm(c, S.xt[5], A.spd[a0 + 1]);
+  X.thr = c.collide_sq_thres ? X.deff * X.deff : X.deff;
+  X.resid = A.resid + ((size_t)slot * A.C + ci) * c.max_outer * 2;   // slot: step of the launch
+  if (first)
+    for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) X.resid[i] = NAN;   // "not evaluated"
+  if (X.coop && ci == 0)
+    for (int i = threadIdx.x; i < 2 * c.max_outer; i += blockDim.x) A.ghist[(size_t)slot * 2 * c.max_outer + i] = NAN;
+  unsigned long long t_k = STAMP_T();
+
+  LoopCtl L;
+  L.flag = first ? 0 : A.cst[(size_t)ci * 4 + 0];
+  L.aliased = first ? 0 : A.cst[(size_t)ci * 4 + 1];
+  L.iters = X.skip ? A.iters[ci] : it0;
+  L.gflag = 0;               // coop: some pair ever collided (casadi/main.py:115)
+  L.stopped = X.skip;
+  L.nanlast = (flags & F_NANLAST) != 0;
+  L.act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
+  L.dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
+  WaveCnt n;
+  if (X.w < NW) agent_part<BIG>(A, X, L, nbar, n);
+  else pair_part<BIG>(A, X, L, nbar, n);
+  __syncthreads();
+  STAMP_ADD(ST_KERNEL, t_k);
+  unsigned long long t_epi = STAMP_T();
+
+  // ---- work counters (accumulated across launches; one workgroup owns row ci) and the
+  // component's state of this launch (every launch)
+  {
+    __shared__ int s_cnt[NWT][8];
+    __shared__ int s_warm;
+    if (threadIdx.x == 0) s_warm = 0;
+    if (X.l == 0) {
+      s_cnt[X.w][0] = n.xqp; s_cnt[X.w][1] = n.zqp; s_cnt[X.w][2] = n.admm_x; s_cnt[X.w][3] = n.admm_z;
+      s_cnt[X.w][4] = n.pdas_x; s_cnt[X.w][5] = n.pdas_z; s_cnt[X.w][6] = n.inexact; s_cnt[X.w][7] = 0;
+    }
+    __syncthreads();
+    if (X.l == 0 && n.warm) atomicOr(&s_warm, X.w < NW ? (1 << X.w) : 4);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long* cn = A.counters + (size_t)ci * 8;
+      cn[0] += (unsigned long long)(X.skip ? 0 : L.iters - it0);
+      for (int k = 0; k < 6; ++k) {
+        unsigned long long sum = 0;
+        for (int ww = 0; ww < NWT; ++ww) sum += (unsigned long long)s_cnt[ww][k];
+        cn[k + 1] += sum;
+      }
+      unsigned long long inex = 0;
+      for (int ww = 0; ww < NWT; ++ww) inex += (unsigned long long)s_cnt[ww][6];
+      cn[7] += inex;
+      A.iters[ci] = L.iters;
+      if (e >= 0) {
+        A.edge_active[e] = L.act ? 1 : 0;
+        A.dischk[e] = L.dis_chk;
+      }
+      A.cst[(size_t)ci * 4 + 0] = L.flag;
+      A.cst[(size_t)ci * 4 + 1] = L.aliased;
+      A.cst[(size_t)ci * 4 + 2] = s_warm;
+      A.cst[(size_t)ci * 4 + 3] = L.stopped ? 1 : 0;
+      if (X.coop && ci == 0) A.giters[slot] = L.iters;
+      if (L.nanlast && L.iters > 0 && !X.skip) {   // global stop at the collision test of this iteration
+        X.resid[2 * (L.iters - 1) + 0] = NAN;
+        X.resid[2 * (L.iters - 1) + 1] = NAN;
+      }
+    }
   }
   if (e >= 0) {
     double* const edge_lds[5] = {S.hat, S.lam, S.S, S.D, S.last};
     double* const edge_hbm[5] = {A.hat, A.lam, A.Sacc, A.Dacc, A.last};
     for (int k = 0; k < 5; ++k)
       for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x) edge_hbm[k][(size_t)e * 4 * H1 + i] = edge_lds[k][i];
-    if (threadIdx.x == 0) A.status[A.N + e] = status_e;
   }
   STAMP_ADD(ST_RED_X, t_epi);
 }
@@ -716,7 +826,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 // sum_t max_c.  The step-to-step state (xt, labels, caches) goes through HBM inside one
 // workgroup (same CU: the barrier's workgroup-scope fences order it).
 template <bool BIG>
-__global__ void __launch_bounds__(NW * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
+__global__ void __launch_bounds__(NWT * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
 #ifdef PIADMM_STAMPS
   if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
   __syncthreads();
@@ -833,13 +943,13 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     DevArgs aa = a;
     void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
     (void)hipGetLastError();
-    return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NW * WAVE), args, (unsigned)sh, s));
+    return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NWT * WAVE), args, (unsigned)sh, s));
   }
   (void)hipGetLastError();   // a stale error of an earlier runtime call is not this launch's
   if (big)
-    hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
+    hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(NWT * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
   else
-    hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(NW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
+    hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(NWT * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
   return launch_rc(hipGetLastError());
 }
 
@@ -853,7 +963,7 @@ bool coop_fits(const DevArgs& a, int device) {
   const bool big = a.cfg.H > HMAX;
   const void* fn = big ? (const void*)k_mpc_step<true> : (const void*)k_mpc_step<false>;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NW * WAVE, sh) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NWT * WAVE, sh) != hipSuccess) return false;
   return (long long)per * ncu >= (long long)a.C;
 }
 

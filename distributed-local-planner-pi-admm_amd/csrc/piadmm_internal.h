@@ -14,7 +14,9 @@ inline int launch_rc(hipError_t e) {
 
 
 constexpr int WAVE = 64;
-constexpr int NW = 2;        // waves per workgroup = agents per component (max)
+constexpr int NW = 2;        // agent waves per workgroup of k_mpc_step = agents per component (max)
+constexpr int PW = NW;       // the pair's wave (k_mpc_step): its own loop, registers and LDS vectors
+constexpr int NWT = NW + 1;  // waves per workgroup of k_mpc_step
 constexpr int HCAP = 64;     // storage stride of per-lane state: lane k <-> time index k, H <= 63
 constexpr int HMAX = 32;     // largest H of the all-in-LDS layout ("LDS mode")
 constexpr int HBIG = 63;     // largest H supported (matrices in HBM / L2 beyond HMAX: "big mode")
@@ -125,7 +127,7 @@ struct DevArgs {
 // a degenerate vertex can hold one or two dependent rows beyond the H variables).
 constexpr int xrows(int H) { return H + 2 < 64 ? H + 2 : 64; }
 // LDS the kernel declares statically (s_int, s_cnt, s_warm) on top of lds_bytes().
-constexpr size_t STATIC_LDS = NW * 272 * 4 + NW * 8 * 4 + 16;
+constexpr size_t STATIC_LDS = NWT * 272 * 4 + NWT * 8 * 4 + 16;
 constexpr size_t MAX_LDS = 160 * 1024;
 
 // fp32 agent K_s^-1 images in LDS mode: per wave H*H floats rounded up to an even count, so
@@ -151,8 +153,8 @@ inline size_t lds_bytes(int H, int precision = 0) {
     d += 64 * LD;                    // pair matrix scratch (wave 0)
     d += NW * (size_t)xrows(H) * (xrows(H) + 1);   // per-wave x-step scratch / Cholesky factor
   }
-  d += NW * 512;                   // per-wave vector buffers
-  d += NW * 256;                   // per-wave factor diagonals (x, z)
+  d += NWT * 512;                  // per-wave vector buffers (agents, pair)
+  d += NWT * 128;                  // per-wave factor diagonals (x-step or pair)
   size_t H1 = H + 1;
   d += 2 * 2 * 2 * H1;             // pos_old (two buffers: outer-iteration parity)
   d += 2 * 3 + 2 * 2 + 2 * H;      // xt, seeds, u
