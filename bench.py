@@ -69,7 +69,6 @@ WORKLOADS = {
                desc="256 agents x H30 per GPU (64 four-vehicle all-pairs crossings, 384 candidate pairs), "
                     "matlab_pi preset"),
     "ch": dict(tiles=1024, H=30, preset="matlab_pi", max_outer=100, tighten=0, scaling="weak", kind="chain",
-               cpu_steps=2,
                desc="1024 agents x H30 per GPU in ONE connected chain (1023 candidate pairs; the component spans "
                     "256 workgroups of 4 agents), matlab_pi preset"),
 }
@@ -155,8 +154,8 @@ def cpu_baseline(wl: dict, budget_s: float, K: int) -> dict:
     cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=1, max_outer=wl["max_outer"], tighten=wl["tighten"],
                                         term_global=1)
     kind = wl.get("kind", "tiles")
-    K = wl.get("cpu_steps", K)      # a bounded sample of the job's steps (a single-component chain
-                                    # runs on one host thread: OpenMP is over components)
+    K = wl.get("cpu_steps", K)      # a bounded sample of the job's steps (the chain: all of the timed
+                                    # steps -- later steps are harder, so a 2-step sample flattered the CPU)
     bopt = pool = None
     try:
         from oracle import cpu_bopt

@@ -1189,7 +1189,9 @@ constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t
 #endif
 template <int NV>
 __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, signed char* lab, double* x, double* y,
-                                         int& nsteps, signed char* flab = nullptr) {
+                                         int& nsteps, signed char* flab = nullptr, bool use_wlab = true) {
+  // (use_wlab = false: a cold start although wlab points at labels -- a flag, not a null
+  // pointer selected at the call site, so that the caller's label array stays in registers)
   constexpr int NR = QP<NV>::NR;
   const int l = lid(), H = P.H, ld = P.fld, H2 = NV * H;
   double* vb_ax = P.vb + 192;      // [192, 192 + NR*H): (A v) by row id
@@ -1421,7 +1423,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       }
       warm = true;
     }
-  } else if (wlab) {
+  } else if (wlab && use_wlab) {
     // ---- x-step: the rows the current labels hold at a bound
 #pragma unroll
     for (int s = 0; s < NR; ++s) {
@@ -1733,7 +1735,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         int ngi = 0;
         signed char glab[NR];
         ensure_q(P);
-        if (gi_solve(P, gi_first >= 2 ? nullptr : flab, glab, x, y, ngi)) {
+        if (gi_solve(P, flab, glab, x, y, ngi, nullptr, gi_first < 2)) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = glab[s];
           // the dual active set's own answer (exact solve of its final working set + one step
