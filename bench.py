@@ -524,6 +524,14 @@ def main():
             bound = 4.0 * sq["valu_insts_per_wave_iter"]
             lat["issue_bound_cycles"] = bound
             lat["frac"] = bound / cyc_iter
+            if sq.get("waves", 0) > 2 * m["C"]:
+                # three waves per component (two agent waves + the pair wave, which mostly waits at
+                # the barriers): the VALU work is the agent waves', so their issue bound is 3/2 of
+                # the average over all waves
+                nw = sq["waves"] / max(m["C"], 1)
+                lat["waves_per_component"] = nw
+                lat["issue_bound_cycles_agent_wave"] = bound * nw / 2.0
+                lat["frac_agent_wave"] = bound * nw / 2.0 / cyc_iter
         lat["source"] = sq["_file"]
         if "fp64_flops_per_step" in sq:
             gf = sq["fp64_flops_per_step"] * K / (m["ev_ms"] / 1e3) / 1e9
