@@ -177,6 +177,29 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GW
 
 // -------------------------------------------------------------------- Z phase: one pair
 // Returns nothing; writes edge_active, and when the pair collides hat, lam, S, D, eres, dischk.
+// The collision test of pair e (casadi/main.py:110-113): writes edge_active, returns it.
+__device__ __forceinline__ bool g_ztest(const DevArgs& A, int e) {
+  const piadmm_config_t& c = A.cfg;
+  const int H = c.H, H1 = H + 1, l = lid();
+  const bool tl = l <= H;
+  const int v1 = A.edges[2 * e], v2 = A.edges[2 * e + 1];
+  const double* p1 = A.pos_old + (size_t)v1 * 2 * H1;
+  const double* p2 = A.pos_old + (size_t)v2 * 2 * H1;
+  const double deff = A.deff[e];
+  const double thr = c.collide_sq_thres ? deff * deff : deff;
+  bool hit = false;
+  if (tl) {
+    const double dx = p1[l] - p2[l], dy = p1[H1 + l] - p2[H1 + l];
+    hit = (dx * dx + dy * dy) < thr;
+  }
+  // the global-PI script has no collision test: its edge problem runs every iteration
+  const bool act = c.no_collision_gate ? true : wany(hit);
+  if (l == 0) A.edge_active[e] = act ? 1 : 0;
+  return act;
+}
+
+// The z-step of a colliding pair e: the pair QP, the hat rollouts, the dual update and the pair's
+// residual terms (casadi/main.py:121-173).
 template <bool BIG>
 __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GWave& W, GCnt& n) {
   const piadmm_config_t& c = A.cfg;
@@ -186,8 +209,6 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
   const double* p1 = A.pos_old + (size_t)v1 * 2 * H1;
   const double* p2 = A.pos_old + (size_t)v2 * 2 * H1;
   const double deff = A.deff[e];
-  const double thr = c.collide_sq_thres ? deff * deff : deff;
-  // collision test (casadi/main.py:110-113)
   double px[2] = {0.0, 0.0}, py[2] = {0.0, 0.0};
   if (tl) {
     px[0] = p1[l];
@@ -195,15 +216,6 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
     px[1] = p2[l];
     py[1] = p2[H1 + l];
   }
-  bool hit = false;
-  if (tl) {
-    const double dx = px[0] - px[1], dy = py[0] - py[1];
-    hit = (dx * dx + dy * dy) < thr;
-  }
-  // the global-PI script has no collision test: its edge problem runs every iteration
-  const bool act = c.no_collision_gate ? true : wany(hit);
-  if (l == 0) A.edge_active[e] = act ? 1 : 0;
-  if (!act) return;
   // pair QP of cost_function_edge (PI_ADMM_class.py:145-169), heading frozen at xt (B3)
   const double* xa = A.xt + 3 * v1;
   const double* xb = A.xt + 3 * v2;
@@ -525,6 +537,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   __shared__ int s_int[GW * 272];
   __shared__ double s_sc[8];
   __shared__ int s_cnt[GW][8];
+  __shared__ unsigned char s_zact[GZMAX];   // this iteration's collision flags (components of <= GZMAX pairs)
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, M = c.max_outer;
   const int ci = blockIdx.x;
@@ -623,40 +636,81 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
     }
     // -------- Z: collision test + pair QPs + dual updates (casadi/main.py:110-162)
     unsigned long long t_zp = STAMP_T();
-    for (int j = e0 + w; j < e1; j += GW) g_zstep<BIG>(A, A.comp_elist[j], t, W, n);
+    // the collision tests of every pair (waves strided), then the colliding pairs dealt round-robin
+    // over the waves in pair order: two colliding pairs never queue on one wave while the other
+    // waits at the barrier (pairs are independent within the phase; the residual sums below run in
+    // pair order whoever solved them).  Components of more than GZMAX pairs: strided, test + solve.
+    const bool deal = e1 - e0 <= GZMAX;
+    if (deal) {
+      for (int j = e0 + w; j < e1; j += GW) {
+        const bool act = g_ztest(A, A.comp_elist[j]);
+        if (l == 0) s_zact[j - e0] = act ? 1 : 0;
+      }
+      __syncthreads();
+    }
+    {
+      int k = 0;                                     // colliding pairs before j (pair order)
+      for (int j = deal ? e0 : e0 + w; j < e1; j += deal ? 1 : GW) {
+        const int e = A.comp_elist[j];
+        bool mine;
+        if (deal) {
+          const bool act = s_zact[j - e0] != 0;
+          mine = act && (k % GW == w);
+          k += act ? 1 : 0;
+        } else {
+          mine = g_ztest(A, e);
+        }
+        if (mine) g_zstep<BIG>(A, e, t, W, n);
+      }
+    }
     STAMP_ADD(ST_ZSTEP, t_zp);
     unsigned long long t_sb = STAMP_T();
     __syncthreads();
     STAMP_ADD(ST_SYNC_B, t_sb);
     unsigned long long t_tm = STAMP_T();
     // -------- T: the component's residuals in pair order and the stop rules (:164-181)
-    if (threadIdx.x == 0) {
-      double rk = 0.0, sk = 0.0, nact = 0.0, nseen = 0.0, nbad = 0.0;
-      for (int j = e0; j < e1; ++j) {
-        const int e = A.comp_elist[j];
-        if (A.counted && !A.counted[e]) continue;    // a cross-rank pair counts on one rank only
-        const double d = A.dischk[e];
-        if (d == d) {
-          nseen += 1.0;
-          nbad += (d > A.deff[e]) ? 0.0 : 1.0;
+    double prk = 0.0, psk = 0.0, pact = 0.0, pseen = 0.0, pbad = 0.0;
+    if (w == 0) {
+      // lane k loads pair e0 + k's terms (one memory latency for up to 64 pairs, not one per pair);
+      // the sums then run in pair order through readlanes -- the order of casadi/main.py:165-173
+      // and of the oracle, so the residuals are the sequential sums
+      for (int j0 = e0; j0 < e1; j0 += WAVE) {
+        const int j = j0 + l;
+        const bool in = j < e1;
+        const int e = in ? A.comp_elist[j] : 0;
+        const bool cnt = in && (!A.counted || A.counted[e]);   // a cross-rank pair counts on one rank only
+        const double d = cnt ? A.dischk[e] : 0.0;
+        const bool seen = cnt && (d == d);
+        const bool bad = seen && !(d > A.deff[e]);
+        const bool act = cnt && A.edge_active[e] != 0;
+        const double r0 = act ? A.eres[2 * e] : 0.0, r1 = act ? A.eres[2 * e + 1] : 0.0;
+        const unsigned long long bseen = __ballot(seen), bbad = __ballot(bad), bact = __ballot(act);
+        const int npr = min(WAVE, e1 - j0);
+        for (int k = 0; k < npr; ++k) {
+          if ((bseen >> k) & 1ull) {
+            pseen += 1.0;
+            pbad += ((bbad >> k) & 1ull) ? 1.0 : 0.0;
+          }
+          if (!((bact >> k) & 1ull)) continue;
+          pact += 1.0;
+          if (!aliased) psk += rdl(r1, k);
+          prk += rdl(r0, k);
         }
-        if (!A.edge_active[e]) continue;
-        nact += 1.0;
-        if (!aliased) sk += A.eres[2 * e + 1];
-        rk += A.eres[2 * e];
       }
-      const bool anyact = nact > 0.0;
+    }
+    if (threadIdx.x == 0) {
+      const bool anyact = pact > 0.0;
       double* cp = A.cpart + (size_t)ci * 5;
-      cp[0] = rk;
-      cp[1] = sk;
-      cp[2] = nact;
-      cp[3] = nseen;
-      cp[4] = nbad;
-      s_sc[0] = rk;
-      s_sc[1] = sk;
+      cp[0] = prk;
+      cp[1] = psk;
+      cp[2] = pact;
+      cp[3] = pseen;
+      cp[4] = pbad;
+      s_sc[0] = prk;
+      s_sc[1] = psk;
       s_sc[2] = anyact ? 1.0 : 0.0;
-      s_sc[3] = nseen;
-      s_sc[4] = nbad;
+      s_sc[3] = pseen;
+      s_sc[4] = pbad;
     }
     __syncthreads();
     const double rk = s_sc[0], sk = s_sc[1];
