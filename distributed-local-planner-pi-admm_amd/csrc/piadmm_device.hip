@@ -40,6 +40,9 @@ struct StepCtx {
   double* resid;
   double* vec_all;
   WaveMem wm;
+  bool spec;        // the speculative loop shape (agent_part)
+  int* vd;          // the pair wave's verdict on an iteration (speculative loop): act, stop, flag, aliased
+  double* vdd;      // and dis_chk
 };
 
 // The outer loop's control state.  Every wave keeps its own copy and updates it from the same
@@ -274,13 +277,31 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     }
   };
   load_cp();
-  for (int it = X.it0; it < X.it_end; ++it) {
-    L.iters = it + 1;
+  // Two loop shapes (the same barriers and decisions in every wave):
+  //  * speculative (no in-kernel grid barrier): the pair wave rolls the agents' controls out, runs
+  //    the collision test, the z-step and the stop decision for iteration it, while the agent waves
+  //    already solve iteration it+1's x-step.  That x-step's QP depends only on hat and lam, which
+  //    change only in a z-step, so when iteration it had no colliding pair it IS iteration it+1's
+  //    x-step and is kept; after a z-step (or a stop) it is discarded and, if the loop goes on,
+  //    solved again with the new consensus term.  Barriers per iteration: A (this iteration's
+  //    controls are in U) and B (the pair wave's verdict); the rollout and the test leave the
+  //    agents' dependent chain.
+  //  * in-kernel global termination (coop): every wave takes part in the grid barrier of the stop
+  //    test, so the agents roll out their own controls and every wave runs the collision test
+  //    (barrier A, then B only after a z-step).
+  const bool specm = X.spec;
+  bool have = false;          // the x-step of iteration `it` is already in U (a kept speculation)
+  int spec_st = 0;
+  int it = X.it0, phase = 0;  // phase 0: before barrier A(it); 1: before barrier B(it)
+  while (it < X.it_end) {
+    if (phase == 0) L.iters = it + 1;
+    const int tgt = phase == 0 ? it : it + 1;         // the iteration this x-step belongs to
+    const bool dox = own && (phase == 0 ? !have : (specm && it + 1 < X.it_end));
     // this iteration's pos_old buffer: a wave may start the next iteration's x-step while
     // another still reads this one's positions (no second barrier without a z-step)
-    double* const pos = S.pos + (it & 1) * 4 * H1;
+    double* const pos = S.pos + (tgt & 1) * 4 * H1;
     // -------- x-step (casadi/main.py:81-106)
-    if (own) {
+    if (dox) {
       unsigned long long t_xs = STAMP_T();
       const bool tl = l <= H;
       double vx = 2.0 * c.Pnorm * (cx_own - rx_own), vy = 2.0 * c.Pnorm * (cy_own - ry_own);
@@ -296,43 +317,79 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
-                               qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && it == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
+                               qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && tgt == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
-      status_x |= stx;
-      ++n.xqp;
-      n.inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
+      if (phase == 0) {
+        status_x |= stx;
+        ++n.xqp;
+        n.inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
+      } else {
+        spec_st = stx;                                 // counted if kept
+      }
       warm_x = true;
       unsigned long long t_rd = STAMP_T();
       const double u = around(ustar[0], c.round_decimals);
       STAMP_ADD(ST_ROUND, t_rd);
-      double px, py, pth;
-      unsigned long long t_r = STAMP_T();
-      rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
-      STAMP_ADD(ST_XROLL, t_r);
-      if (l <= H) {
-        pos[(w * 2 + 0) * H1 + l] = px;
-        pos[(w * 2 + 1) * H1 + l] = py;
+      if (!specm) {
+        double px, py, pth;
+        unsigned long long t_r = STAMP_T();
+        rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+        STAMP_ADD(ST_XROLL, t_r);
+        if (l <= H) {
+          pos[(w * 2 + 0) * H1 + l] = px;
+          pos[(w * 2 + 1) * H1 + l] = py;
+        }
       }
-      if (l < H) S.u[w * H + l] = u;
+      if (l < H) S.u[(tgt & 1) * 2 * H + w * H + l] = u;
       STAMP_ADD(ST_XSTEP, t_xs);
     }
+    if (phase == 0 && have && own) {                   // the kept speculation counts now
+      status_x |= spec_st;
+      ++n.xqp;
+      n.inexact += (spec_st & PIADMM_QP_INEXACT) ? 1 : 0;
+    }
     unsigned long long t_sa = STAMP_T();
-    __syncthreads();                                     // A: every agent's positions
-    STAMP_ADD(ST_SYNC_A, t_sa);
-    L.act = collide(X, pos);
-    if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
+    __syncthreads();                                     // A(it) or, speculative phase 1, B(it)
+    STAMP_ADD(phase == 0 ? ST_SYNC_A : ST_SYNC_B, t_sa);
+    if (!specm) {
+      L.act = collide(X, pos);
+      if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
+        L.stopped = true;
+        break;
+      }
+      L.flag = 1;
+      // (the pair wave runs the z-step and records the residuals now)
+      unsigned long long t_sb = STAMP_T();
+      if (__builtin_expect(L.act, 0)) {
+        __syncthreads();                                 // B: hat, lam, S, D, last, S.sc
+        load_cp();
+      }
+      STAMP_ADD(ST_SYNC_B, t_sb);
+      if (iter_tail(A, X, L, it, nbar)) break;
+      ++it;
+      continue;
+    }
+    if (phase == 0) {
+      phase = 1;
+      continue;
+    }
+    // barrier B(it): the pair wave's verdict on iteration it
+    L.act = X.vd[0] != 0;
+    L.flag = X.vd[2];
+    L.aliased = X.vd[3];
+    L.dis_chk = *X.vdd;
+    if (X.vd[1]) {
       L.stopped = true;
       break;
     }
-    L.flag = 1;
-    // (the pair wave runs the z-step and records the residuals now)
-    unsigned long long t_sb = STAMP_T();
     if (__builtin_expect(L.act, 0)) {
-      __syncthreads();                                   // B: hat, lam, S, D, last, S.sc
-      load_cp();
+      load_cp();                                         // the speculation used the old hat, lam
+      have = false;
+    } else {
+      have = it + 1 < X.it_end;
     }
-    STAMP_ADD(ST_SYNC_B, t_sb);
-    if (iter_tail(A, X, L, it, nbar)) break;
+    ++it;
+    phase = 0;
   }
   n.warm = own && warm_x;
   // ---- the agent's state of this launch and, in the last launch, outputs and propagation
@@ -342,7 +399,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     // the last executed iteration's buffer (a skipped launch: the buffer its state was restored to)
     const double* posl = S.pos + ((X.skip ? X.it0 - 1 : L.iters - 1) & 1) * 4 * H1;
     for (int i = l; i < 2 * H1; i += WAVE) A.pos_old[(size_t)a * 2 * H1 + i] = posl[w * 2 * H1 + i];
-    const double u = (l < H) ? S.u[w * H + l] : 0.0;
+    const double u = (l < H) ? S.u[((X.skip ? X.it0 - 1 : L.iters - 1) & 1) * 2 * H + w * H + l] : 0.0;
     if (l < H) A.u[(size_t)a * H + l] = u;
     if (l == 0) {
       A.status[a] = status_x;
@@ -485,15 +542,52 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
   }
   __syncthreads();
 
+  // speculative loop shape (agent_part): this wave also rolls the agents' controls out and
+  // publishes the iteration's verdict (X.vd) before barrier B
+  const bool specm = X.spec;
+  // the agents' start states and speeds (the per-iteration rollouts of the speculative shape)
+  double ra_s[2] = {0.0, 0.0};
+  if (specm)
+    for (int v = 0; v < X.na; ++v) ra_s[v] = A.spd[X.a0 + v];
   for (int it = X.it0; it < X.it_end; ++it) {
     L.iters = it + 1;
     double* const pos = S.pos + (it & 1) * 4 * H1;
     unsigned long long t_sa = STAMP_T();
-    __syncthreads();                                     // A: every agent's positions
+    __syncthreads();                                     // A: every agent's positions / controls
     STAMP_ADD(ST_SYNC_A, t_sa);
+    if (specm) {
+      // pos_old = dynamic_update_local of the rounded controls (casadi/main.py:105), per agent
+      // both agents' rollouts side by side (two independent DPP-scan / sincos chains in one block,
+      // so their latencies overlap; a single-agent component's second one is discarded)
+      const bool nonlin_pos = c.pos_model != 0;
+      double px[2], py[2], pth[2];
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const bool va = v < X.na;
+        const double u = (l < H && va) ? S.u[(it & 1) * 2 * H + v * H + l] : 0.0;
+        rollout_r(va ? S.xt[3 * v + 0] : 0.0, va ? S.xt[3 * v + 1] : 0.0, va ? S.xt[3 * v + 2] : 0.0, ra_s[v],
+                  ra_s[v] / c.L, u, c, H, nonlin_pos, px[v], py[v], pth[v]);
+      }
+      if (l <= H)
+        for (int v = 0; v < X.na; ++v) {
+          pos[(v * 2 + 0) * H1 + l] = px[v];
+          pos[(v * 2 + 1) * H1 + l] = py[v];
+        }
+      wsync();
+    }
     L.act = collide(X, pos);
     if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
       L.stopped = true;
+      if (specm) {
+        if (l == 0) {
+          X.vd[0] = 0;
+          X.vd[1] = 1;
+          X.vd[2] = L.flag;
+          X.vd[3] = L.aliased;
+          *X.vdd = L.dis_chk;
+        }
+        __syncthreads();                                 // B: the verdict
+      }
       break;
     }
     L.flag = 1;
@@ -615,6 +709,23 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
         for (int i = l; i < 4 * H1; i += WAVE) S.last[i] = S.hat[i];
       STAMP_ADD(ST_TERMW, t_tw);
     }
+    if (specm) {
+      // the stop decision here (iter_tail without a grid barrier), published with the iteration's
+      // flags before barrier B; the agents adopt it from X.vd
+      const bool stop = iter_tail(A, X, L, it, nbar);
+      if (l == 0) {
+        X.vd[0] = L.act ? 1 : 0;
+        X.vd[1] = stop ? 1 : 0;
+        X.vd[2] = L.flag;
+        X.vd[3] = L.aliased;
+        *X.vdd = L.dis_chk;
+      }
+      unsigned long long t_sb = STAMP_T();
+      __syncthreads();                                   // B: the verdict (and the z-step's state)
+      STAMP_ADD(ST_SYNC_B, t_sb);
+      if (stop) break;
+      continue;
+    }
     unsigned long long t_sb = STAMP_T();
     if (__builtin_expect(L.act, 0)) __syncthreads();     // B
     STAMP_ADD(ST_SYNC_B, t_sb);
@@ -654,8 +765,12 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
                                               int& nbar) {
   extern __shared__ double lds[];
   __shared__ int s_int[NWT * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
+  __shared__ int s_vd[4];
+  __shared__ double s_vdd;
   const piadmm_config_t& c = A.cfg;
   StepCtx X;
+  X.vd = s_vd;
+  X.vdd = &s_vdd;
   X.H = c.H;
   X.H1 = c.H + 1;
   X.ci = blockIdx.x;
@@ -684,8 +799,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   S.pos = fdiag_all + NWT * 128;
   S.xt = S.pos + 8 * H1;   // pos_old double-buffered by outer-iteration parity
   S.seed = S.xt + 6;
-  S.u = S.seed + 4;
-  S.hat = S.u + 2 * H;
+  S.u = S.seed + 4;         // agent controls, double-buffered by outer-iteration parity (2 x 2H)
+  S.hat = S.u + 4 * H;
   S.lam = S.hat + 4 * H1;
   S.S = S.lam + 4 * H1;
   S.D = S.S + 4 * H1;
@@ -697,6 +812,12 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   X.last_launch = (flags & F_LAST) != 0;
   X.global = (flags & F_GLOBAL) != 0;
   X.coop = (flags & F_COOP) != 0;   // global stop decided in-kernel (cooperative launch)
+  // the speculative loop shape where it pays: no grid barrier in the loop, and the nonlinear
+  // position model (MATLAB's dynamic_update_local, a sincos rollout per iteration) whose rollout
+  // is worth taking off the agents' chain -- measured: matlab_pi 256 x H30 0.534 -> 0.518 ms per
+  // step; the linearised model's cheap rollout does not pay for the second barrier
+  // (casadi_default 64 x H20 0.633 -> 0.677 ms)
+  X.spec = !X.coop && c.pos_model != 0;
   X.it0 = it0;
   const bool first = X.first;
   // a component whose step already ended in an earlier launch of this step (per-component stop,
@@ -734,7 +855,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
       // state of the previous launch of this step
       for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
         S.pos[((it0 - 1) & 1) * 4 * H1 + i] = (i < na * 2 * H1) ? A.pos_old[(size_t)a0 * 2 * H1 + i] : 0.0;
-      for (int i = threadIdx.x; i < na * H; i += blockDim.x) S.u[i] = A.u[(size_t)a0 * H + i];
+      for (int i = threadIdx.x; i < na * H; i += blockDim.x) S.u[((it0 - 1) & 1) * 2 * H + i] = A.u[(size_t)a0 * H + i];
       for (int k = 0; k < 5; ++k)
         for (int i = threadIdx.x; i < 4 * H1; i += blockDim.x)
           edge_lds[k][i] = (e >= 0) ? edge_hbm[k][(size_t)e * 4 * H1 + i] : 0.0;

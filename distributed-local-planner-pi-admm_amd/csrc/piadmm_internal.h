@@ -127,7 +127,7 @@ struct DevArgs {
 // a degenerate vertex can hold one or two dependent rows beyond the H variables).
 constexpr int xrows(int H) { return H + 2 < 64 ? H + 2 : 64; }
 // LDS the kernel declares statically (s_int, s_cnt, s_warm) on top of lds_bytes().
-constexpr size_t STATIC_LDS = NWT * 272 * 4 + NWT * 8 * 4 + 16;
+constexpr size_t STATIC_LDS = NWT * 272 * 4 + NWT * 8 * 4 + 16 + 4 * 4 + 8;
 constexpr size_t MAX_LDS = 160 * 1024;
 
 // fp32 agent K_s^-1 images in LDS mode: per wave H*H floats rounded up to an even count, so
@@ -157,7 +157,7 @@ inline size_t lds_bytes(int H, int precision = 0) {
   d += NWT * 128;                  // per-wave factor diagonals (x-step or pair)
   size_t H1 = H + 1;
   d += 2 * 2 * 2 * H1;             // pos_old (two buffers: outer-iteration parity)
-  d += 2 * 3 + 2 * 2 + 2 * H;      // xt, seeds, u
+  d += 2 * 3 + 2 * 2 + 4 * H;      // xt, seeds, u (two buffers: outer-iteration parity)
   d += 5 * 2 * 2 * H1;             // hat, lam, S, D, last_hat
   d += 32;                         // scalars
   if (H > HMAX && f32) d += 2 * (size_t)H * H + 2;   // big mode: fp32 image of the pair K_s^-1
@@ -173,6 +173,7 @@ constexpr int F_COOP = 16;    // global termination decided in-kernel (cooperati
 
 // Graph mode: LDS per workgroup of k_graph_step (GW waves, one component per workgroup).
 constexpr int GW = 2;
+constexpr int GZMAX = 1024;   // pairs per component whose colliding pairs are balanced over the waves
 // Dual active-set columns P^-1 n_a in LDS per wave (H <= HMAX; beyond, in HBM): the pair's
 // 2H-long columns (63 of them) or the x-step's H-long ones, in turn.
 constexpr int GYCAP = 63;
