@@ -290,16 +290,63 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
   //    test, so the agents roll out their own controls and every wave runs the collision test
   //    (barrier A, then B only after a z-step).
   const bool specm = X.spec;
+  if (!specm) {
+  for (int it = X.it0; it < X.it_end; ++it) {
+    L.iters = it + 1;
+    double* const pos = S.pos + (it & 1) * 4 * H1;
+    if (own) {
+      unsigned long long t_xs = STAMP_T();
+      const bool tl = l <= H;
+      double vx = 2.0 * c.Pnorm * (cx_own - rx_own), vy = 2.0 * c.Pnorm * (cy_own - ry_own);
+      if (cpl) {
+        vx = vx + c.rho * cpx;
+        vy = vy + c.rho * cpy;
+      }
+      const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
+      const double wsh = shdn(wt, 1);
+      qx.wq = (l < H) ? wsh : 0.0;
+      qx.qvalid = false;
+      STAMP_ADD(ST_XQ, t_xs);
+      double ustar[1];
+      unsigned long long t_q = STAMP_T();
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+                               qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && it == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
+      STAMP_ADD(ST_XQP, t_q);
+      status_x |= stx;
+      ++n.xqp;
+      n.inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
+      warm_x = true;
+      const double u = around(ustar[0], c.round_decimals);
+      double px, py, pth;
+      rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+      if (l <= H) {
+        pos[(w * 2 + 0) * H1 + l] = px;
+        pos[(w * 2 + 1) * H1 + l] = py;
+      }
+      if (l < H) S.u[(it & 1) * 2 * H + w * H + l] = u;
+      STAMP_ADD(ST_XSTEP, t_xs);
+    }
+    __syncthreads();                                     // A: every agent's positions
+    L.act = collide(X, pos);
+    if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
+      L.stopped = true;
+      break;
+    }
+    L.flag = 1;
+    if (__builtin_expect(L.act, 0)) {
+      __syncthreads();                                   // B: hat, lam, S, D, last, S.sc
+      load_cp();
+    }
+    if (iter_tail(A, X, L, it, nbar)) break;
+  }
+  } else {
   bool have = false;          // the x-step of iteration `it` is already in U (a kept speculation)
   int spec_st = 0;
   int it = X.it0, phase = 0;  // phase 0: before barrier A(it); 1: before barrier B(it)
   while (it < X.it_end) {
     if (phase == 0) L.iters = it + 1;
     const int tgt = phase == 0 ? it : it + 1;         // the iteration this x-step belongs to
-    const bool dox = own && (phase == 0 ? !have : (specm && it + 1 < X.it_end));
-    // this iteration's pos_old buffer: a wave may start the next iteration's x-step while
-    // another still reads this one's positions (no second barrier without a z-step)
-    double* const pos = S.pos + (tgt & 1) * 4 * H1;
+    const bool dox = own && (phase == 0 ? !have : it + 1 < X.it_end);
     // -------- x-step (casadi/main.py:81-106)
     if (dox) {
       unsigned long long t_xs = STAMP_T();
@@ -330,16 +377,6 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       unsigned long long t_rd = STAMP_T();
       const double u = around(ustar[0], c.round_decimals);
       STAMP_ADD(ST_ROUND, t_rd);
-      if (!specm) {
-        double px, py, pth;
-        unsigned long long t_r = STAMP_T();
-        rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
-        STAMP_ADD(ST_XROLL, t_r);
-        if (l <= H) {
-          pos[(w * 2 + 0) * H1 + l] = px;
-          pos[(w * 2 + 1) * H1 + l] = py;
-        }
-      }
       if (l < H) S.u[(tgt & 1) * 2 * H + w * H + l] = u;
       STAMP_ADD(ST_XSTEP, t_xs);
     }
@@ -349,26 +386,8 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       n.inexact += (spec_st & PIADMM_QP_INEXACT) ? 1 : 0;
     }
     unsigned long long t_sa = STAMP_T();
-    __syncthreads();                                     // A(it) or, speculative phase 1, B(it)
+    __syncthreads();                                     // A(it) (phase 0) or B(it) (phase 1)
     STAMP_ADD(phase == 0 ? ST_SYNC_A : ST_SYNC_B, t_sa);
-    if (!specm) {
-      L.act = collide(X, pos);
-      if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
-        L.stopped = true;
-        break;
-      }
-      L.flag = 1;
-      // (the pair wave runs the z-step and records the residuals now)
-      unsigned long long t_sb = STAMP_T();
-      if (__builtin_expect(L.act, 0)) {
-        __syncthreads();                                 // B: hat, lam, S, D, last, S.sc
-        load_cp();
-      }
-      STAMP_ADD(ST_SYNC_B, t_sb);
-      if (iter_tail(A, X, L, it, nbar)) break;
-      ++it;
-      continue;
-    }
     if (phase == 0) {
       phase = 1;
       continue;
@@ -390,6 +409,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     }
     ++it;
     phase = 0;
+  }
   }
   n.warm = own && warm_x;
   // ---- the agent's state of this launch and, in the last launch, outputs and propagation
