@@ -56,6 +56,8 @@ struct QP {
   int* gws;               // pair: HBM warm working set of the dual active set (GI_WS ints)
   bool gws_warm = true;   // pair: start from the stored set (false: cold start, the set is still saved)
   int tstep;              // MPC step index (warm-set bookkeeping)
+  int pre_m = -1;         // pair: rows of the stored active set already appended (gi_solve prebuild), -1: none
+  int pre_wbits = 0;
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
   // Row s of vehicle v = s / 2: even = box (lanes < H), odd = rate (lanes < H-1), 4 = hinge
@@ -1189,7 +1191,11 @@ constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t
 #endif
 template <int NV>
 __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, signed char* lab, double* x, double* y,
-                                         int& nsteps, signed char* flab = nullptr, bool use_wlab = true) {
+                                         int& nsteps, signed char* flab = nullptr, bool use_wlab = true,
+                                         bool prebuild = false) {
+  // (prebuild: only append the pair's stored active set -- S^-1, the Y columns and the codes
+  // depend on the step's geometry, not on q -- and return; the next solve of this QP starts from
+  // it.  The pair wave does it while the agents' first x-steps run.)
   // (use_wlab = false: a cold start although wlab points at labels -- a flag, not a null
   // pointer selected at the call site, so that the caller's label array stays in registers)
   constexpr int NR = QP<NV>::NR;
@@ -1399,10 +1405,22 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     if (delta > DEP_TOL * spp) append(pc, yp, r, delta, 0.0);
     if (NV == 2) STAMP_CNT(ST_N_WARMROW, 1);
   };
-  start();
+  if (prebuild) {
+    m = 0;
+    wbits = 0;
+    ua = 0.0;
+  } else {
+    start();
+  }
   bool warm = false;
   unsigned long long t_wb = STAMP_T();
-  if (P.gws && P.gws_warm) {
+  if (!prebuild && P.pre_m >= 0) {
+    // the stored active set was appended before q was known (a prebuild): x0 is this call's
+    m = P.pre_m;
+    wbits = P.pre_wbits;
+    P.pre_m = -1;
+    warm = true;
+  } else if (P.gws && P.gws_warm) {
     // ---- pair: the stored active set (this step's, or the previous step's shifted)
     const int gm = P.gws[0], gt = P.gws[1];
     const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
@@ -1439,6 +1457,12 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     warm = true;
   }
   STAMP_ADD(NV == 2 ? ST_ZR_GEMV : ST_ZR_X, t_wb);
+  if (prebuild) {
+    P.pre_m = warm ? m : -1;
+    P.pre_wbits = wbits;
+    wsync();
+    return true;
+  }
   unsigned long long t_wf = STAMP_T();
   if (warm) {
     {

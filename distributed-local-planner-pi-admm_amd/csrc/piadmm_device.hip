@@ -569,6 +569,18 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
   double ra_s[2] = {0.0, 0.0};
   if (specm)
     for (int v = 0; v < X.na; ++v) ra_s[v] = A.spd[X.a0 + v];
+  // the pair QP's first solve of the step goes straight to the dual active set from the stored
+  // active set (no warm labels yet): append those rows now, while the agents solve their first
+  // x-steps (they depend on the step's geometry only; setup_pair built it)
+  if (first && e >= 0 && qe.ycap > 0 && X.it0 < X.it_end) {
+    double xd[2];
+    double yd[5];
+    signed char ld[5];
+    int nd = 0;
+    unsigned long long t_pb = STAMP_T();
+    gi_solve(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
+    STAMP_ADD(ST_ZR_SOLVE, t_pb);
+  }
   for (int it = X.it0; it < X.it_end; ++it) {
     L.iters = it + 1;
     double* const pos = S.pos + (it & 1) * 4 * H1;
