@@ -202,6 +202,60 @@ __device__ __forceinline__ double around(double x, int d) {
   return rint(x * f) / f;
 }
 
+// ============================================================ near-tie log (piadmm_get_near_ties)
+// One event of a discrete decision taken within A.tie_tol of its threshold.  Called by ONE lane,
+// in a cold branch (ties are rare: the hot path pays a compare and a ballot).
+__device__ __forceinline__ void tie_record(const DevArgs& A, int t, int it, int kind, int id, int idx, double margin) {
+  atomicAdd(A.tie_cnt + kind, 1ull);
+  const int k = atomicAdd(A.tie_n, 1);
+  if (k < A.tie_cap) {
+    int* ev = A.tie_ev + 6 * k;
+    ev[0] = t;
+    ev[1] = it;
+    ev[2] = kind;
+    ev[3] = id;
+    ev[4] = idx;
+    ev[5] = 0;
+    A.tie_mg[k] = margin;
+  }
+}
+// around(x, d) near its rounding boundary: x 10^d within tol 10^d of k + 1/2 (per lane; the
+// caller ballots).  Returns the signed absolute margin x - (k + 1/2) 10^-d in *m.
+__device__ __forceinline__ bool round_near(double x, int d, double tol, double* m) {
+  const double f = pow10i(d);
+  const double y = x * f;
+  const double b = floor(y) + 0.5;
+  *m = (y - b) / f;
+  return fabs(y - b) <= tol * f;
+}
+// Every lane flagged in `near` logs its round tie (one event per lane; ties are rare).
+__device__ __forceinline__ void round_ties(const DevArgs& A, int t, int it, int kind, int id, int idx0, double x,
+                                           bool valid) {
+  double m;
+  const bool nr = valid && round_near(x, A.cfg.round_decimals, A.tie_tol, &m);
+  if (__builtin_expect(wany(nr), 0))
+    if (nr) tie_record(A, t, it, kind, id, idx0 + lid(), m);
+}
+// The collision test any_k(d_k^2 < thr) == (min_k d_k^2 < thr): a tie when min_k d_k^2 lies within
+// tol thr of thr.  d2 per time lane (valid lanes only); decided by two ballots, the minimum (a wave
+// reduction) only in the cold branch.
+__device__ __forceinline__ void collide_tie(const DevArgs& A, int t, int it, int e, double d2, bool valid, double thr) {
+  const double tol = A.tie_tol;
+  const bool lo = valid && d2 < thr * (1.0 - tol);
+  const bool near = valid && d2 <= thr * (1.0 + tol);
+  if (__builtin_expect(!wany(lo) && wany(near), 0)) {
+    const double mn = wmin(valid ? d2 : INFINITY);
+    const unsigned long long at = __ballot(valid && d2 == mn);
+    if (lid() == 0) tie_record(A, t, it, PIADMM_TIE_COLLIDE, e, (int)__builtin_ctzll(at), (mn - thr) / thr);
+  }
+}
+// A scalar threshold test v <= thr (the stop test) or v > thr (the distance check) taken within
+// tol |thr| of thr: logged by the calling lane.
+__device__ __forceinline__ void scalar_tie(const DevArgs& A, int t, int it, int kind, int id, int idx, double v,
+                                           double thr) {
+  if (__builtin_expect(fabs(v - thr) <= A.tie_tol * fabs(thr), 0)) tie_record(A, t, it, kind, id, idx, (v - thr) / thr);
+}
+
 // sum_{k=0}^{H} (k-1-i)+ (k-1-j)+ = (T'T)_{ij}, exact in integers.
 __device__ __forceinline__ double TT(int i, int j, int H) {
   const int a = max(i, j), b = min(i, j);

@@ -68,6 +68,13 @@ struct piadmm_ctx {
   int* h_ctl = nullptr;
   int chunk_guess = 2;
   bool host_decide = false;
+  // near-tie log (piadmm_get_near_ties): tolerance, and the ties of stop decisions the host takes
+  double tie_tol = 1e-9;
+  std::vector<piadmm_near_tie_t> host_ties;
+  unsigned long long host_tie_cnt[PIADMM_TIE_KINDS] = {};
+  // MPC steps per persistent launch agreed over the job's ranks (the fixed-iteration residual
+  // history is all-reduced once per launch: every rank must cut the steps into the same launches)
+  bool cap_synced = false;
 };
 
 namespace {
@@ -78,6 +85,21 @@ int fail(piadmm_ctx* h, int code, const std::string& msg) {
   if (h) h->err = msg;
   g_err = msg;
   return code;
+}
+
+// A stop / distance decision the host takes within tie_tol of its threshold (the device kernels
+// log their own, pd::scalar_tie).
+void host_tie(piadmm_ctx* h, int t, int it, int kind, int id, int idx, double v, double thr) {
+  if (!(std::fabs(v - thr) <= h->tie_tol * std::fabs(thr))) return;
+  ++h->host_tie_cnt[kind];
+  piadmm_near_tie_t ev{};
+  ev.step = t;
+  ev.iter = it;
+  ev.kind = kind;
+  ev.id = id;
+  ev.index = idx;
+  ev.margin = (v - thr) / thr;
+  if (h->host_ties.size() < PIADMM_TIE_CAP) h->host_ties.push_back(ev);
 }
 
 #define HIPCHK(h, expr)                                                              \
@@ -313,6 +335,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   free_all(h);
   h->step_open = false;
   h->split = false;
+  h->cap_synced = false;
   h->comp_ptr.assign(1, 0);
   h->comp_edge.clear();
   std::vector<int> nbr(N, 0);
@@ -320,6 +343,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   // Scenario.components()), agent / pair lists per component, neighbour CSR sorted by
   // neighbour id (the order of the x-step's consensus sum)
   std::vector<int> g_aptr, g_alist, g_eptr, g_elist, g_nptr, g_nedge, g_ndir;
+  std::vector<int> s_cptr, s_elist;     // split: pairs per original component (the residual-sum order)
   if (simple) {
     for (int a = 0; a < N;) {
       const int e = pair_of[a];
@@ -367,6 +391,16 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
         bool any = false;
         for (int k = 0; k < C; ++k) any |= csize[k] > block;
         if (any) {
+          // the original components' pair lists (pairs in increasing index): k_graph_partials sums
+          // the residual terms in this order, the reference's (casadi/main.py:165-173)
+          s_cptr.assign(C + 1, 0);
+          for (int e = 0; e < n_edges; ++e) ++s_cptr[comp[edges[2 * e]] + 1];
+          for (int k = 0; k < C; ++k) s_cptr[k + 1] += s_cptr[k];
+          s_elist.resize(n_edges);
+          {
+            std::vector<int> fill(s_cptr.begin(), s_cptr.end() - 1);
+            for (int e = 0; e < n_edges; ++e) s_elist[fill[comp[edges[2 * e]]]++] = e;
+          }
           std::vector<int> seen(C, 0), cur(C, -1), nb;
           int NB = 0;
           for (int a = 0; a < N; ++a) {
@@ -489,7 +523,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   rc |= dalloc(h, &A.qs_e, E * 12 * pd::WAVE);
   rc |= dalloc(h, &A.ql_e, E * 5 * pd::WAVE);
   rc |= dalloc(h, &A.cst, C * 4);
-  rc |= dalloc(h, &h->d_part, (size_t)h->cfg.max_outer * std::max(5, 2 * h->step_cap));
+  rc |= dalloc(h, &h->d_part, std::max<size_t>(33, (size_t)h->cfg.max_outer * std::max(5, 2 * h->step_cap)));
   rc |= dalloc(h, &A.counters, C * 8);
   rc |= dalloc(h, &A.rho_x, (size_t)N);
   rc |= dalloc(h, &A.rho_e, E);
@@ -501,6 +535,18 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   rc |= dalloc(h, &A.ghist, (size_t)h->step_cap * std::max(h->cfg.max_outer, 1) * 2);
   rc |= dalloc(h, &A.giters, (size_t)h->step_cap);
   rc |= dalloc(h, &A.gctl, 4);
+  rc |= dalloc(h, &A.tie_cnt, PIADMM_TIE_KINDS);
+  rc |= dalloc(h, &A.tie_n, 1);
+  rc |= dalloc(h, &A.tie_ev, (size_t)PIADMM_TIE_CAP * 6);
+  rc |= dalloc(h, &A.tie_mg, (size_t)PIADMM_TIE_CAP);
+  A.tie_cap = PIADMM_TIE_CAP;
+  A.tie_tol = h->tie_tol;
+  int *d_scp = nullptr, *d_sel = nullptr;
+  if (h->split) {
+    rc |= dalloc(h, &A.eterm, E * 2);
+    rc |= dalloc(h, &d_scp, s_cptr.size());
+    rc |= dalloc(h, &d_sel, E);
+  }
   int *d_gap = nullptr, *d_gal = nullptr, *d_gep = nullptr, *d_gel = nullptr, *d_gnp = nullptr, *d_gne = nullptr,
       *d_gnd = nullptr;
   if (A.graph) {
@@ -563,6 +609,17 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     A.nbr_edge = d_gne;
     A.nbr_dir = d_gnd;
   }
+  if (h->split) {
+    h->graph_host.push_back(s_cptr);
+    h->graph_host.push_back(s_elist);
+    const auto& hc = h->graph_host[h->graph_host.size() - 2];
+    const auto& he = h->graph_host.back();
+    HIPCHK(h, hipMemcpyAsync(d_scp, hc.data(), hc.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+    if (E) HIPCHK(h, hipMemcpyAsync(d_sel, he.data(), he.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+    A.sum_cptr = d_scp;
+    A.sum_elist = d_sel;
+    A.sum_C = (int)hc.size() - 1;
+  }
   if (sharded) {
     h->shard_host.assign(owned, owned + N);
     h->shard_host.insert(h->shard_host.end(), counted, counted + E);
@@ -619,6 +676,7 @@ int32_t piadmm_set_allreduce(piadmm_handle_t h, piadmm_allreduce_fn fn, void* ct
   if (h->comm && fn) return fail(h, PIADMM_E_STATE, "the handle already has an RCCL communicator");
   h->xfn = fn;
   h->xctx = ctx;
+  h->cap_synced = false;
   return PIADMM_OK;
 }
 
@@ -654,60 +712,56 @@ static int launch_step(const pd::DevArgs& a, int t, int n, int it0, int it1, int
   return a.graph ? pd::launch_graph_step(a, t, n, it0, it1, flags, s) : pd::launch_mpc_step(a, t, n, it0, it1, flags, s);
 }
 
-// MPC steps t .. t+n-1 (n <= step_cap).  Per-component termination, or fixed iterations
-// under term_global: ONE persistent launch for all n steps (each workgroup runs its
-// component's steps back to back), plus, under term_global, the component-summed residual
-// history of every step, all-reduced once (n x 2 x max_outer doubles).  Global termination
-// with the stopping test on (one step per call): one launch per outer iteration, the rank's
-// partials all-reduced over RCCL and read back, the stop decided on the host exactly as
-// casadi/main.py:115-118,174-178 (MATLAB :191-210) do over all agents, then a final launch
-// for outputs and propagation.
-// Sharded graph with pairs across ranks: every outer iteration is an X launch
-// (x-steps of the rank's own agents; boundary agents write px | py | u to their exchange slot),
-// ONE all-reduce of the exchange buffer (the ranks' slots are disjoint and zero elsewhere, so
-// the sum is an all-gather), and a Z launch (ghost agents read their owner's values; every
-// pair with an own agent -- a cross-rank pair on both of its ranks, bit-identically -- does its
-// collision test, pair QP and dual update; a cross-rank pair counts its residual on the rank
-// of its first agent only).  Natural termination adds the 5-double all-reduce of the
-// termination partials and the host decision of the unsharded host-decided path.
+// The launches of ONE outer iteration `it` of MPC step tk under the global scope (term_global,
+// the stop decided outside the kernel): one launch; or -- a sharded graph with pairs across ranks
+// (SURVEY.md 8e), or a connected component split over workgroups -- an X launch (the x-steps;
+// boundary agents write px | py | u to their exchange slot), ONE all-reduce of the exchange buffer
+// (sharded: the ranks' slots are disjoint and zero elsewhere, so the sum is an all-gather), and a Z
+// launch (ghost agents read their owner's values; every local pair -- a cross-rank pair on both of
+// its ranks, bit-identically -- runs its collision test, pair QP, dual update and residual terms).
+// A split component's blocks reset their pairs in a step-init launch before any block's first
+// x-step reads them (casadi/main.py:52-63).
+static int32_t iteration_launches(piadmm_handle_t h, int32_t tk, int it, int extra) {
+  hipStream_t s = h->stream;
+  int f = (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | extra;
+  if (h->xchg || h->split) {
+    if (it == 0 && h->split) {
+      LAUNCH(h, launch_step(h->a, tk, 1, 0, 0, pd::F_FIRST | pd::F_GLOBAL | pd::F_INITONLY, s));
+      f &= ~pd::F_FIRST;
+    }
+    LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f | pd::F_XONLY, s));
+    const size_t nx = h->xchg ? (size_t)h->n_slots * 3 * (h->cfg.H + 1) : 0;
+    if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
+    LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, pd::F_GLOBAL | pd::F_ZONLY | extra, s));
+  } else {
+    LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f, s));
+  }
+  return PIADMM_OK;
+}
+
 // One MPC step under device-decided global termination (term_global with natural termination
-// across ranks -- RCCL or the host transport -- or PIADMM_NO_COOP on one rank).  Chunks of outer
-// iterations are enqueued ahead: per iteration the iteration launch (an X launch, the exchange
-// all-reduce and a Z launch for a sharded graph), the termination partials, their all-reduce and
-// k_decide, which applies the reference's stop rules (casadi/main.py:115-118,174-178) on the
-// device and sets the stop flag; launches after the stop return at once.  The host reads the stop
-// state once per chunk (chunk = the previous step's iteration count, doubled while the step runs
-// on), instead of one host round trip per outer iteration; the LAST launch takes the iteration
-// count and the NANLAST case from the device.
+// across ranks -- RCCL or the host transport --, a split component, or PIADMM_NO_COOP on one rank).
+// Chunks of outer iterations are enqueued ahead: per iteration its launches (iteration_launches),
+// the termination partials, their all-reduce and k_decide, which applies the reference's stop rules
+// (casadi/main.py:115-118,174-178) on the device and sets the stop flag; launches after the stop
+// return at once.  The host reads the stop state once per chunk (chunk = the previous step's
+// iteration count, doubled while the step runs on), instead of one host round trip per outer
+// iteration; the LAST launch takes the iteration count and the NANLAST case from the device.
 static int32_t devstop_step(piadmm_handle_t h, int32_t tk, bool sync_outputs) {
   const piadmm_config_t& c = h->cfg;
   hipStream_t s = h->stream;
   const int M = c.max_outer;
-  const size_t nx = h->xchg ? (size_t)h->n_slots * 3 * (c.H + 1) : 0;
-  const bool phases = h->xchg || h->split;      // X and Z phases as separate launches
   HIPCHK(h, hipMemsetAsync(h->a.gctl, 0, 4 * sizeof(int), s));
   if (!h->a.graph) LAUNCH(h, pd::launch_pair_deff(h->a, s));
   int it = 0, K = std::max(1, std::min(h->chunk_guess, M));
   while (true) {
     const int n = std::min(K, M - it);
     for (int j = 0; j < n; ++j, ++it) {
-      int f = (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | pd::F_DEVSTOP;
-      if (it == 0 && h->split) {
-        // the blocks of a split component reset their pairs before any block's x-step reads them
-        LAUNCH(h, launch_step(h->a, tk, 1, 0, 0, pd::F_FIRST | pd::F_GLOBAL | pd::F_INITONLY, s));
-        f &= ~pd::F_FIRST;
-      }
-      if (phases) {
-        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f | pd::F_XONLY, s));
-        if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
-        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, pd::F_GLOBAL | pd::F_DEVSTOP | pd::F_ZONLY, s));
-      } else {
-        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f, s));
-      }
+      if (int rc = iteration_launches(h, tk, it, pd::F_DEVSTOP)) return rc;
       double* part = h->d_part + (size_t)5 * it;
       LAUNCH(h, h->a.graph ? pd::launch_graph_partials(h->a, part, s, 1) : pd::launch_term_partials(h->a, it, part, s, 1));
       if (int rc = allreduce(h, part, part, 5)) return rc;
-      LAUNCH(h, pd::launch_decide(h->a, it, part, s));
+      LAUNCH(h, pd::launch_decide(h->a, tk, it, part, s));
     }
     HIPCHK(h, hipMemcpyAsync(h->h_ctl, h->a.gctl, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
@@ -730,71 +784,16 @@ static int32_t devstop_step(piadmm_handle_t h, int32_t tk, bool sync_outputs) {
   return PIADMM_OK;
 }
 
-static int32_t run_steps_xchg(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outputs) {
-  const piadmm_config_t& c = h->cfg;
-  hipStream_t s = h->stream;
-  const int M = c.max_outer;
-  const size_t nx = (size_t)h->n_slots * 3 * (c.H + 1);
-  for (int k = 0; k < n; ++k) {
-    const int tk = t + k;
-    if (!c.fixed_iters && !h->host_decide) {
-      if (int rc = devstop_step(h, tk, sync_outputs && k == n - 1)) return rc;
-      continue;
-    }
-    h->ghist.assign((size_t)2 * M, NAN);
-    int flag = 0, nit = 0, nanlast = 0;
-    for (int it = 0; it < M; ++it) {
-      int f = (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL | pd::F_XONLY;
-      if (it == 0 && h->split) {   // (see devstop_step)
-        LAUNCH(h, launch_step(h->a, tk, 1, 0, 0, pd::F_FIRST | pd::F_GLOBAL | pd::F_INITONLY, s));
-        f &= ~pd::F_FIRST;
-      }
-      LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, f, s));
-      if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
-      LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, pd::F_GLOBAL | pd::F_ZONLY, s));
-      nit = it + 1;
-      if (c.fixed_iters) continue;
-      double* part = h->d_part + (size_t)5 * it;
-      LAUNCH(h, pd::launch_graph_partials(h->a, part, s));
-      if (int rc = allreduce(h, part, part, 5)) return rc;
-      HIPCHK(h, hipMemcpyAsync(h->h_part, part, 5 * sizeof(double), hipMemcpyDeviceToHost, s));
-      HIPCHK(h, hipStreamSynchronize(s));
-      const double rk = h->h_part[0], sk = h->h_part[1], n_act = h->h_part[2];
-      const double n_seen = h->h_part[3], n_bad = h->h_part[4];
-      if (n_act == 0.0 && flag == 0) {      // no pair collides anywhere: stop (casadi/main.py:115-116)
-        nanlast = 1;
-        break;
-      }
-      flag = 1;
-      h->ghist[2 * it + 0] = rk;
-      h->ghist[2 * it + 1] = sk;
-      if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || (n_seen > 0.0 && n_bad == 0.0))) break;
-    }
-    h->giters = nit;
-    LAUNCH(h, launch_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
-    if (c.fixed_iters) {
-      LAUNCH(h, pd::launch_resid_history(h->a, 1, h->d_part, s));
-      if (int rc = allreduce(h, h->d_part, h->d_part, (size_t)2 * M)) return rc;
-      if (sync_outputs && k == n - 1) {
-        HIPCHK(h, hipMemcpyAsync(h->h_part, h->d_part, (size_t)2 * M * sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPCHK(h, hipStreamSynchronize(s));
-        h->ghist.assign(h->h_part, h->h_part + 2 * M);
-      }
-    }
-  }
-  return PIADMM_OK;
-}
-
 // One outer iteration `it` of MPC step t under host-decided global termination (term_global
-// without the in-kernel stop test: an RCCL communicator, a host transport, or host stepping):
-// the iteration launch, the job's termination partials (all-reduced), and the reference's stop
-// rules over all agents (casadi/main.py:115-118,174-178; MATLAB :191-210).  flag / nanlast carry
-// the step's state; *stop = 1 when the step ends at this iteration.
+// without the in-kernel stop test: PIADMM_HOST_DECIDE, or host stepping): the iteration's launches,
+// the job's termination partials (all-reduced), and the reference's stop rules over all agents
+// (casadi/main.py:115-118,174-178; MATLAB :191-210).  flag / nanlast carry the step's state;
+// *stop = 1 when the step ends at this iteration.
 static int32_t global_iteration(piadmm_handle_t h, int32_t tk, int it, int& flag, int& nanlast, int* stop) {
   const piadmm_config_t& c = h->cfg;
   hipStream_t s = h->stream;
   *stop = 0;
-  LAUNCH(h, launch_step(h->a, tk, 1, it, it + 1, (it == 0 ? pd::F_FIRST : 0) | pd::F_GLOBAL, s));
+  if (int rc = iteration_launches(h, tk, it, 0)) return rc;
   double* part = h->d_part + (size_t)5 * it;
   LAUNCH(h, h->a.graph ? pd::launch_graph_partials(h->a, part, s) : pd::launch_term_partials(h->a, it, part, s));
   if (int rc = allreduce(h, part, part, 5)) return rc;
@@ -808,23 +807,71 @@ static int32_t global_iteration(piadmm_handle_t h, int32_t tk, int it, int& flag
     return PIADMM_OK;
   }
   flag = 1;
-  if (c.fixed_iters) {                  // throughput mode: the history only, never a stop
-    h->ghist[2 * it + 0] = rk;
-    h->ghist[2 * it + 1] = sk;
-    return PIADMM_OK;
-  }
   h->ghist[2 * it + 0] = rk;
   h->ghist[2 * it + 1] = sk;
+  if (c.fixed_iters) return PIADMM_OK;   // throughput mode: the history only, never a stop
+  host_tie(h, tk, it, PIADMM_TIE_STOP, -1, 0, rk, c.eps_pri);
+  host_tie(h, tk, it, PIADMM_TIE_STOP, -1, 1, sk, c.eps_dual);
   const bool dist_ok = n_seen > 0.0 && n_bad == 0.0;
   if (rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok)) *stop = 1;
   return PIADMM_OK;
 }
 
+// MPC steps of a job whose iterations are split into X and Z launches (a sharded graph with pairs
+// across ranks, or a component split over workgroups), one step at a time.  Fixed iterations: the
+// steps' residual histories are all-reduced ONCE for the n steps (n x 2 x max_outer doubles), the
+// same collective as run_steps' persistent launch, so ranks of one job that take different paths
+// (a split component on one rank only) still issue matching collectives.
+static int32_t run_steps_phases(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outputs) {
+  const piadmm_config_t& c = h->cfg;
+  hipStream_t s = h->stream;
+  const int M = c.max_outer;
+  for (int k = 0; k < n; ++k) {
+    const int tk = t + k;
+    if (!c.fixed_iters && !h->host_decide) {
+      if (int rc = devstop_step(h, tk, sync_outputs && k == n - 1)) return rc;
+      continue;
+    }
+    h->ghist.assign((size_t)2 * M, NAN);
+    int flag = 0, nit = 0, nanlast = 0;
+    for (int it = 0; it < M; ++it) {
+      nit = it + 1;
+      if (c.fixed_iters) {
+        if (int rc = iteration_launches(h, tk, it, 0)) return rc;
+        continue;
+      }
+      int stop = 0;
+      if (int rc = global_iteration(h, tk, it, flag, nanlast, &stop)) return rc;
+      if (stop) break;
+    }
+    h->giters = nit;
+    LAUNCH(h, launch_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
+    if (c.fixed_iters) LAUNCH(h, pd::launch_resid_history(h->a, 1, h->d_part + (size_t)k * 2 * M, s));
+  }
+  if (c.fixed_iters) {
+    if (int rc = allreduce(h, h->d_part, h->d_part, (size_t)n * 2 * M)) return rc;
+    h->giters = M;
+    if (sync_outputs) {
+      HIPCHK(h, hipMemcpyAsync(h->h_part, h->d_part + (size_t)(n - 1) * 2 * M, (size_t)2 * M * sizeof(double),
+                               hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      h->ghist.assign(h->h_part, h->h_part + 2 * M);
+    }
+  }
+  return PIADMM_OK;
+}
+
+// MPC steps t .. t+n-1 (n <= step_cap).  Per-component termination, or fixed iterations under
+// term_global: ONE persistent launch for all n steps (each workgroup runs its component's steps
+// back to back), plus, under term_global, the component-summed residual history of every step,
+// all-reduced once (n x 2 x max_outer doubles).  Natural global termination: in-kernel behind a
+// grid barrier (one rank, cooperative launch), else one step at a time with the stop decided on
+// the device (devstop_step) or, PIADMM_HOST_DECIDE=1, on the host after every outer iteration.
 static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outputs) {
   const piadmm_config_t& c = h->cfg;
   hipStream_t s = h->stream;
   const int M = c.max_outer;
-  if (h->xchg || h->split) return run_steps_xchg(h, t, n, sync_outputs);
+  if (h->xchg || h->split) return run_steps_phases(h, t, n, sync_outputs);
   if (!c.term_global) {
     LAUNCH(h, launch_step(h->a, t, n, 0, M, pd::F_FIRST | pd::F_LAST, s));
     return PIADMM_OK;
@@ -880,6 +927,29 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
   return PIADMM_OK;
 }
 
+// The job's ranks agree on the MPC steps per launch (the smallest): the fixed-iteration residual
+// history is all-reduced once per launch, so every rank must cut a run into the same launches
+// (step_cap depends on the rank's component count).  An all-gather through the sum: slot k of a
+// 33-double buffer counts the ranks whose cap is k.
+static int32_t sync_step_cap(piadmm_handle_t h) {
+  double v[33] = {};
+  v[std::min(32, std::max(1, h->step_cap))] = 1.0;
+  hipStream_t s = h->stream;
+  HIPCHK(h, hipMemcpyAsync(h->d_part, v, sizeof(v), hipMemcpyHostToDevice, s));   // (d_part: >= 33 doubles)
+  if (int rc = allreduce(h, h->d_part, h->d_part, 33)) return rc;
+  HIPCHK(h, hipMemcpyAsync(v, h->d_part, sizeof(v), hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  int cap = h->step_cap;
+  for (int k = 1; k <= 32; ++k)
+    if (v[k] > 0.0) {
+      cap = std::min(cap, k);
+      break;
+    }
+  h->step_cap = cap;
+  h->cap_synced = true;
+  return PIADMM_OK;
+}
+
 static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
@@ -887,6 +957,8 @@ static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
   if (n < 0 || t0 < 0 || t0 + (n > 0 ? n - 1 : 0) + h->cfg.H + 1 > h->T)
     return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
   HIPCHK(h, hipSetDevice(h->cfg.device));
+  if ((h->comm || h->xfn) && !h->cap_synced)
+    if (int rc = sync_step_cap(h)) return rc;
   for (int i = 0; i < n;) {
     const int k = std::min(h->step_cap, n - i);
     if (int rc = run_steps(h, t0 + i, k, i + k == n)) return rc;
@@ -931,9 +1003,6 @@ int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_o
 int32_t piadmm_outer_iter(piadmm_handle_t h, int32_t t, int32_t it, int32_t* stop_out) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
-  if (h->xchg || h->split)
-    return fail(h, PIADMM_E_STATE, "host stepping of a sharded graph or of components split over workgroups "
-                                   "is not supported");
   const piadmm_config_t& c = h->cfg;
   if (it < 0 || it >= c.max_outer) return fail(h, PIADMM_E_ARG, "it must be in [0, max_outer)");
   if (t < 0 || t + c.H + 1 > h->T) return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
@@ -1065,6 +1134,7 @@ int32_t piadmm_comm_init(piadmm_handle_t h, const uint8_t* id_in, int32_t nranks
   NCCLCHK(h, ncclCommInitRank(&h->comm, nranks, id, rank));
   h->nranks = nranks;
   h->rank = rank;
+  h->cap_synced = false;
   return PIADMM_OK;
 }
 
@@ -1189,11 +1259,112 @@ int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n) {
   return PIADMM_OK;
 }
 
+int32_t piadmm_set_tie_tolerance(piadmm_handle_t h, double tol) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!(tol >= 0.0) || !std::isfinite(tol)) return fail(h, PIADMM_E_ARG, "tie tolerance must be finite and >= 0");
+  h->tie_tol = tol;
+  h->a.tie_tol = tol;          // (the kernels take DevArgs by value: from the next launch on)
+  return PIADMM_OK;
+}
+
+int32_t piadmm_get_near_ties(piadmm_handle_t h, uint64_t* counts, piadmm_near_tie_t* events, int32_t max_events,
+                             int32_t* n_events) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  if (max_events < 0 || (max_events > 0 && !events)) return fail(h, PIADMM_E_ARG, "bad events / max_events");
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  hipStream_t s = h->stream;
+  unsigned long long cnt[PIADMM_TIE_KINDS];
+  int nd = 0;
+  HIPCHK(h, hipMemcpyAsync(cnt, h->a.tie_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipMemcpyAsync(&nd, h->a.tie_n, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  const int kept = std::min(nd, PIADMM_TIE_CAP);
+  std::vector<int> ev((size_t)kept * 6);
+  std::vector<double> mg((size_t)kept);
+  if (kept > 0) {
+    HIPCHK(h, hipMemcpyAsync(ev.data(), h->a.tie_ev, ev.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(mg.data(), h->a.tie_mg, mg.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+  }
+  if (counts)
+    for (int k = 0; k < PIADMM_TIE_KINDS; ++k) counts[k] = cnt[k] + h->host_tie_cnt[k];
+  int w = 0;
+  for (int i = 0; i < kept && w < max_events; ++i, ++w) {
+    piadmm_near_tie_t& o = events[w];
+    o.step = ev[6 * i];
+    o.iter = ev[6 * i + 1];
+    o.kind = ev[6 * i + 2];
+    o.id = ev[6 * i + 3];
+    o.index = ev[6 * i + 4];
+    o.reserved = 0;
+    o.margin = mg[i];
+  }
+  for (size_t i = 0; i < h->host_ties.size() && w < max_events; ++i, ++w) events[w] = h->host_ties[i];
+  if (n_events) *n_events = nd + (int)h->host_ties.size();
+  return PIADMM_OK;
+}
+
+int32_t piadmm_get_step_state(piadmm_handle_t h, double* xt, double* hat, double* lam, double* S, double* D,
+                              double* last_hat, double* rho_pi) {
+  if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  if (h->step_open) return fail(h, PIADMM_E_STATE, "a host-stepped MPC step is open: piadmm_step_finish first");
+  const size_t N = h->N, E = h->E, H1 = h->cfg.H + 1;
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  hipStream_t s = h->stream;
+  if (xt) HIPCHK(h, hipMemcpyAsync(xt, h->a.xt, N * 3 * 8, hipMemcpyDeviceToHost, s));
+  double* src[5] = {h->a.hat, h->a.lam, h->a.Sacc, h->a.Dacc, h->a.last};
+  double* dst[5] = {hat, lam, S, D, last_hat};
+  for (int k = 0; k < 5; ++k)
+    if (dst[k] && E) HIPCHK(h, hipMemcpyAsync(dst[k], src[k], E * 4 * H1 * 8, hipMemcpyDeviceToHost, s));
+  if (rho_pi && E) {
+    if (h->a.rho_pi) HIPCHK(h, hipMemcpyAsync(rho_pi, h->a.rho_pi, E * 8, hipMemcpyDeviceToHost, s));
+    else
+      for (size_t e = 0; e < E; ++e) rho_pi[e] = h->cfg.rho;
+  }
+  HIPCHK(h, hipStreamSynchronize(s));
+  return PIADMM_OK;
+}
+
+int32_t piadmm_set_state(piadmm_handle_t h, const double* xt, const double* hat, const double* lam, const double* S,
+                         const double* D, const double* last_hat, const double* rho_pi) {
+  if (!h || !xt) return fail(h, PIADMM_E_ARG, "null argument (xt is required)");
+  if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
+  const size_t N = h->N, E = h->E, H1 = h->cfg.H + 1;
+  for (size_t i = 0; i < 3 * N; ++i)
+    if (!std::isfinite(xt[i])) return fail(h, PIADMM_E_ARG, "non-finite state");
+  if (rho_pi)
+    for (size_t e = 0; e < E; ++e)
+      if (!(rho_pi[e] > 0.0)) return fail(h, PIADMM_E_ARG, "rho_pi must be > 0");
+  // xt, and a fresh receding-horizon sequence (labels, warm active sets, ADMM penalties)
+  if (int rc = piadmm_set_xt(h, xt)) return rc;
+  HIPCHK(h, hipSetDevice(h->cfg.device));
+  hipStream_t s = h->stream;
+  double* dst[5] = {h->a.hat, h->a.lam, h->a.Sacc, h->a.Dacc, h->a.last};
+  const double* src[5] = {hat, lam, S, D, last_hat};
+  for (int k = 0; k < 5 && E; ++k) {
+    if (src[k]) HIPCHK(h, hipMemcpyAsync(dst[k], src[k], E * 4 * H1 * 8, hipMemcpyHostToDevice, s));
+    else HIPCHK(h, hipMemsetAsync(dst[k], 0, E * 4 * H1 * 8, s));
+  }
+  if (h->a.rho_pi && E) {
+    std::vector<double> r(rho_pi ? rho_pi : h->rho_pi_init.data(), (rho_pi ? rho_pi : h->rho_pi_init.data()) + E);
+    HIPCHK(h, hipMemcpyAsync(h->a.rho_pi, r.data(), E * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+  }
+  HIPCHK(h, hipStreamSynchronize(s));
+  return PIADMM_OK;
+}
+
 int32_t piadmm_reset_counters(piadmm_handle_t h) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
   HIPCHK(h, hipSetDevice(h->cfg.device));
   HIPCHK(h, hipMemsetAsync(h->a.counters, 0, (size_t)h->C * 8 * 8, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->a.tie_cnt, 0, PIADMM_TIE_KINDS * sizeof(unsigned long long), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->a.tie_n, 0, sizeof(int), h->stream));
+  h->host_ties.clear();
+  for (auto& v : h->host_tie_cnt) v = 0;
   if (h->a.stamps) HIPCHK(h, hipMemsetAsync(h->a.stamps, 0, (size_t)h->C * 64 * 8, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PIADMM_OK;

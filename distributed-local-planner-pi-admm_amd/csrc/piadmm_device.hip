@@ -54,14 +54,18 @@ struct LoopCtl {
 };
 
 // collision graph (casadi/main.py:110-118), computed by every wave from this iteration's positions
-__device__ __forceinline__ bool collide(const StepCtx& X, const double* pos) {
+// (the pair wave logs a near tie, piadmm_get_near_ties: every wave runs the test in the plain loop)
+__device__ __forceinline__ bool collide(const DevArgs& A, const StepCtx& X, const double* pos, int it) {
   if (X.e < 0 || X.na != 2) return false;
   bool hit = false;
+  double d2 = 0.0;
   if (X.l <= X.H) {
     const double dx = pos[0 * X.H1 + X.l] - pos[2 * X.H1 + X.l];
     const double dy = pos[1 * X.H1 + X.l] - pos[3 * X.H1 + X.l];
-    hit = (dx * dx + dy * dy) < X.thr;
+    d2 = dx * dx + dy * dy;
+    hit = d2 < X.thr;
   }
+  if (X.w == PW) collide_tie(A, X.t, it, X.e, d2, X.l <= X.H, X.thr);
   return wany(hit);
 }
 
@@ -75,6 +79,10 @@ __device__ __forceinline__ bool iter_tail(const DevArgs& A, const StepCtx& X, Lo
   const double rk = L.act ? S.sc[0] : 0.0;
   const double sk = L.act ? S.sc[1] : 0.0;
   if (L.act) L.dis_chk = S.sc[2];
+  if (!c.fixed_iters && !X.global && X.w == PW && X.l == 0) {   // near ties of the stop test (one wave)
+    scalar_tie(A, X.t, it, PIADMM_TIE_STOP, X.ci, 0, rk, c.eps_pri);
+    scalar_tie(A, X.t, it, PIADMM_TIE_STOP, X.ci, 1, sk, c.eps_dual);
+  }
   if (!c.fixed_iters && !X.global && rk <= c.eps_pri && sk <= c.eps_dual &&
       (!c.term_dist_check || L.dis_chk > X.deff)) {
     L.stopped = true;
@@ -136,6 +144,10 @@ __device__ __forceinline__ bool iter_tail(const DevArgs& A, const StepCtx& X, Lo
       A.ghist[((size_t)X.slot * c.max_outer + it) * 2 + 1] = tsk;
     }
     const bool dist_ok = tseen > 0.0 && tbad == 0.0;
+    if (ci == 0 && threadIdx.x == 0) {
+      scalar_tie(A, X.t, it, PIADMM_TIE_STOP, -1, 0, trk, c.eps_pri);
+      scalar_tie(A, X.t, it, PIADMM_TIE_STOP, -1, 1, tsk, c.eps_dual);
+    }
     if (trk <= c.eps_pri && tsk <= c.eps_dual && (!c.term_dist_check || dist_ok)) {
       L.stopped = true;
       return true;
@@ -317,6 +329,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       n.inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
       warm_x = true;
       const double u = around(ustar[0], c.round_decimals);
+      if (c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
       double px, py, pth;
       rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
       if (l <= H) {
@@ -327,7 +340,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       STAMP_ADD(ST_XSTEP, t_xs);
     }
     __syncthreads();                                     // A: every agent's positions
-    L.act = collide(X, pos);
+    L.act = collide(A, X, pos, it);
     if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
       L.stopped = true;
       break;
@@ -376,6 +389,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       warm_x = true;
       unsigned long long t_rd = STAMP_T();
       const double u = around(ustar[0], c.round_decimals);
+      if (c.round_decimals >= 0) round_ties(A, t, tgt, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
       STAMP_ADD(ST_ROUND, t_rd);
       if (l < H) S.u[(tgt & 1) * 2 * H + w * H + l] = u;
       STAMP_ADD(ST_XSTEP, t_xs);
@@ -607,7 +621,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
         }
       wsync();
     }
-    L.act = collide(X, pos);
+    L.act = collide(A, X, pos, it);
     if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
       L.stopped = true;
       if (specm) {
@@ -654,6 +668,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       double hx[2], hy[2], hth;
       for (int v = 0; v < 2; ++v) {
         const double uv = (l < H) ? around(uh[v], c.round_decimals) : 0.0;
+        if (c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_UHAT, e, v * H, uh[v], l < H);
         rollout(S.xt + 3 * v, A.spd[X.a0 + v], uv, c, H, true, hx[v], hy[v], hth);
       }
       // dual update (plain :161-162 / PI + anti-windup MATLAB :156-188)
@@ -717,6 +732,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
         S.sc[0] = 2.0 * sqrt(rr);
         S.sc[1] = L.aliased ? 0.0 : 2.0 * sqrt(ss);
         S.sc[2] = rdl(dist, 1);
+        if (c.term_dist_check) scalar_tie(A, t, it, PIADMM_TIE_DIST, e, 0, S.sc[2], X.deff);
       }
       STAMP_ADD(ST_ZSTEP, t_z);
     }
@@ -863,8 +879,14 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     S.xt[3 * threadIdx.x + 0] = x;
     S.xt[3 * threadIdx.x + 1] = y;
     S.xt[3 * threadIdx.x + 2] = th;
-    S.seed[2 * threadIdx.x + 0] = around(x + c.dt * s * cos(th), c.round_decimals);
-    S.seed[2 * threadIdx.x + 1] = around(y + c.dt * s * sin(th), c.round_decimals);
+    const double sx = x + c.dt * s * cos(th), sy = y + c.dt * s * sin(th);
+    S.seed[2 * threadIdx.x + 0] = around(sx, c.round_decimals);
+    S.seed[2 * threadIdx.x + 1] = around(sy, c.round_decimals);
+    double m;   // near ties of the seeds' rounding, logged once per step (the first launch)
+    if ((flags & F_FIRST) && c.round_decimals >= 0 && round_near(sx, c.round_decimals, A.tie_tol, &m))
+      tie_record(A, t, -1, PIADMM_TIE_ROUND_SEED, a, 0, m);
+    if ((flags & F_FIRST) && c.round_decimals >= 0 && round_near(sy, c.round_decimals, A.tie_tol, &m))
+      tie_record(A, t, -1, PIADMM_TIE_ROUND_SEED, a, 1, m);
   }
   for (int i = threadIdx.x; i < 32; i += blockDim.x) S.sc[i] = 0.0;
   {
@@ -1130,7 +1152,7 @@ int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s, i
 // the all-reduced partials of outer iteration `it`, decided on the device (F_DEVSTOP): the same
 // rules as the host decision in piadmm_capi.cpp global_iteration.  gctl: [0] stop, [1] the stop
 // came at the collision test (NANLAST), [2] iterations executed, [3] some pair ever collided.
-__global__ void k_decide(DevArgs A, int it, const double* part) {
+__global__ void k_decide(DevArgs A, int t, int it, const double* part) {
   int* g = A.gctl;
   if (g[0]) return;
   const piadmm_config_t& c = A.cfg;
@@ -1144,13 +1166,17 @@ __global__ void k_decide(DevArgs A, int it, const double* part) {
   g[3] = 1;
   A.ghist[2 * it + 0] = rk;
   A.ghist[2 * it + 1] = sk;
+  if (!c.fixed_iters) {
+    scalar_tie(A, t, it, PIADMM_TIE_STOP, -1, 0, rk, c.eps_pri);
+    scalar_tie(A, t, it, PIADMM_TIE_STOP, -1, 1, sk, c.eps_dual);
+  }
   if (!c.fixed_iters && rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || (n_seen > 0.0 && n_bad == 0.0)))
     g[0] = 1;
 }
 
-int launch_decide(const DevArgs& a, int it, const double* part, hipStream_t s) {
+int launch_decide(const DevArgs& a, int t, int it, const double* part, hipStream_t s) {
   (void)hipGetLastError();
-  hipLaunchKernelGGL(k_decide, dim3(1), dim3(1), 0, s, a, it, part);
+  hipLaunchKernelGGL(k_decide, dim3(1), dim3(1), 0, s, a, t, it, part);
   return launch_rc(hipGetLastError());
 }
 

@@ -48,7 +48,7 @@ struct GCnt {
 
 // -------------------------------------------------------------------- X phase: one agent
 template <bool BIG>
-__device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GWave& W, GCnt& n) {
+__device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, int it, const GWave& W, GCnt& n) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, l = lid();
   const bool tl = l <= H;
@@ -137,6 +137,7 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GW
   n.inexact += (st & PIADMM_QP_INEXACT) ? 1 : 0;
   // round (casadi/main.py:103), pos_old = dynamic_update_local (:105)
   const double u = around(ustar[0], c.round_decimals);
+  if (c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_U, a, 0, ustar[0], l < H);
   double px, py, pth;
   rollout_r(xt3[0], xt3[1], xt3[2], s, s / c.L, (l < H) ? u : 0.0, c, H, c.pos_model != 0, px, py, pth);
   double* po = A.pos_old + (size_t)a * 2 * H1;
@@ -178,7 +179,7 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, const GW
 // -------------------------------------------------------------------- Z phase: one pair
 // Returns nothing; writes edge_active, and when the pair collides hat, lam, S, D, eres, dischk.
 // The collision test of pair e (casadi/main.py:110-113): writes edge_active, returns it.
-__device__ __forceinline__ bool g_ztest(const DevArgs& A, int e) {
+__device__ __forceinline__ bool g_ztest(const DevArgs& A, int e, int t, int it) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, l = lid();
   const bool tl = l <= H;
@@ -188,11 +189,14 @@ __device__ __forceinline__ bool g_ztest(const DevArgs& A, int e) {
   const double deff = A.deff[e];
   const double thr = c.collide_sq_thres ? deff * deff : deff;
   bool hit = false;
+  double d2 = 0.0;
   if (tl) {
     const double dx = p1[l] - p2[l], dy = p1[H1 + l] - p2[H1 + l];
-    hit = (dx * dx + dy * dy) < thr;
+    d2 = dx * dx + dy * dy;
+    hit = d2 < thr;
   }
   // the global-PI script has no collision test: its edge problem runs every iteration
+  if (!c.no_collision_gate) collide_tie(A, t, it, e, d2, tl, thr);
   const bool act = c.no_collision_gate ? true : wany(hit);
   if (l == 0) A.edge_active[e] = act ? 1 : 0;
   return act;
@@ -201,7 +205,7 @@ __device__ __forceinline__ bool g_ztest(const DevArgs& A, int e) {
 // The z-step of a colliding pair e: the pair QP, the hat rollouts, the dual update and the pair's
 // residual terms (casadi/main.py:121-173).
 template <bool BIG>
-__device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GWave& W, GCnt& n) {
+__device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, const GWave& W, GCnt& n) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, l = lid();
   const bool tl = l <= H;
@@ -311,6 +315,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
   double hx[2], hy[2], hth;
   for (int v = 0; v < 2; ++v) {
     const double uv = (l < H) ? around(uh[v], c.round_decimals) : 0.0;
+    if (c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_UHAT, e, v * H, uh[v], l < H);
     rollout(v ? xb : xa, A.spd[v ? v2 : v1], uv, c, H, true, hx[v], hy[v], hth);
   }
   double rr = 0.0, ss = 0.0, dchk;
@@ -437,6 +442,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
     qw[(7 + q) * WAVE + l] = qe.E[q] * ys[q];
     lw[q * WAVE + l] = lab[q];
   }
+  if (c.term_dist_check && l == 0) scalar_tie(A, t, it, PIADMM_TIE_DIST, e, 0, dchk, deff);
   if (l == 0) {
     A.eres[2 * e] = rfac * sqrt(rr);
     A.eres[2 * e + 1] = rfac * sqrt(ss);
@@ -450,15 +456,21 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, const GW
 // -------------------------------------------------------------------- step init / final
 // Seeds (casadi/main.py:48-49), the per-step reset of hat, lam and the PI accumulators (:52-63;
 // shifted one slot with warm_duals, optimizer.py:337-344), the warm labels of the previous step.
-__device__ __forceinline__ void g_step_init(const DevArgs& A, int ci, int w) {
+__device__ __forceinline__ void g_step_init(const DevArgs& A, int ci, int w, int t) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, l = lid();
   for (int i = A.comp_aptr[ci] + w; i < A.comp_aptr[ci + 1]; i += GW) {
     const int a = A.comp_alist[i];
     const double x = A.xt[3 * a], y = A.xt[3 * a + 1], th = A.xt[3 * a + 2], s = A.spd[a];
     if (l == 0) {
-      A.seed_g[2 * a] = around(x + c.dt * s * cos(th), c.round_decimals);
-      A.seed_g[2 * a + 1] = around(y + c.dt * s * sin(th), c.round_decimals);
+      const double sx = x + c.dt * s * cos(th), sy = y + c.dt * s * sin(th);
+      A.seed_g[2 * a] = around(sx, c.round_decimals);
+      A.seed_g[2 * a + 1] = around(sy, c.round_decimals);
+      double m;
+      if (c.round_decimals >= 0 && round_near(sx, c.round_decimals, A.tie_tol, &m))
+        tie_record(A, t, -1, PIADMM_TIE_ROUND_SEED, a, 0, m);
+      if (c.round_decimals >= 0 && round_near(sy, c.round_decimals, A.tie_tol, &m))
+        tie_record(A, t, -1, PIADMM_TIE_ROUND_SEED, a, 1, m);
     }
     // the previous step's final labels shifted by one time slot: a guess for the first polish
     const bool wo = A.warm_ok[a] != 0;
@@ -577,7 +589,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
 
   unsigned long long t_body = STAMP_T();
   if (first) {
-    g_step_init(A, ci, w);
+    g_step_init(A, ci, w, t);
     for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
     if (coop && ci == 0)
       for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) A.ghist[(size_t)slot * 2 * M + i] = NAN;
@@ -613,7 +625,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       unsigned long long t_xp = STAMP_T();
       for (int i = a0 + w; i < a1; i += GW) {
         const int a = A.comp_alist[i];
-        if (!A.owned || A.owned[a]) g_xstep<BIG>(A, a, t, W, n);
+        if (!A.owned || A.owned[a]) g_xstep<BIG>(A, a, t, it, W, n);
       }
       STAMP_ADD(ST_XSTEP, t_xp);
       unsigned long long t_sa = STAMP_T();
@@ -643,7 +655,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
     const bool deal = e1 - e0 <= GZMAX;
     if (deal) {
       for (int j = e0 + w; j < e1; j += GW) {
-        const bool act = g_ztest(A, A.comp_elist[j]);
+        const bool act = g_ztest(A, A.comp_elist[j], t, it);
         if (l == 0) s_zact[j - e0] = act ? 1 : 0;
       }
       __syncthreads();
@@ -658,9 +670,9 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
           mine = act && (k % GW == w);
           k += act ? 1 : 0;
         } else {
-          mine = g_ztest(A, e);
+          mine = g_ztest(A, e, t, it);
         }
-        if (mine) g_zstep<BIG>(A, e, t, W, n);
+        if (mine) g_zstep<BIG>(A, e, t, it, W, n);
       }
     }
     STAMP_ADD(ST_ZSTEP, t_zp);
@@ -684,6 +696,12 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
         const bool bad = seen && !(d > A.deff[e]);
         const bool act = cnt && A.edge_active[e] != 0;
         const double r0 = act ? A.eres[2 * e] : 0.0, r1 = act ? A.eres[2 * e + 1] : 0.0;
+        // split component: the pair's terms of this iteration's sum, added in the reference's
+        // order over the whole original component by k_graph_partials
+        if (A.eterm && in) {
+          A.eterm[2 * e] = r0;
+          A.eterm[2 * e + 1] = aliased ? 0.0 : r1;
+        }
         const unsigned long long bseen = __ballot(seen), bbad = __ballot(bad), bact = __ballot(act);
         const int npr = min(WAVE, e1 - j0);
         for (int k = 0; k < npr; ++k) {
@@ -728,6 +746,10 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       resid[2 * it + 1] = sk;
     }
     bool stop = !c.fixed_iters && !global && rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok);
+    if (!c.fixed_iters && !global && threadIdx.x == 0) {
+      scalar_tie(A, t, it, PIADMM_TIE_STOP, ci, 0, rk, c.eps_pri);
+      scalar_tie(A, t, it, PIADMM_TIE_STOP, ci, 1, sk, c.eps_dual);
+    }
     if (coop && !c.fixed_iters) {
       // global stop in-kernel: per-component partials, one grid barrier, the same fixed-order
       // sum in every workgroup (k_graph_partials sums in this order on the host-decided path)
@@ -766,6 +788,10 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       if (ci == 0 && threadIdx.x == 0) {
         A.ghist[((size_t)slot * M + it) * 2 + 0] = trk;
         A.ghist[((size_t)slot * M + it) * 2 + 1] = tsk;
+      }
+      if (ci == 0 && threadIdx.x == 0) {
+        scalar_tie(A, t, it, PIADMM_TIE_STOP, -1, 0, trk, c.eps_pri);
+        scalar_tie(A, t, it, PIADMM_TIE_STOP, -1, 1, tsk, c.eps_dual);
       }
       if (trk <= c.eps_pri && tsk <= c.eps_dual && (!c.term_dist_check || (tseen > 0.0 && tbad == 0.0))) stop = true;
     }
@@ -845,6 +871,11 @@ namespace pd {
 // Termination partials of the last iteration summed over components (host-decided global
 // termination in graph mode): the in-kernel (cooperative) order -- thread k accumulates
 // components k, k + GW*WAVE, ... in order, then the per-thread sums in thread order.
+// Components split over workgroups (A.sum_C > 0): rk and sk are instead the reference's sums over
+// the ORIGINAL components -- each component's pairs in increasing pair order, then the components
+// in order (casadi/main.py:165-173; the oracle's comp_r sum) -- from the pairs' terms the blocks'
+// T phases wrote (A.eterm), wave 0 summing rk and wave 1 sk: bit-identical to the same job on one
+// workgroup per component.  (The counts -- active pairs, distance checks -- are integers: any order.)
 __global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double* out, int devstop) {
   if (devstop && A.gctl[0]) return;
   constexpr int NT = GW * WAVE;
@@ -854,10 +885,28 @@ __global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double*
     for (int q = 0; q < 5; ++q) v[q] += A.cpart[(size_t)ci * 5 + q];
   for (int q = 0; q < 5; ++q) red[q][threadIdx.x] = v[q];
   __syncthreads();
-  if (threadIdx.x < 5) {
+  const bool split = A.sum_C > 0;
+  if (threadIdx.x < 5 && !(split && threadIdx.x < 2)) {
     double tot = 0.0;
     for (int k = 0; k < NT; ++k) tot += red[threadIdx.x][k];
     out[threadIdx.x] = tot;
+  }
+  if (split) {
+    const int q = threadIdx.x >> 6;            // wave 0: rk, wave 1: sk
+    const int l = lid();
+    double tot = 0.0;
+    for (int k = 0; k < A.sum_C; ++k) {
+      const int j1 = A.sum_cptr[k + 1];
+      double cs = 0.0;
+      for (int j0 = A.sum_cptr[k]; j0 < j1; j0 += WAVE) {
+        const int j = j0 + l;
+        const double r = j < j1 ? A.eterm[2 * A.sum_elist[j] + q] : 0.0;
+        const int n = min(WAVE, j1 - j0);
+        for (int i = 0; i < n; ++i) cs += rdl(r, i);
+      }
+      tot += cs;
+    }
+    if (l == 0) out[q] = tot;
   }
 }
 

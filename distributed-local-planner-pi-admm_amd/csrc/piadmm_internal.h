@@ -121,6 +121,24 @@ struct DevArgs {
   double* rho_pi;           // E   rho of the pair (casadi_old_PI_ADMM/main.py:139)
   double* xcache_coef;      // N   x-step P coefficient 2 Pnorm + sum_e rho_e the caches were built for
   double* ecache_rho;       // E   pair penalty the pair's polish tables were built for
+  // ---- components split over workgroups (graph mode, term_global): the job's residual sums in the
+  // reference's order -- per ORIGINAL connected component its pairs in increasing pair order, then
+  // the components in order (casadi/main.py:165-173; the oracle's comp_r sum) -- instead of the
+  // blocks' partial sums.  The T phase writes each pair's effective terms, k_graph_partials sums them.
+  double* eterm;            // E*2 (rk_e, sk_e) of this iteration's sum (0: inactive / not counted / aliased)
+  const int* sum_cptr;      // sum_C+1 pairs of original component k: sum_elist[sum_cptr[k] .. sum_cptr[k+1])
+  const int* sum_elist;     // E
+  int sum_C;                // 0: no split (the blocks ARE the components)
+  // ---- near-tie log (piadmm_get_near_ties): the reference's discrete decisions taken within
+  // tie_tol of their threshold -- rounding (casadi/main.py:48-49,103,153), the collision test
+  // (:112-113), the stop test (:174) and MATLAB's distance check -- where two exact
+  // implementations may resolve them differently
+  unsigned long long* tie_cnt;   // PIADMM_TIE_KINDS counts
+  int* tie_n;                    // events so far (may exceed tie_cap)
+  int* tie_ev;                   // tie_cap x 6 ints: step, iter, kind, id, index, 0
+  double* tie_mg;                // tie_cap margins
+  int tie_cap;
+  double tie_tol;
 };
 
 // Big mode: rows of the per-wave x-step factor scratch (working sets of up to H + 2 rows:
@@ -207,7 +225,7 @@ int launch_detect_emit(const double* xs, const double* rs, int n, double inv_cs,
                        const int* order, const int* off, int* out, hipStream_t s);
 bool graph_coop_fits(const DevArgs& a, int device);
 int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s, int devstop = 0);
-int launch_decide(const DevArgs& a, int it, const double* part, hipStream_t s);
+int launch_decide(const DevArgs& a, int t, int it, const double* part, hipStream_t s);
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s, int devstop = 0);
 int launch_resid_history(const DevArgs& a, int nsteps, double* out, hipStream_t s);

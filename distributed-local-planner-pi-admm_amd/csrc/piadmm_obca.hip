@@ -1228,6 +1228,7 @@ int32_t piadmm_obca_destroy(piadmm_obca_t h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->d_rec) { (void)hipFree(h->d_rec); (void)hipFree(h->d_out); (void)hipFree(h->d_ist); }
+  if (h->d_stamps) (void)hipFree(h->d_stamps);
   if (h->e0) (void)hipEventDestroy(h->e0);
   if (h->e1) (void)hipEventDestroy(h->e1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1242,6 +1243,9 @@ int32_t piadmm_obca_upload(piadmm_obca_t h, const double* recs, int32_t n) {
   if (!recs || n <= 0) return fail(h, PIADMM_E_ARG, "obca_upload: recs / n");
   if (int rc = check_recs(h, recs, n)) return rc;
   OHIP(h, hipSetDevice(h->device));
+  // no batch until this upload succeeds: a failed reallocation or copy must not leave a batch size
+  // that a later obca_run would launch on freed (null) buffers
+  h->n = 0;
   if (int rc = ensure(h, n)) return rc;
   OHIP(h, hipMemcpyAsync(h->d_rec, recs, (size_t)n * obca::REC * sizeof(double), hipMemcpyHostToDevice, h->stream));
   OHIP(h, hipStreamSynchronize(h->stream));
@@ -1287,7 +1291,9 @@ int32_t piadmm_obca_debug_stamps(piadmm_obca_t h, uint64_t* out, int32_t n) {
   if (!h) return PIADMM_E_ARG;
   if (!h->d_stamps) return fail(h, PIADMM_E_STATE, "not a stamps build (make stamps)");
   if (n != h->n * obca::NSTAMP) return fail(h, PIADMM_E_ARG, "obca_debug_stamps: n must be 16 x the batch");
-  OHIP(h, hipMemcpy(out, h->d_stamps, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  OHIP(h, hipSetDevice(h->device));
+  OHIP(h, hipMemcpyAsync(out, h->d_stamps, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+  OHIP(h, hipStreamSynchronize(h->stream));
   return 0;
 }
 

@@ -85,6 +85,10 @@ SYMBOLS = [
                                           _P(ctypes.c_uint8)]),
     ("piadmm_set_allreduce", c_i32, [_H, ctypes.c_void_p, ctypes.c_void_p]),
     ("piadmm_candidate_pairs", c_i32, [_H, _dp, _dp, c_i32, _ip, c_i32, _ip, _P(ctypes.c_float)]),
+    ("piadmm_set_tie_tolerance", c_i32, [_H, c_dbl]),
+    ("piadmm_get_near_ties", c_i32, [_H, _P(ctypes.c_uint64), ctypes.c_void_p, c_i32, _ip]),
+    ("piadmm_get_step_state", c_i32, [_H, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    ("piadmm_set_state", c_i32, [_H, _dp, _dp, _dp, _dp, _dp, _dp, _dp]),
     ("piadmm_obca_create", c_i32, [c_i32, _P(_H)]),
     ("piadmm_obca_destroy", c_i32, [_H]),
     ("piadmm_obca_last_error", ctypes.c_char_p, [_H]),
@@ -95,6 +99,12 @@ SYMBOLS = [
     ("piadmm_obca_download", c_i32, [_H, _dp, _ip, c_i32]),
     ("piadmm_obca_debug_stamps", c_i32, [_H, _P(ctypes.c_uint64), c_i32]),
 ]
+
+# piadmm_near_tie_t (include/piadmm.h, ABI 6) as a NumPy record
+TIE_KINDS = ("round_u", "round_uhat", "round_seed", "collide", "stop", "dist")
+TIE_DTYPE = np.dtype([("step", np.int32), ("iter", np.int32), ("kind", np.int32), ("id", np.int32),
+                      ("index", np.int32), ("reserved", np.int32), ("margin", np.float64)])
+TIE_CAP = 4096
 
 # piadmm_allreduce_fn: int32_t (*)(void* ctx, double* buf, int64_t n)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_i32, ctypes.c_void_p, _dp, ctypes.c_int64)

@@ -91,6 +91,37 @@ def load_run(path: str) -> RunRecord:
                      resid=d["resid"], dual_max=d["dual_max"], dual_min=d["dual_min"], meta=meta)
 
 
+CHECKPOINT_KEYS = ("xt", "hat", "lam", "S", "D", "last_hat", "rho_pi")
+
+
+def save_checkpoint(path: str, state: dict, cfg=None) -> str:
+    """Checkpoint of an MPC run between two steps (the ``.npz`` dump of xt,
+    duals, S, D): ``state`` from ``PI_ADMM_MI355X.step_state()`` (or the oracle's edge state) --
+    xt, the pair state hat / lam / S / D / last_hat (carried by warm_duals, a12), the global-PI
+    pair penalties rho_pi -- and the next reference time index ``t``.  The reference keeps this
+    state only in Python variables (``casadi/main.py:52-63,180``)."""
+    base = path[:-4] if path.endswith(".npz") else path
+    arrs = {k: np.asarray(state[k], np.float64) for k in CHECKPOINT_KEYS if state.get(k) is not None}
+    arrs["t"] = np.array(int(state.get("t", 0)), np.int64)
+    if cfg is not None:
+        arrs["cfg_json"] = np.array(json.dumps(dataclasses.asdict(cfg), sort_keys=True))
+    np.savez_compressed(base + ".npz", **arrs)
+    return base + ".npz"
+
+
+def load_checkpoint(path: str, cfg=None) -> dict:
+    """The state :func:`save_checkpoint` wrote (NumPy only, no pickles), for
+    ``PI_ADMM_MI355X.set_state``.  With ``cfg``: refuses a checkpoint of another configuration."""
+    base = path[:-4] if path.endswith(".npz") else path
+    d = np.load(base + ".npz", allow_pickle=False)
+    if cfg is not None and "cfg_json" in d.files:
+        if json.loads(str(d["cfg_json"])) != json.loads(json.dumps(dataclasses.asdict(cfg), sort_keys=True)):
+            raise ValueError("checkpoint was written with another configuration")
+    st = {k: d[k] for k in CHECKPOINT_KEYS if k in d.files}
+    st["t"] = int(d["t"])
+    return st
+
+
 def plot_run(rec: RunRecord, path: str, agents=None) -> str:
     """The reference's figure (``casadi/main.py:206-220``): one scatter per vehicle of its
     positions over the run; more than two agents get one colour each."""

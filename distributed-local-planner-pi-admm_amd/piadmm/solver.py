@@ -201,7 +201,54 @@ class PI_ADMM_MI355X:
         return np.array(buf, dtype=np.int64).reshape(self.C, 8)
 
     def reset_counters(self):
+        """Zero the work counters and the near-tie log."""
         self._check(self.lib.piadmm_reset_counters(self._h))
+
+    def set_tie_tolerance(self, tol: float):
+        """Tolerance of the near-tie log (default 1e-9; piadmm_set_tie_tolerance)."""
+        self._check(self.lib.piadmm_set_tie_tolerance(self._h, float(tol)))
+
+    def near_ties(self):
+        """(counts per kind, events) of the near-tie log since the last reset (piadmm_get_near_ties):
+        the reference's discrete decisions -- rounding (casadi/main.py:48-49,103,153), the collision
+        test (:112-113), the stop test (:174), MATLAB's distance check -- taken within the tolerance
+        of their threshold.  events: a NumPy record array (step, iter, kind, id, index, margin)."""
+        cnt = (ctypes.c_uint64 * len(_lib.TIE_KINDS))()
+        ev = np.zeros(_lib.TIE_CAP * 2, _lib.TIE_DTYPE)
+        n = ctypes.c_int32()
+        self._check(self.lib.piadmm_get_near_ties(self._h, cnt, ev.ctypes.data, ev.size, ctypes.byref(n)))
+        return dict(zip(_lib.TIE_KINDS, (int(v) for v in cnt))), ev[:min(int(n.value), ev.size)].copy()
+
+    def step_state(self) -> dict:
+        """The state that carries into the next MPC step (piadmm_get_step_state): xt, and hat, lam,
+        S, D, last_hat (warm_duals, a12) and the global-PI pair penalties rho_pi -- a checkpoint."""
+        H1 = self.cfg.H + 1
+        out = dict(xt=np.empty((self.N, 3)), hat=np.empty((self.E, 2, 2, H1)), lam=np.empty((self.E, 2, 2, H1)),
+                   S=np.empty((self.E, 2, 2, H1)), D=np.empty((self.E, 2, 2, H1)),
+                   last_hat=np.empty((self.E, 2, 2, H1)), rho_pi=np.empty(self.E))
+        e = (lambda k: _lib.dptr(out[k]) if self.E else None)
+        self._check(self.lib.piadmm_get_step_state(self._h, _lib.dptr(out["xt"]), e("hat"), e("lam"), e("S"),
+                                                   e("D"), e("last_hat"), e("rho_pi")))
+        out["t"] = self.t
+        return out
+
+    def set_state(self, st: dict):
+        """Resume from a checkpoint (:meth:`step_state`, or piadmm.io.load_checkpoint): xt and the
+        carried pair state; the next :meth:`mpc_step` runs at st["t"] when given."""
+        H1 = self.cfg.H + 1
+        xt = np.ascontiguousarray(st["xt"], np.float64).reshape(self.N, 3)
+
+        def arr(k, shape):
+            v = st.get(k)
+            if v is None or not self.E:
+                return None
+            return np.ascontiguousarray(v, np.float64).reshape(shape)
+        parts = [arr(k, (self.E, 2, 2, H1)) for k in ("hat", "lam", "S", "D", "last_hat")]
+        rho = arr("rho_pi", (self.E,))
+        self._check(self.lib.piadmm_set_state(self._h, _lib.dptr(xt), *[_lib.dptr(p) for p in parts], _lib.dptr(rho)))
+        self.xt = xt.copy()
+        if st.get("t") is not None:
+            self.t = int(st["t"])
 
     def set_xt(self, xt: np.ndarray):
         xt = np.ascontiguousarray(xt, np.float64)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PIADMM_ABI_VERSION 5
+#define PIADMM_ABI_VERSION 6
 
 enum {
   PIADMM_OK = 0,
@@ -189,7 +189,9 @@ int32_t piadmm_get_state(piadmm_handle_t h, double* xt, double* u, double* pos_o
  * over all agents with term_global, else once every component has stopped -- a stopped
  * component keeps its state while the others continue).  Calling on after a stop, or out of
  * order, is PIADMM_E_STATE.  piadmm_step_finish then propagates (casadi/main.py:185-192); no
- * other step call is accepted while a host-stepped step is open.  Not for sharded graphs. */
+ * other step call is accepted while a host-stepped step is open.  (ABI 6: also a sharded graph --
+ * every rank steps, the exchange all-reduce inside each call -- and a component split over
+ * workgroups.) */
 int32_t piadmm_outer_iter(piadmm_handle_t h, int32_t t, int32_t it, int32_t* stop_out);
 int32_t piadmm_step_finish(piadmm_handle_t h, double* xt_out /* N x 3 */, double* u_out /* N x H */);
 
@@ -206,6 +208,55 @@ int32_t piadmm_get_counters(piadmm_handle_t h, uint64_t* out8);
 int32_t piadmm_reset_counters(piadmm_handle_t h);
 /* The same counters per component (C x 8 uint64, n >= 8*C). */
 int32_t piadmm_get_component_counters(piadmm_handle_t h, uint64_t* out, int32_t n);
+
+/* ABI 6: near-tie log.  The reference's loop takes discrete decisions --
+ * rounding to round_decimals (casadi/main.py:48-49,103,153), the collision test d^2 < thr
+ * (:112-113), the stop test rk <= eps_pri, sk <= eps_dual (:174) and MATLAB's distance check
+ * dis_vec(2) > dis_thres (ADMM_CVX_..._PI_antiwindup.m:202).  Two exact implementations (this
+ * library, a CPU port, the reference) agree on every continuous value to rounding, so their
+ * trajectories can part only where such a decision falls within rounding of its threshold.  The
+ * library records every decision taken within `tol` of its threshold (default 1e-9):
+ *   PIADMM_TIE_ROUND_U     an x-step control        id = agent, index = horizon slot k
+ *   PIADMM_TIE_ROUND_UHAT  a pair (edge) control    id = pair,  index = side * H + k
+ *   PIADMM_TIE_ROUND_SEED  a seed                   id = agent, index = 0 (x) / 1 (y)
+ *     margin = value - nearest rounding boundary (k + 1/2) 10^-d, absolute, |margin| <= tol
+ *   PIADMM_TIE_COLLIDE     the collision test       id = pair, index = closest slot k,
+ *     margin = (min_k d_k^2 - thr) / thr (relative)
+ *   PIADMM_TIE_STOP        the stop test            id = component (-1: the job under term_global),
+ *     index 0: rk vs eps_pri, 1: sk vs eps_dual, margin = (r - eps) / eps (relative)
+ *   PIADMM_TIE_DIST        the distance check       id = pair (-1: unknown), margin = (d - d_eff) / d_eff
+ * Each event carries the reference time index of the MPC step and the outer iteration (-1: the
+ * step's seeds).  Counts and events accumulate until piadmm_reset_counters; at most
+ * PIADMM_TIE_CAP events are kept (*n_events reports the total). */
+#define PIADMM_TIE_ROUND_U 0
+#define PIADMM_TIE_ROUND_UHAT 1
+#define PIADMM_TIE_ROUND_SEED 2
+#define PIADMM_TIE_COLLIDE 3
+#define PIADMM_TIE_STOP 4
+#define PIADMM_TIE_DIST 5
+#define PIADMM_TIE_KINDS 6
+#define PIADMM_TIE_CAP 4096
+typedef struct piadmm_near_tie {
+  int32_t step, iter, kind, id, index, reserved;
+  double margin;
+} piadmm_near_tie_t;
+int32_t piadmm_set_tie_tolerance(piadmm_handle_t h, double tol);
+int32_t piadmm_get_near_ties(piadmm_handle_t h, uint64_t* counts /* PIADMM_TIE_KINDS, may be NULL */,
+                             piadmm_near_tie_t* events /* may be NULL */, int32_t max_events, int32_t* n_events);
+
+/* ABI 6: checkpoint / resume.  The state that carries from one MPC step to the
+ * next: xt (N x 3) and, for warm_duals (a12) and the global-PI law, hat / lam / S / D / last_hat
+ * (E x 2 x 2 x (H+1), the layout of piadmm_get_state; last_hat = last_iter_hat_pos,
+ * casadi/main.py:180) and the global-PI pair penalties rho_pi (E).  piadmm_get_step_state reads it
+ * after a step; piadmm_set_state writes it before the next (any pointer but xt may be NULL: that
+ * part is zeroed, as at the reference's per-step reset, casadi/main.py:52-63; rho_pi NULL: the
+ * configured rho).  A run resumed from a checkpoint continues like the uninterrupted one, to
+ * rounding: the QP solvers' warm starts (active sets, labels) are not part of the checkpoint, and
+ * they are guesses only -- every answer is the certified minimiser of the same QP. */
+int32_t piadmm_get_step_state(piadmm_handle_t h, double* xt, double* hat, double* lam, double* S, double* D,
+                              double* last_hat, double* rho_pi);
+int32_t piadmm_set_state(piadmm_handle_t h, const double* xt, const double* hat, const double* lam,
+                         const double* S, const double* D, const double* last_hat, const double* rho_pi);
 
 /* Multi-GPU (term_global): one process per GPU, one handle each, joined by an RCCL
  * communicator over xGMI.  Rank 0 calls piadmm_comm_unique_id and ships the 128 bytes to

@@ -46,6 +46,10 @@ def load():
         lib.piadmm_cpu_run_graph.argtypes = [ctypes.POINTER(_Cfg), ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int,
                                              P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P, P]
         lib.piadmm_cpu_run_graph.restype = ctypes.c_int
+        lib.piadmm_cpu_set_tie_tol.argtypes = [ctypes.c_double]
+        lib.piadmm_cpu_set_tie_tol.restype = None
+        lib.piadmm_cpu_get_ties.argtypes = [P, P, P, ctypes.c_int]
+        lib.piadmm_cpu_get_ties.restype = ctypes.c_int
         if lib.piadmm_cpu_cfg_size() != ctypes.sizeof(_Cfg):
             raise RuntimeError("libpiadmm_cpu.so config layout differs from oracle/cpu_bopt.py")
         _lib = lib
@@ -69,11 +73,18 @@ def is_tiled(scn) -> bool:
         scn.edges, np.stack([np.arange(0, N, 2), np.arange(1, N, 2)], 1))
 
 
-def run(cfg, scn, n_steps: int, threads: int = 1, t0: int = 0, records: bool = True):
+TIE_DTYPE = np.dtype([("step", np.int32), ("iter", np.int32), ("kind", np.int32), ("id", np.int32),
+                      ("index", np.int32), ("reserved", np.int32), ("margin", np.float64)])
+TIE_KINDS = ("round_u", "round_uhat", "round_seed", "collide", "stop", "dist")
+
+
+def run(cfg, scn, n_steps: int, threads: int = 1, t0: int = 0, records: bool = True, tie_tol: float = 1e-9):
     """n_steps MPC steps of any scenario (candidate graph scn.edges).  Returns dict(seconds, xt
-    (S,N,3), u (S,N,H), iters (S,C), resid (S,C,max_outer,2) NaN-padded, counters); C = connected
-    components in order of their first agent (the oracle's Scenario.components())."""
+    (S,N,3), u (S,N,H), iters (S,C), resid (S,C,max_outer,2) NaN-padded, counters, ties); C =
+    connected components in order of their first agent (the oracle's Scenario.components()).
+    ties = (counts per kind, events): the near-tie log (include/piadmm.h piadmm_get_near_ties)."""
     lib = load()
+    lib.piadmm_cpu_set_tie_tol(float(tie_tol))
     c = _cfg(cfg)
     N, H, MO = scn.n_agents, cfg.H, cfg.max_outer
     C = int(scn.components()[1])
@@ -94,8 +105,17 @@ def run(cfg, scn, n_steps: int, threads: int = 1, t0: int = 0, records: bool = T
                                   cnt.ctypes.data)
     if rc != C:
         raise RuntimeError(f"piadmm_cpu_run_graph failed ({rc})")
+    tcnt = np.zeros(len(TIE_KINDS), np.int64)
+    ev = np.zeros((4096, 6), np.int32)
+    mg = np.zeros(4096)
+    nt = lib.piadmm_cpu_get_ties(tcnt.ctypes.data, ev.ctypes.data, mg.ctypes.data, 4096)
+    ties = np.zeros(nt, TIE_DTYPE)
+    for k, f in enumerate(("step", "iter", "kind", "id", "index", "reserved")):
+        ties[f] = ev[:nt, k]
+    ties["margin"] = mg[:nt]
     return {"seconds": secs.value, "xt": xt, "u": u, "iters": iters, "resid": resid,
-            "counters": dict(zip(("x_qps", "z_qps", "x_hits", "gi_steps", "inexact"), cnt.tolist()))}
+            "counters": dict(zip(("x_qps", "z_qps", "x_hits", "gi_steps", "inexact"), cnt.tolist())),
+            "ties": (dict(zip(TIE_KINDS, tcnt.tolist())), ties)}
 
 
 def time_baseline(cfg, n_tiles: int, budget_s: float, n_steps: int = 20, threads: int | None = None,

@@ -607,7 +607,39 @@ struct Ctx {
   int T;
   Run& run;
   int t;                 // MPC step (reference slice t .. t+H)
+  int it = 0;            // outer iteration (near-tie log)
 };
+
+// ---------------------------------------------------------------- near-tie log
+// The mirror of piadmm_get_near_ties (include/piadmm.h, oracle TieLog): the reference's discrete
+// decisions taken within g_tie_tol of their threshold.  Rare: one critical section per event.
+enum { TIE_ROUND_U = 0, TIE_ROUND_UHAT, TIE_ROUND_SEED, TIE_COLLIDE, TIE_STOP, TIE_DIST, TIE_KINDS };
+double g_tie_tol = 1e-9;
+std::vector<int> g_tie_ev;          // 6 ints per event: step, iter, kind, id, index, 0
+std::vector<double> g_tie_mg;
+long long g_tie_cnt[TIE_KINDS] = {};
+
+void tie_add(int t, int it, int kind, int id, int idx, double m) {
+#pragma omp critical(piadmm_ties)
+  {
+    ++g_tie_cnt[kind];
+    if (g_tie_mg.size() < 4096) {
+      const int e[6] = {t, it, kind, id, idx, 0};
+      g_tie_ev.insert(g_tie_ev.end(), e, e + 6);
+      g_tie_mg.push_back(m);
+    }
+  }
+}
+void tie_round(const CpuCfg& c, int t, int it, int kind, int id, int idx, double x) {
+  if (c.round_decimals < 0) return;
+  double f = 1.0;
+  for (int i = 0; i < c.round_decimals; ++i) f *= 10.0;
+  const double y = x * f, b = std::floor(y) + 0.5;
+  if (std::fabs(y - b) <= g_tie_tol * f) tie_add(t, it, kind, id, idx, (y - b) / f);
+}
+void tie_scalar(int t, int it, int kind, int id, int idx, double v, double thr) {
+  if (std::fabs(v - thr) <= g_tie_tol * std::fabs(thr)) tie_add(t, it, kind, id, idx, (v - thr) / thr);
+}
 
 // x-step of agent a (casadi/main.py:81-106; oracle xstep_qp / solve_xstep)
 void x_step(Ctx& X, World& Wd, int a, Work& W) {
@@ -689,7 +721,10 @@ void x_step(Ctx& X, World& Wd, int a, Work& W) {
     if (ok) ok = certify(Q, A.ws, x, lin_none);
     if (!ok) ++X.run.inexact;
   }
-  for (int k = 0; k < H; ++k) A.u[k] = around(x[k], c.round_decimals);
+  for (int k = 0; k < H; ++k) {
+    A.u[k] = around(x[k], c.round_decimals);
+    tie_round(c, X.t, X.it, TIE_ROUND_U, a, k, x[k]);
+  }
   if (c.pos_model == 0) rollout_linear(A.xt, A.u.data(), A.spd, c.dt, c.L, H, A.px.data(), A.py.data());
   else rollout_nonlinear(A.xt, A.u.data(), A.spd, c.dt, c.L, H, A.px.data(), A.py.data());
 }
@@ -774,7 +809,10 @@ void z_step(Ctx& X, World& Wd, int e, int t, Work& W) {
   P.pws_t = t;
   std::vector<double> uh(H), hx(R), hy(R);
   for (int d = 0; d < 2; ++d) {
-    for (int k = 0; k < H; ++k) uh[k] = around(x[d * H + k], c.round_decimals);
+    for (int k = 0; k < H; ++k) {
+      uh[k] = around(x[d * H + k], c.round_decimals);
+      tie_round(c, t, X.it, TIE_ROUND_UHAT, e, d * H + k, x[d * H + k]);
+    }
     rollout_nonlinear(ag[d]->xt, uh.data(), ag[d]->spd, c.dt, c.L, H, hx.data(), hy.data());
     double* ht = &P.hat[(size_t)d * 2 * R];
     for (int k = 0; k < R; ++k) {
@@ -827,12 +865,15 @@ void dual_update(const CpuCfg& c, World& Wd, Pair& P, const double* dist) {
 
 // seeds (casadi/main.py:48-49), the per-step reset of the pair state (:52-63; with warm_duals the
 // previous step's shifted one slot, optimizer.py:337-344 / oracle shift_horizon), safety distance
-void begin_step(const CpuCfg& c, World& Wd, Comp& C, bool first_step) {
+void begin_step(const CpuCfg& c, World& Wd, Comp& C, bool first_step, int t) {
   const int R = c.H + 1;
   for (int a : C.agents) {
     Agent& A = Wd.ag[a];
-    A.seeds[0] = around(A.xt[0] + c.dt * A.spd * std::cos(A.xt[2]), c.round_decimals);
-    A.seeds[1] = around(A.xt[1] + c.dt * A.spd * std::sin(A.xt[2]), c.round_decimals);
+    const double sx = A.xt[0] + c.dt * A.spd * std::cos(A.xt[2]), sy = A.xt[1] + c.dt * A.spd * std::sin(A.xt[2]);
+    A.seeds[0] = around(sx, c.round_decimals);
+    A.seeds[1] = around(sy, c.round_decimals);
+    tie_round(c, t, -1, TIE_ROUND_SEED, a, 0, sx);
+    tie_round(c, t, -1, TIE_ROUND_SEED, a, 1, sy);
   }
   for (int e : C.pairs) {
     Pair& P = Wd.pr[e];
@@ -863,6 +904,7 @@ void iterate(Ctx& X, World& Wd, Comp& C, int t, int it, Work& W) {
   const CpuCfg& c = X.c;
   const int R = c.H + 1;
   C.iters = it + 1;
+  X.it = it;
   for (int a : C.agents) x_step(X, Wd, a, W);
   double rk = 0.0, sk = 0.0, nact = 0.0, nseen = 0.0, nbad = 0.0;
   for (int e : C.pairs) {
@@ -870,9 +912,25 @@ void iterate(Ctx& X, World& Wd, Comp& C, int t, int it, Work& W) {
     const Agent &a0 = Wd.ag[P.v[0]], &a1 = Wd.ag[P.v[1]];
     const double thr = c.collide_sq_thres ? P.d_eff * P.d_eff : P.d_eff;
     bool col = c.no_collision_gate != 0;
+    double dmin2 = INFINITY;
+    int kmin = 0;
     for (int k = 0; k < R && !col; ++k) {
       const double dx = a0.px[k] - a1.px[k], dy = a0.py[k] - a1.py[k];
-      col = (dx * dx + dy * dy) < thr;
+      const double d2 = dx * dx + dy * dy;
+      col = d2 < thr;
+      if (d2 < dmin2) { dmin2 = d2; kmin = k; }
+    }
+    // near tie of the test (oracle TieLog.collide): no slot decisively below, the minimum within tol
+    // (a colliding pair's scan stops at its first hit, below thr (1 - tol) unless that hit is a tie)
+    if (!c.no_collision_gate && (!col || dmin2 >= thr * (1.0 - g_tie_tol)) && dmin2 <= thr * (1.0 + g_tie_tol)) {
+      bool lo = false;
+      for (int k = 0; k < R; ++k) {
+        const double dx = a0.px[k] - a1.px[k], dy = a0.py[k] - a1.py[k];
+        const double d2 = dx * dx + dy * dy;
+        lo |= d2 < thr * (1.0 - g_tie_tol);
+        if (d2 < dmin2) { dmin2 = d2; kmin = k; }
+      }
+      if (!lo) tie_add(t, it, TIE_COLLIDE, e, kmin, (dmin2 - thr) / thr);
     }
     P.active = col;
     if (col) {
@@ -884,6 +942,7 @@ void iterate(Ctx& X, World& Wd, Comp& C, int t, int it, Work& W) {
       }
       dual_update(c, Wd, P, dist);
       P.dis_chk = dist[1];
+      if (c.term_dist_check) tie_scalar(t, it, TIE_DIST, e, 0, P.dis_chk, P.d_eff);
       P.seen = true;
       // residuals (oracle pair_residuals): v1 side only, times 2
       const double* hat0 = &P.hat[0];
@@ -917,13 +976,17 @@ void iterate(Ctx& X, World& Wd, Comp& C, int t, int it, Work& W) {
 }
 
 // stop rules of one termination group (casadi/main.py:115-118,174-181); part = summed partials
-void decide(const CpuCfg& c, const double* part, bool& g_flag, bool& g_alias, bool& g_done) {
+void decide(const CpuCfg& c, const double* part, bool& g_flag, bool& g_alias, bool& g_done, int t, int it, int gid) {
   const double rk = part[0], sk = part[1], n_act = part[2], n_seen = part[3], n_bad = part[4];
   if (n_act == 0 && !g_flag && !c.fixed_iters) {
     g_done = true;
     return;
   }
   g_flag = true;
+  if (!c.fixed_iters) {
+    tie_scalar(t, it, TIE_STOP, gid, 0, rk, c.eps_pri);
+    tie_scalar(t, it, TIE_STOP, gid, 1, sk, c.eps_dual);
+  }
   const bool dist_ok = n_seen > 0 && n_bad == 0;
   if (!c.fixed_iters && rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok)) {
     g_done = true;
@@ -967,6 +1030,17 @@ extern "C" {
 
 int piadmm_cpu_cfg_size() { return (int)sizeof(CpuCfg); }
 
+// Near-tie log of the last run (the mirror of piadmm_get_near_ties): tolerance, counts per kind,
+// events (6 ints + margin each, at most cap).  Returns the number of events kept.
+void piadmm_cpu_set_tie_tol(double tol) { g_tie_tol = tol; }
+int piadmm_cpu_get_ties(long long* counts, int* ev, double* mg, int cap) {
+  if (counts) std::memcpy(counts, g_tie_cnt, sizeof(g_tie_cnt));
+  const int n = std::min<int>((int)g_tie_mg.size(), cap);
+  if (ev) std::memcpy(ev, g_tie_ev.data(), sizeof(int) * 6 * (size_t)n);
+  if (mg) std::memcpy(mg, g_tie_mg.data(), sizeof(double) * (size_t)n);
+  return n;
+}
+
 // Runs n_steps MPC steps (t = t0 ...) of N agents with the E candidate pairs `edges` (E x 2,
 // v1 < v2) on `threads` OpenMP threads, OpenMP over connected components (labelled in order of
 // their first agent, the oracle's Scenario.components(); agents and pairs of a component in
@@ -982,6 +1056,9 @@ int piadmm_cpu_run_graph(const CpuCfg* cfg, int N, const double* spd, const doub
   if (H < 3 || H > 63 || N < 1 || E < 0 || t0 + n_steps + H > T || MO < 1) return -1;
   if (c.dual_mode != 0 && c.dual_mode != 1) return -1;
   if (threads < 1) threads = 1;
+  g_tie_ev.clear();
+  g_tie_mg.clear();
+  for (auto& v : g_tie_cnt) v = 0;
   World Wd;
   Wd.ag.resize(N);
   Wd.pr.resize(E);
@@ -1044,12 +1121,12 @@ int piadmm_cpu_run_graph(const CpuCfg* cfg, int N, const double* spd, const doub
         Ctx X{c, ref, T, run, t};
         thread_local Work W;
         Comp& Cm = Wd.comps[k];
-        begin_step(c, Wd, Cm, st == 0);
+        begin_step(c, Wd, Cm, st == 0, t);
         bool gf = false, ga = false;
         for (int it = 0; it < MO && !Cm.done; ++it) {
           iterate(X, Wd, Cm, t, it, W);
           bool gd = false;
-          decide(c, Cm.part, gf, ga, gd);
+          decide(c, Cm.part, gf, ga, gd, t, it, k);
           Cm.done = gd;
           after_decide(c, Wd, Cm, gf, ga);
         }
@@ -1057,7 +1134,7 @@ int piadmm_cpu_run_graph(const CpuCfg* cfg, int N, const double* spd, const doub
       }
     } else {
       // the reference's global scope: one stop decision per outer iteration over all components
-      for (int k = 0; k < C; ++k) begin_step(c, Wd, Wd.comps[k], st == 0);
+      for (int k = 0; k < C; ++k) begin_step(c, Wd, Wd.comps[k], st == 0, t);
       bool gf = false, ga = false, gd = false;
       for (int it = 0; it < MO && !gd; ++it) {
 #pragma omp parallel for schedule(dynamic, 4) num_threads(threads)
@@ -1070,7 +1147,7 @@ int piadmm_cpu_run_graph(const CpuCfg* cfg, int N, const double* spd, const doub
         double part[5] = {0, 0, 0, 0, 0};
         for (int k = 0; k < C; ++k)                 // component order (the oracle's sum)
           for (int j = 0; j < 5; ++j) part[j] += Wd.comps[k].part[j];
-        decide(c, part, gf, ga, gd);
+        decide(c, part, gf, ga, gd, t, it, -1);
         for (int k = 0; k < C; ++k) {
           Wd.comps[k].done = gd;
           after_decide(c, Wd, Wd.comps[k], gf, ga);   // recorded unless no pair ever collided (gf)

@@ -284,6 +284,45 @@ def shift_horizon(a):
     return np.concatenate([a[..., 1:], a[..., -1:]], axis=-1)
 
 
+# ----------------------------------------------------------------------------- near ties
+# Kinds of include/piadmm.h (PIADMM_TIE_*): the reference's discrete decisions.
+TIE_ROUND_U, TIE_ROUND_UHAT, TIE_ROUND_SEED, TIE_COLLIDE, TIE_STOP, TIE_DIST = range(6)
+
+
+def round_margins(x, decimals):
+    """Signed distance of each x to the nearest rounding boundary (k + 1/2) 10^-d of np.around
+    (casadi/main.py:48-49,103,153), computed as the kernels do: (x 10^d - (floor(x 10^d) + 1/2)) / 10^d."""
+    f = 10.0 ** decimals
+    y = np.asarray(x, np.float64) * f
+    return (y - (np.floor(y) + 0.5)) / f
+
+
+class TieLog:
+    """Near-tie log of the oracle: the mirror of piadmm_get_near_ties (same kinds, ids, margins)."""
+
+    def __init__(self, tol=1e-9):
+        self.tol = float(tol)
+        self.events = []          # (step, iter, kind, id, index, margin)
+
+    def rounding(self, t, it, kind, ident, x, decimals, idx0=0):
+        if decimals < 0:
+            return
+        m = round_margins(x, decimals)
+        for k in np.nonzero(np.abs(m) * 10.0 ** decimals <= self.tol * 10.0 ** decimals)[0]:
+            self.events.append((t, it, kind, ident, idx0 + int(k), float(m[k])))
+
+    def collide(self, t, it, e, d2, thr):
+        lo = np.any(d2 < thr * (1.0 - self.tol))
+        near = np.any(d2 <= thr * (1.0 + self.tol))
+        if not lo and near:
+            k = int(np.argmin(d2))
+            self.events.append((t, it, TIE_COLLIDE, e, k, float((d2[k] - thr) / thr)))
+
+    def scalar(self, t, it, kind, ident, idx, v, thr):
+        if abs(v - thr) <= self.tol * abs(thr):
+            self.events.append((t, it, kind, ident, idx, float((v - thr) / thr)))
+
+
 # ----------------------------------------------------------------------------- state
 @dataclasses.dataclass
 class StepRecord:
@@ -327,6 +366,7 @@ class Oracle:
         # global PI: the pair's adaptive penalty, kept across MPC steps like PI_ADMM.param.rho
         # (casadi_old_PI_ADMM/main.py:139 is never reset)
         self.rho_pi = np.full(self.E, float(cfg.rho))
+        self.ties = TieLog()        # near ties of the discrete decisions (piadmm_get_near_ties)
 
     def seeds(self):
         """``casadi/main.py:48-49``."""
@@ -362,6 +402,10 @@ class Oracle:
         cnt = (lambda e: True) if self.counted is None else (lambda e: bool(self.counted[e]))
         t = self.t
         seeds = self.seeds()
+        for i in range(N):
+            raw = (self.xt[i, 0] + cfg.dt * self.scn.spd[i] * np.cos(self.xt[i, 2]),
+                   self.xt[i, 1] + cfg.dt * self.scn.spd[i] * np.sin(self.xt[i, 2]))
+            self.ties.rounding(t, -1, TIE_ROUND_SEED, i, np.array(raw), cfg.round_decimals)
         pos_old = np.zeros((N, 2, H + 1))
         if cfg.warm_duals and self.edge_state is not None:
             # a12: the previous step's duals, edge positions and PI accumulators, shifted
@@ -401,6 +445,7 @@ class Oracle:
                     u_star, _ = solve_xstep(cfg, self.xt[i], self.scn.spd[i],
                                             self.scn.ref[i, :, t:t + H + 1], terms)
                     u = around(u_star, cfg.round_decimals)
+                    self.ties.rounding(t, it, TIE_ROUND_U, int(i), u_star, cfg.round_decimals)
                     roll = rollout_linear if cfg.pos_model == 0 else rollout_nonlinear
                     px, py, _ = roll(self.xt[i], u, self.scn.spd[i], cfg.dt, cfg.L)
                     pos_old[i, 0], pos_old[i, 1] = px, py
@@ -411,6 +456,9 @@ class Oracle:
                 for e in edges:
                     v1, v2 = self.scn.edges[e]
                     active[e] = True if cfg.no_collision_gate else collides(cfg, pos_old[v1], pos_old[v2], d_eff[e])
+                    if not cfg.no_collision_gate:
+                        d2 = np.square(pos_old[v1][0] - pos_old[v2][0]) + np.square(pos_old[v1][1] - pos_old[v2][1])
+                        self.ties.collide(t, it, int(e), d2, cfg.collide_thr(d_eff[e]))
                 act = [e for e in edges if active[e]]
                 # ---- z-step + dual update, casadi/main.py:121-162 (none when no pair is active)
                 for e in act:
@@ -418,6 +466,8 @@ class Oracle:
                     uh, _ = solve_edge(cfg, self.xt[v1], self.scn.spd[v1], self.xt[v2], self.scn.spd[v2],
                                        pos_old[v1], pos_old[v2], lam[e, 0], lam[e, 1], seeds[v1], seeds[v2],
                                        d_eff[e], self.rho_pi[e] if gpi else None)
+                    for d in range(2):
+                        self.ties.rounding(t, it, TIE_ROUND_UHAT, int(e), uh[d], cfg.round_decimals, idx0=d * H)
                     uh = around(uh, cfg.round_decimals)
                     for d, v in enumerate((v1, v2)):
                         hx, hy, _ = rollout_nonlinear(self.xt[v], uh[d], self.scn.spd[v], cfg.dt, cfg.L)
@@ -425,11 +475,15 @@ class Oracle:
                     if gpi:
                         dis_chk[e] = dual_update_global_pi(cfg, self.xt, self.scn.spd, self.primal_u, v1, v2,
                                                            pos_old, hat[e], lam[e], S[e], D[e], self.rho_pi, e)
+                        if cfg.term_dist_check:
+                            self.ties.scalar(t, it, TIE_DIST, int(e), 0, dis_chk[e], d_eff[e])
                         continue
                     dvec = pos_old[v1] - pos_old[v2]
                     dist = np.sqrt(np.sum(dvec * dvec, axis=0))
                     dual_update(cfg, pos_old[v1], pos_old[v2], hat[e], lam[e], S[e], D[e], dist)
                     dis_chk[e] = dist[1]
+                    if cfg.term_dist_check:
+                        self.ties.scalar(t, it, TIE_DIST, int(e), 0, dis_chk[e], d_eff[e])
                 # ---- residuals, casadi/main.py:164-178 (per component; summed over the group)
                 comp_r = []
                 for c in gcomps:
@@ -463,6 +517,10 @@ class Oracle:
                 if cfg.term_global:
                     global_resid.append((rk_g, sk_g))
                 dist_ok = n_seen > 0 and n_bad == 0
+                if not cfg.fixed_iters:
+                    gid = -1 if cfg.term_global else int(gcomps[0])
+                    self.ties.scalar(t, it, TIE_STOP, gid, 0, rk_g, cfg.eps_pri)
+                    self.ties.scalar(t, it, TIE_STOP, gid, 1, sk_g, cfg.eps_dual)
                 if (not cfg.fixed_iters and rk_g <= cfg.eps_pri and sk_g <= cfg.eps_dual
                         and (not cfg.term_dist_check or dist_ok)):
                     g_done[g] = True

@@ -23,7 +23,7 @@ def test_library_is_built_for_gfx950():
     lib = _lib.load()
     info = lib.piadmm_build_info().decode()
     assert "gfx950" in info
-    assert lib.piadmm_abi_version() == 5
+    assert lib.piadmm_abi_version() == 6
 
 
 def test_exports_every_declared_symbol():
@@ -63,6 +63,15 @@ def test_create_fails_loudly_without_device():
     from piadmm.solver import PI_ADMM_MI355X
     with pytest.raises(_lib.PiadmmError):
         PI_ADMM_MI355X(config.casadi_default(H=10), scenario.intersection(10))
+
+
+def test_near_tie_record_layout_matches_header():
+    """piadmm_near_tie_t = 6 int32 + one double (32 bytes); kinds and capacity as in the header."""
+    src = open(HEADER).read()
+    assert _lib.TIE_DTYPE.itemsize == 32
+    for k, name in enumerate(_lib.TIE_KINDS):
+        assert re.search(rf"#define PIADMM_TIE_{name.upper()} {k}\b", src), name
+    assert re.search(rf"#define PIADMM_TIE_CAP {_lib.TIE_CAP}\b", src)
 
 
 def test_header_enums_match_python():

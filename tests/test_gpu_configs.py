@@ -129,30 +129,52 @@ def test_gpu_equals_bopt_cpu_baseline_at_full_size(Solver, preset, H, tiles, n_s
             close(rg.xt, rc["xt"][k])
 
 
-@pytest.mark.parametrize("kw,n_steps", [({"fixed_iters": 1, "term_global": 1}, 3), ({"term_global": 1}, 5)])
+def _dev(u1, x1, u2, x2):
+    return max(float(np.max(np.abs(u1 - u2))), float(np.max(np.abs(x1 - x2) / (1.0 + np.abs(x2)))))
+
+
+@pytest.mark.parametrize("kw,n_steps", [({"fixed_iters": 1, "term_global": 1}, 6), ({"term_global": 1}, 20)])
 def test_gpu_equals_bopt_on_the_crossing_workload(Solver, kw, n_steps):
     """bench.py --crossing at its full size (64 four-vehicle all-pairs crossings, 256 agents, 384
-    candidate pairs, H30, matlab_pi, the reference's global scope) on the graph kernel equals the
-    B-opt CPU baseline on the same job (1e-8): the crossing's cpu_baseline times this exact work."""
+    candidate pairs, H30, matlab_pi, the reference's global scope) on the graph kernel against the
+    B-opt CPU baseline (the crossing's cpu_baseline), over every bench step.
+
+    (1) Step by step from common inputs: B-opt runs step k from the GPU's state at step k; every
+        step's outer-iteration count equals, its controls and next state agree within the 1e-5
+        contract (held 1e-6) -- the MPC step map is the same on both sides, all 20 steps.
+    (2) Free running: this coupled job never converges (100 PI iterations per step from step 3 on)
+        and amplifies any perturbation ~1e4x per step: B-opt against ITSELF started from xt0 (1 +
+        1e-12) parts at step 6 (profiles/crossing_sensitivity_r04.json), with no decision near a
+        threshold (the near-tie logs are empty at 1e-9).  The GPU's free-running deviation from
+        B-opt stays inside that envelope at every step before the parting: the GPU is closer to
+        B-opt than B-opt is to itself under a 1e-12 perturbation of the initial state."""
     from oracle import cpu_bopt
+    from piadmm.scenario import Scenario
     H = 30
     cfg = config.matlab_pi(H=H, **kw)
     scn = scenario.concat([scenario.crossing(4, H, n_steps=n_steps + 2, seed=k) for k in range(64)])
-    rc = cpu_bopt.run(cfg, scn, n_steps, threads=4)
-    assert rc["counters"]["inexact"] == 0 and rc["counters"]["z_qps"] > 0
-    dev = []
+    ref = cpu_bopt.run(cfg, scn, n_steps, threads=8)
+    assert ref["counters"]["inexact"] == 0 and ref["counters"]["z_qps"] > 0
+    pert = cpu_bopt.run(cfg, Scenario(spd=scn.spd, xt0=scn.xt0 * (1.0 + 1e-12), ref=scn.ref, edges=scn.edges,
+                                      n_steps=scn.n_steps), n_steps, threads=8)
+    resync, free, env = [], [], []
     with Solver(cfg, scn) as s:
+        xt_prev = scn.xt0.copy()
         for k in range(n_steps):
             rg = s.mpc_step()
             assert np.all(rg.status == 0)
-            np.testing.assert_array_equal(rg.iters, rc["iters"][k])
-            dev.append(max(float(np.max(np.abs(rg.u - rc["u"][k]))),
-                           float(np.max(np.abs(rg.xt - rc["xt"][k]) / (1.0 + np.abs(rc["xt"][k]))))))
-    # The first steps agree to 1e-8.  Under natural termination this job runs 100 coupled outer
-    # iterations per step from step 3 on (the global stop never fires): rounding-level differences of
-    # two exact solvers (summation orders) are carried through 100 PI dual updates per step and grow
-    # step by step -- held to 1e-6 here, 10x inside the 1e-5 contract.  Further on (r03 run: step 6)
-    # a borderline discrete event (a collision test d^2 < thr, a round-to-1e-4 boundary) resolves
-    # differently on the two sides and the trajectories part: the comparison stops at step 5.
-    assert max(dev[:3]) <= 1e-8, dev
-    assert max(dev) <= 1e-6, dev
+            one = cpu_bopt.run(cfg, Scenario(spd=scn.spd, xt0=xt_prev, ref=scn.ref, edges=scn.edges,
+                                             n_steps=scn.n_steps), 1, threads=8, t0=k)
+            assert one["counters"]["inexact"] == 0
+            np.testing.assert_array_equal(rg.iters, one["iters"][0], err_msg=f"step {k}")
+            resync.append(_dev(rg.u, rg.xt, one["u"][0], one["xt"][0]))
+            free.append(_dev(rg.u, rg.xt, ref["u"][k], ref["xt"][k]))
+            env.append(_dev(pert["u"][k], pert["xt"][k], ref["u"][k], ref["xt"][k]))
+            xt_prev = rg.xt.copy()
+        counts, events = s.near_ties()
+    assert max(resync) <= 1e-6, resync
+    part = next((k for k in range(n_steps) if env[k] > 1e-3), n_steps)
+    for k in range(part):
+        assert free[k] <= max(env[k], 1e-9), (k, free[:part], env[:part])
+    print(f"crossing {kw}: resync max {max(resync):.2e}, free {['%.1e' % v for v in free]}, "
+          f"envelope {['%.1e' % v for v in env]}, near ties {counts}")

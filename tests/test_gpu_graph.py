@@ -186,34 +186,65 @@ def test_global_pi_on_a_crossing(Solver):
 def test_component_split_over_workgroups(Solver, monkeypatch, fixed):
     """A connected component larger than the workgroup block (term_global) spans several
     workgroups: blocks of 4 agents, a pair owned by the block of its first agent, the X and Z
-    phases as separate launches.  A 24-vehicle chain (one component) equals the same job on one
-    workgroup (PIADMM_GRAPH_BLOCK=0) to 1e-10 and the oracle to 1e-8 -- steps with 1 to 23 outer
-    iterations, natural and fixed termination."""
+    phases as separate launches.  The job's residual sums run over the whole component in pair
+    order (k_graph_partials, casadi/main.py:165-173), so a 24-vehicle chain (one component) equals
+    the same job on one workgroup (PIADMM_GRAPH_BLOCK=0) to 1e-10 -- stop decisions included -- over
+    all 24 steps (1 to 23 outer iterations, natural and fixed termination), and the oracle to 1e-8
+    up to the first step with a logged near tie (none at the default 1e-9 here: all 24 steps)."""
     H = 12
     cfg = config.matlab_pi(H=H, term_global=1, fixed_iters=fixed, max_outer=30 if fixed else 100)
-    scn = scenario.crossing(24, H, n_steps=24, seed=1, pairs="chain")
+    scn = scenario.crossing(24, H, n_steps=26, seed=1, pairs="chain")
     s1 = Solver(cfg, scn)
     monkeypatch.setenv("PIADMM_GRAPH_BLOCK", "0")
     s2 = Solver(cfg, scn)
     monkeypatch.delenv("PIADMM_GRAPH_BLOCK")
     orc = O.Oracle(cfg, scn)
+    tied = None                          # first step with a near tie (GPU or oracle)
     try:
         assert s1.C == 6 and s2.C == 1 and s1.steps_per_launch() == 1
-        # (beyond step 12 the job's stop test becomes borderline -- rk within rounding of eps --
-        # and the blocks' summation order of the residual partials may resolve it differently)
-        for k in range(12):
-            r1, r2, ro = s1.mpc_step(), s2.mpc_step(), orc.mpc_step()
+        for k in range(24):
+            r1, r2 = s1.mpc_step(), s2.mpc_step()
             assert np.all(r1.status == 0)
-            assert r1.global_iters == r2.global_iters == int(ro.iters[0])
+            assert r1.global_iters == r2.global_iters
             np.testing.assert_allclose(r1.xt, r2.xt, rtol=1e-10, atol=1e-10, err_msg=f"step {k}")
             np.testing.assert_allclose(r1.u, r2.u, rtol=1e-10, atol=1e-10, err_msg=f"step {k}")
             n = r1.global_iters
-            np.testing.assert_allclose(r1.global_resid[:n], r2.global_resid[:n], rtol=1e-9, atol=1e-12)
-            close(r1.xt, ro.xt)
-            close(r1.u, ro.u)
+            np.testing.assert_array_equal(r1.global_resid[:n], r2.global_resid[:n])   # bit-identical sums
+            if tied is None:
+                ro = orc.mpc_step()
+                if s1.near_ties()[1].size or orc.ties.events:
+                    tied = k
+                    continue
+                assert r1.global_iters == int(ro.iters[0]), f"step {k}"
+                close(r1.xt, ro.xt)
+                close(r1.u, ro.u)
+        assert tied is None, f"near tie at step {tied}: {s1.near_ties()}, {orc.ties.events[:3]}"
     finally:
         s1.close()
         s2.close()
+
+
+def test_split_component_host_stepping(Solver):
+    """Host stepping (piadmm_outer_iter, ABI 5) of a component split over workgroups: the step-init
+    launch, then per iteration the X and Z launches and the pair-order partials; equal to
+    mpc_step of the same job, iteration counts and residual histories included."""
+    H = 12
+    cfg = config.matlab_pi(H=H, term_global=1)
+    scn = scenario.crossing(12, H, n_steps=8, seed=2, pairs="chain")
+    with Solver(cfg, scn) as s1, Solver(cfg, scn) as s2:
+        assert s1.C > 1
+        for k in range(5):
+            r1 = s1.mpc_step()
+            it = 0
+            while True:
+                stop = s2.outer_iter(it)
+                it += 1
+                if stop or it == cfg.max_outer:
+                    break
+            xt, u = s2.step_finish()
+            assert it == r1.global_iters, (k, it, r1.global_iters)
+            np.testing.assert_array_equal(xt, r1.xt)
+            np.testing.assert_array_equal(u, r1.u)
 
 
 def test_large_connected_graph_split(Solver, monkeypatch):

@@ -65,3 +65,22 @@ def test_cli_run_matches_oracle(tmp_path):
     np.testing.assert_allclose(got.x_vec, want.x_vec, rtol=1e-8, atol=1e-8)
     np.testing.assert_array_equal(got.iter_his, want.iter_his)
     assert os.path.getsize(out + ".png") > 1000
+
+
+def test_checkpoint_round_trip(tmp_path):
+    """save_checkpoint / load_checkpoint: xt, the carried pair state and the
+    next time index through an .npz written and read without pickles; a checkpoint of another
+    configuration is refused."""
+    cfg = config.matlab_pi(H=8, warm_duals=1)
+    orc = O.Oracle(cfg, scenario.intersection(8, n_steps=6))
+    for _ in range(3):
+        orc.mpc_step()
+    hat, lam, S, D, last = orc.edge_state
+    st = dict(xt=orc.xt, hat=hat, lam=lam, S=S, D=D, last_hat=last, rho_pi=orc.rho_pi, t=orc.t)
+    path = io.save_checkpoint(str(tmp_path / "c"), st, cfg)
+    back = io.load_checkpoint(path, cfg)
+    assert back["t"] == 3
+    for k in io.CHECKPOINT_KEYS:
+        np.testing.assert_array_equal(back[k], np.asarray(st[k]))
+    with pytest.raises(ValueError):
+        io.load_checkpoint(path, cfg.replace(H=9))
