@@ -181,8 +181,11 @@ def cpu_baseline(wl: dict, budget_s: float, K: int) -> dict:
     return bopt
 
 
-def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_rank: int, dist, split="components"):
-    """Time K MPC steps of workload wl on this rank; returns (metrics, counters, solver info)."""
+def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_rank: int, dist, split="components",
+        share: int = 0):
+    """Time K MPC steps of workload wl on this rank; returns (metrics, counters, solver info).
+    share > 1 (strong scaling, one process): rank 0's share of a share-rank job alone on this GPU --
+    its agents (and, interleaved, its ghosts), every collective a no-op (SURVEY.md 8e readiness)."""
     from piadmm import config, scenario
     from piadmm import dist as pdist
     from piadmm.solver import PI_ADMM_MI355X
@@ -193,11 +196,12 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
     shard = None
     if wl["scaling"] == "strong":
         full = scenario.tiled(wl["tiles"], H, n_steps=n_steps, perturb=True, seed=0)
+        srank, sworld = (0, share) if share > 1 else (rank, world)
         if split == "interleaved":
-            shard = pdist.shard_graph(full, rank, world, pdist.owners_interleaved(full.n_agents, world))
+            shard = pdist.shard_graph(full, srank, sworld, pdist.owners_interleaved(full.n_agents, sworld))
             scn = shard.scn
         else:
-            scn = pdist.shard(full, rank, world)
+            scn = pdist.shard(full, srank, sworld)
     else:
         scn = make_scenario(wl, n_steps, rank)
     from piadmm.solver import device_count
@@ -407,6 +411,10 @@ def main():
     ap.add_argument("--obca-batch", type=int, default=4096, help="--obca: local problems per GPU")
     ap.add_argument("--split", choices=("components", "interleaved"), default="components",
                     help="--strong: whole tiles per rank, or every tile across two ranks (boundary exchange)")
+    ap.add_argument("--share", type=int, default=0,
+                    help="--strong on one GPU: time rank 0's share of a SHARE-rank job alone, collectives as "
+                         "no-ops (interleaved: the exchange is a device copy, ghosts read zeros) -- the "
+                         "per-rank compute of the strong-scaling model, DESIGN.md section 7")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "0"))
@@ -438,12 +446,19 @@ def main():
 
     H, M = wl["H"], wl["max_outer"]
     K, W = args.steps, args.warmup
-    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist, args.split)
+    if args.share and (not args.strong or world != 1):
+        raise SystemExit("bench.py: --share needs --strong on one GPU")
+    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist, args.split, args.share)
 
     # value = units all ranks processed / the max-over-ranks wall time.  Weak scaling: one unit =
     # one outer iteration of a rank's (256-agent) block, so all ranks processed world x job
     # iterations; strong scaling: the unit is an outer iteration of the whole 1024-agent job.
     units = m["job_iters"] * (world if wl["scaling"] == "weak" else 1)
+    if args.share:
+        # one rank's share alone: its iterations are the job's (every rank runs them), but only
+        # 1/share of the job's agents -- the rate is the share's, not a scaling claim
+        wl = dict(wl, desc=wl["desc"] + f"; rank 0's SHARE of a {args.share}-rank job alone on one GPU "
+                                        f"({args.split}), collectives as no-ops")
     value = units / m["wall"]
     agents_job = m["N"] * world if wl["scaling"] == "weak" else 2 * wl["tiles"]
     avg_launch_s = (m["ev_ms"] / 1e3) / m["n_launch"]
@@ -540,7 +555,7 @@ def main():
     line["latency"] = lat
 
     if not args.natural and not args.no_natural:
-        mn, cn = run(wl, True, K, W, rank, world, local_rank, dist, args.split)
+        mn, cn = run(wl, True, K, W, rank, world, local_rank, dist, args.split, args.share)
         line["natural"] = {
             "ms_per_step": mn["wall"] / K * 1e3,
             "outer_iters_per_step": mn["job_iters"] / K,

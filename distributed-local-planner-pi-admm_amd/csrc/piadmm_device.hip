@@ -41,8 +41,10 @@ struct StepCtx {
   double* vec_all;
   WaveMem wm;
   bool spec;        // the speculative loop shape (agent_part)
+  bool roll;        // speculative loop with the roller wave (roll_part): agent 1's rollout on wave RW
   int* vd;          // the pair wave's verdict on an iteration (speculative loop): act, stop, flag, aliased
   double* vdd;      // and dis_chk
+  int* rflag;       // the roller's progress: it + 1 once agent 1's positions of iteration it are in LDS
 };
 
 // The outer loop's control state.  Every wave keeps its own copy and updates it from the same
@@ -601,7 +603,23 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     unsigned long long t_sa = STAMP_T();
     __syncthreads();                                     // A: every agent's positions / controls
     STAMP_ADD(ST_SYNC_A, t_sa);
-    if (specm) {
+    if (specm && X.roll) {
+      // pos_old = dynamic_update_local of the rounded controls (casadi/main.py:105): agent 0's here,
+      // agent 1's on the roller wave at the same time (roll_part); then wait for the roller's flag
+      const bool nonlin_pos = c.pos_model != 0;
+      double px, py, pth;
+      const double u = (l < H) ? S.u[(it & 1) * 2 * H + l] : 0.0;
+      rollout_r(S.xt[0], S.xt[1], S.xt[2], ra_s[0], ra_s[0] / c.L, u, c, H, nonlin_pos, px, py, pth);
+      if (l <= H) {
+        pos[0 * H1 + l] = px;
+        pos[1 * H1 + l] = py;
+      }
+      unsigned long long t_rw = STAMP_T();
+      while (__hip_atomic_load(X.rflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != it + 1)
+        __builtin_amdgcn_s_sleep(1);
+      STAMP_ADD(ST_XROLL, t_rw);
+      wsync();
+    } else if (specm) {
       // pos_old = dynamic_update_local of the rounded controls (casadi/main.py:105), per agent
       // both agents' rollouts side by side (two independent DPP-scan / sincos chains in one block,
       // so their latencies overlap; a single-agent component's second one is discarded)
@@ -800,6 +818,40 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
   }
 }
 
+// -------------------------------------------------------------------- the roller wave (RW)
+// Speculative loop only: agent 1's rollout of each iteration's rounded controls (pos_old =
+// dynamic_update_local, casadi/main.py:105), concurrent with the pair wave's rollout of agent 0, so
+// the pair wave's chain before the verdict (two rollouts, the collision test) -- which the agent
+// waves wait for at barrier B -- holds one rollout, not two.  It takes the same barriers (A, B) and
+// stops with the pair wave's verdict.
+__device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
+  const piadmm_config_t& c = A.cfg;
+  const int H = X.H, H1 = X.H1, l = X.l;
+  const CompLds& S = X.S;
+  const bool has = X.na == 2;
+  const double s = has ? A.spd[X.a0 + 1] : 0.0;
+  const double x0 = has ? S.xt[3] : 0.0, y0 = has ? S.xt[4] : 0.0, th0 = has ? S.xt[5] : 0.0;
+  const bool nonlin_pos = c.pos_model != 0;
+  __syncthreads();                                       // the parts' setup barrier
+  for (int it = X.it0; it < X.it_end; ++it) {
+    double* const pos = S.pos + (it & 1) * 4 * H1;
+    __syncthreads();                                     // A: the agents' controls of iteration it
+    if (has) {
+      double px, py, pth;
+      const double u = (l < H) ? S.u[(it & 1) * 2 * H + H + l] : 0.0;
+      rollout_r(x0, y0, th0, s, s / c.L, u, c, H, nonlin_pos, px, py, pth);
+      if (l <= H) {
+        pos[2 * H1 + l] = px;
+        pos[3 * H1 + l] = py;
+      }
+    }
+    // (release: the wave's position stores complete before the flag)
+    if (l == 0) __hip_atomic_store(X.rflag, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();                                     // B: the pair wave's verdict
+    if (X.vd[1]) break;
+  }
+}
+
 // One launch runs outer iterations [it0, it1) of MPC step t for every component (one
 // workgroup each).  The fused mode is one launch (0, max_outer, FIRST | LAST); the global
 // termination mode (term_global, reference quirk B9) runs one launch per outer iteration,
@@ -815,10 +867,13 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   __shared__ int s_int[NWT * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
   __shared__ int s_vd[4];
   __shared__ double s_vdd;
+  __shared__ int s_rflag;
   const piadmm_config_t& c = A.cfg;
   StepCtx X;
   X.vd = s_vd;
   X.vdd = &s_vdd;
+  X.rflag = &s_rflag;
+  if (threadIdx.x == 0) s_rflag = 0;   // (iterations count from it0 >= 0: the flag waits for it + 1)
   X.H = c.H;
   X.H1 = c.H + 1;
   X.ci = blockIdx.x;
@@ -866,6 +921,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   // step; the linearised model's cheap rollout does not pay for the second barrier
   // (casadi_default 64 x H20 0.633 -> 0.677 ms)
   X.spec = !X.coop && c.pos_model != 0;
+  X.roll = X.spec && blockDim.x == NWA * WAVE;   // launch_mpc_step adds the roller wave to this shape
   X.it0 = it0;
   const bool first = X.first;
   // a component whose step already ended in an earlier launch of this step (per-component stop,
@@ -939,7 +995,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   L.dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
   WaveCnt n;
   if (X.w < NW) agent_part<BIG>(A, X, L, nbar, n);
-  else pair_part<BIG>(A, X, L, nbar, n);
+  else if (X.w == PW) pair_part<BIG>(A, X, L, nbar, n);
+  else roll_part(A, X);
   __syncthreads();
   STAMP_ADD(ST_KERNEL, t_k);
   unsigned long long t_epi = STAMP_T();
@@ -947,7 +1004,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   // ---- work counters (accumulated across launches; one workgroup owns row ci) and the
   // component's state of this launch (every launch)
   {
-    __shared__ int s_cnt[NWT][8];
+    __shared__ int s_cnt[NWA][8];
     __shared__ int s_warm;
     if (threadIdx.x == 0) s_warm = 0;
     if (X.l == 0) {
@@ -960,13 +1017,14 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     if (threadIdx.x == 0) {
       unsigned long long* cn = A.counters + (size_t)ci * 8;
       cn[0] += (unsigned long long)(X.skip ? 0 : L.iters - it0);
+      const int nw = (int)(blockDim.x / WAVE);
       for (int k = 0; k < 6; ++k) {
         unsigned long long sum = 0;
-        for (int ww = 0; ww < NWT; ++ww) sum += (unsigned long long)s_cnt[ww][k];
+        for (int ww = 0; ww < nw; ++ww) sum += (unsigned long long)s_cnt[ww][k];
         cn[k + 1] += sum;
       }
       unsigned long long inex = 0;
-      for (int ww = 0; ww < NWT; ++ww) inex += (unsigned long long)s_cnt[ww][6];
+      for (int ww = 0; ww < nw; ++ww) inex += (unsigned long long)s_cnt[ww][6];
       cn[7] += inex;
       A.iters[ci] = L.iters;
       if (e >= 0) {
@@ -1001,7 +1059,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 // sum_t max_c.  The step-to-step state (xt, labels, caches) goes through HBM inside one
 // workgroup (same CU: the barrier's workgroup-scope fences order it).
 template <bool BIG>
-__global__ void __launch_bounds__(NWT * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
+__global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
 #ifdef PIADMM_STAMPS
   if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
   __syncthreads();
@@ -1121,10 +1179,17 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NWT * WAVE), args, (unsigned)sh, s));
   }
   (void)hipGetLastError();   // a stale error of an earlier runtime call is not this launch's
+  // the speculative loop (no grid barrier, the nonlinear position model: mpc_step_body) runs with
+  // the roller wave; PIADMM_NO_ROLLER=1 keeps three waves (the pair wave rolls both agents out)
+  static const bool no_roller = [] {
+    const char* e = std::getenv("PIADMM_NO_ROLLER");
+    return e && e[0] == '1';
+  }();
+  const int nt = (a.cfg.pos_model != 0 && !no_roller ? NWA : NWT) * WAVE;
   if (big)
-    hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(NWT * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
+    hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(nt), sh, s, a, t, nsteps, it0, it1, flags);
   else
-    hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(NWT * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
+    hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(nt), sh, s, a, t, nsteps, it0, it1, flags);
   return launch_rc(hipGetLastError());
 }
 

@@ -16,7 +16,10 @@ inline int launch_rc(hipError_t e) {
 constexpr int WAVE = 64;
 constexpr int NW = 2;        // agent waves per workgroup of k_mpc_step = agents per component (max)
 constexpr int PW = NW;       // the pair's wave (k_mpc_step): its own loop, registers and LDS vectors
-constexpr int NWT = NW + 1;  // waves per workgroup of k_mpc_step
+constexpr int NWT = NW + 1;  // waves per workgroup of k_mpc_step that solve QPs
+constexpr int RW = NW + 1;   // speculative loop only: the roller wave -- agent 1's per-iteration rollout,
+                             // concurrent with the pair wave's rollout of agent 0
+constexpr int NWA = NW + 2;  // waves per workgroup of k_mpc_step in the speculative loop
 constexpr int HCAP = 64;     // storage stride of per-lane state: lane k <-> time index k, H <= 63
 constexpr int HMAX = 32;     // largest H of the all-in-LDS layout ("LDS mode")
 constexpr int HBIG = 63;     // largest H supported (matrices in HBM / L2 beyond HMAX: "big mode")
@@ -145,7 +148,7 @@ struct DevArgs {
 // a degenerate vertex can hold one or two dependent rows beyond the H variables).
 constexpr int xrows(int H) { return H + 2 < 64 ? H + 2 : 64; }
 // LDS the kernel declares statically (s_int, s_cnt, s_warm) on top of lds_bytes().
-constexpr size_t STATIC_LDS = NWT * 272 * 4 + NWT * 8 * 4 + 16 + 4 * 4 + 8;
+constexpr size_t STATIC_LDS = NWT * 272 * 4 + NWA * 8 * 4 + 16 + 4 * 4 + 8 + 8;
 constexpr size_t MAX_LDS = 160 * 1024;
 
 // fp32 agent K_s^-1 images in LDS mode: per wave H*H floats rounded up to an even count, so
