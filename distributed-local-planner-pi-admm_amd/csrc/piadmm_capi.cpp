@@ -838,6 +838,9 @@ static int32_t run_steps_phases(piadmm_handle_t h, int32_t t, int32_t n, bool sy
       nit = it + 1;
       if (c.fixed_iters) {
         if (int rc = iteration_launches(h, tk, it, 0)) return rc;
+        // the iteration's (rk, sk): a split component's sums in the reference's pair order
+        // (k_graph_partials), a sharded graph's the blocks' partials -- the history of the step
+        if (h->split) LAUNCH(h, pd::launch_graph_partials(h->a, h->d_part + (size_t)k * 2 * M + 2 * it, s, 0, 2));
         continue;
       }
       int stop = 0;
@@ -846,7 +849,7 @@ static int32_t run_steps_phases(piadmm_handle_t h, int32_t t, int32_t n, bool sy
     }
     h->giters = nit;
     LAUNCH(h, launch_step(h->a, tk, 1, nit, nit, pd::F_LAST | pd::F_GLOBAL | (nanlast ? pd::F_NANLAST : 0), s));
-    if (c.fixed_iters) LAUNCH(h, pd::launch_resid_history(h->a, 1, h->d_part + (size_t)k * 2 * M, s));
+    if (c.fixed_iters && !h->split) LAUNCH(h, pd::launch_resid_history(h->a, 1, h->d_part + (size_t)k * 2 * M, s));
   }
   if (c.fixed_iters) {
     if (int rc = allreduce(h, h->d_part, h->d_part, (size_t)n * 2 * M)) return rc;

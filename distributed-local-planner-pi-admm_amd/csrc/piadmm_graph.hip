@@ -876,7 +876,7 @@ namespace pd {
 // in order (casadi/main.py:165-173; the oracle's comp_r sum) -- from the pairs' terms the blocks'
 // T phases wrote (A.eterm), wave 0 summing rk and wave 1 sk: bit-identical to the same job on one
 // workgroup per component.  (The counts -- active pairs, distance checks -- are integers: any order.)
-__global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double* out, int devstop) {
+__global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double* out, int devstop, int nout) {
   if (devstop && A.gctl[0]) return;
   constexpr int NT = GW * WAVE;
   __shared__ double red[5][NT];
@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double*
   for (int q = 0; q < 5; ++q) red[q][threadIdx.x] = v[q];
   __syncthreads();
   const bool split = A.sum_C > 0;
-  if (threadIdx.x < 5 && !(split && threadIdx.x < 2)) {
+  if ((int)threadIdx.x < nout && !(split && threadIdx.x < 2)) {
     double tot = 0.0;
     for (int k = 0; k < NT; ++k) tot += red[threadIdx.x][k];
     out[threadIdx.x] = tot;
@@ -948,9 +948,9 @@ bool graph_coop_fits(const DevArgs& a, int device) {
   return (long long)per * ncu >= (long long)a.C;
 }
 
-int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s, int devstop) {
+int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s, int devstop, int nout) {
   (void)hipGetLastError();
-  hipLaunchKernelGGL(k_graph_partials, dim3(1), dim3(GW * WAVE), 0, s, a, out, devstop);
+  hipLaunchKernelGGL(k_graph_partials, dim3(1), dim3(GW * WAVE), 0, s, a, out, devstop, nout);
   return launch_rc(hipGetLastError());
 }
 

@@ -227,7 +227,7 @@ constexpr int DETECT_SCAN_B = 1024;   // ints per workgroup of the detection's s
 int launch_detect_emit(const double* xs, const double* rs, int n, double inv_cs, unsigned T, const int* start,
                        const int* order, const int* off, int* out, hipStream_t s);
 bool graph_coop_fits(const DevArgs& a, int device);
-int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s, int devstop = 0);
+int launch_graph_partials(const DevArgs& a, double* out, hipStream_t s, int devstop = 0, int nout = 5);
 int launch_decide(const DevArgs& a, int t, int it, const double* part, hipStream_t s);
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s, int devstop = 0);

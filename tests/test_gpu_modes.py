@@ -176,30 +176,31 @@ def test_device_decided_termination_equals_host_decision(Solver, monkeypatch, ki
 @pytest.mark.parametrize("kind", ["fused_warm_duals", "graph_warm_duals", "global_pi"])
 def test_checkpoint_resume_equals_uninterrupted_run(Solver, tmp_path, kind):
     """piadmm_get_step_state / piadmm_set_state + piadmm.io checkpoints: a run
-    checkpointed after step 5 (xt and the carried pair state: warm_duals' hat / lam / S / D /
-    last_hat, the global-PI pair penalties, casadi_old_PI_ADMM/main.py:139) and resumed in a NEW
-    handle equals the uninterrupted run over the remaining steps (to rounding: the QP solvers' warm
-    starts are not part of the checkpoint, every answer is the certified minimiser)."""
+    checkpointed mid-run (after the first collisions: xt and the carried pair state -- warm_duals'
+    hat / lam / S / D / last_hat, the global-PI pair penalties, casadi_old_PI_ADMM/main.py:139) and
+    resumed in a NEW handle equals the uninterrupted run over the remaining steps (to rounding: the
+    QP solvers' warm starts are not part of the checkpoint, every answer is the certified minimiser)."""
     from piadmm import io
     if kind == "fused_warm_duals":
-        cfg, scn = config.matlab_pi(H=15, warm_duals=1), scenario.tiled(4, 15, n_steps=14, seed=2)
+        cfg, scn, k1, k2 = config.matlab_pi(H=15, warm_duals=1), scenario.tiled(4, 15, n_steps=16, seed=2), 9, 14
     elif kind == "graph_warm_duals":
-        cfg, scn = config.matlab_pi(H=15, warm_duals=1), scenario.crossing(4, 15, n_steps=14, seed=4)
+        cfg, scn, k1, k2 = config.matlab_pi(H=15, warm_duals=1), scenario.crossing(4, 15, n_steps=14, seed=4), 7, 12
     else:
-        cfg, scn = config.casadi_old_pi(H=8, fixed_iters=1, max_outer=10), scenario.intersection(8, n_steps=14)
+        cfg, scn, k1, k2 = (config.casadi_old_pi(H=8, fixed_iters=1, max_outer=10), scenario.intersection(8, n_steps=22),
+                            17, 20)
     with Solver(cfg, scn) as a:
-        full = [a.mpc_step() for _ in range(5)]
+        full = [a.mpc_step() for _ in range(k1)]
         path = io.save_checkpoint(str(tmp_path / "ckpt"), a.step_state(), cfg)
-        full += [a.mpc_step() for _ in range(5)]
+        full += [a.mpc_step() for _ in range(k2 - k1)]
     st = io.load_checkpoint(path, cfg)
-    assert st["t"] == 5
+    assert st["t"] == k1
     if kind != "global_pi":
         assert np.any(st["lam"] != 0.0)            # the carried duals are in the checkpoint
     else:
         assert np.any(st["rho_pi"] != cfg.rho)     # the adapted penalties are
     with Solver(cfg, scn) as b:
         b.set_state(st)
-        for k in range(5, 10):
+        for k in range(k1, k2):
             r = b.mpc_step()
             np.testing.assert_array_equal(r.iters, full[k].iters, err_msg=f"step {k}")
             np.testing.assert_allclose(r.xt, full[k].xt, rtol=1e-10, atol=1e-10, err_msg=f"step {k}")
