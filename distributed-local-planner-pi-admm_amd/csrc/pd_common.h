@@ -203,6 +203,7 @@ __device__ __forceinline__ double around(double x, int d) {
 }
 
 // ============================================================ near-tie log (piadmm_get_near_ties)
+#ifndef PIADMM_NO_TIES   // (-DPIADMM_NO_TIES: a diagnostic build without the log, to price it)
 // One event of a discrete decision taken within A.tie_tol of its threshold.  Called by ONE lane,
 // in a cold branch (ties are rare: the hot path pays a compare and a ballot).
 __device__ __forceinline__ void tie_record(const DevArgs& A, int t, int it, int kind, int id, int idx, double margin) {
@@ -255,6 +256,14 @@ __device__ __forceinline__ void scalar_tie(const DevArgs& A, int t, int it, int 
                                            double thr) {
   if (__builtin_expect(fabs(v - thr) <= A.tie_tol * fabs(thr), 0)) tie_record(A, t, it, kind, id, idx, (v - thr) / thr);
 }
+
+#else
+__device__ __forceinline__ void tie_record(const DevArgs&, int, int, int, int, int, double) {}
+__device__ __forceinline__ bool round_near(double, int, double, double*) { return false; }
+__device__ __forceinline__ void round_ties(const DevArgs&, int, int, int, int, int, double, bool) {}
+__device__ __forceinline__ void collide_tie(const DevArgs&, int, int, int, double, bool, double) {}
+__device__ __forceinline__ void scalar_tie(const DevArgs&, int, int, int, int, int, double, double) {}
+#endif
 
 // sum_{k=0}^{H} (k-1-i)+ (k-1-j)+ = (T'T)_{ij}, exact in integers.
 __device__ __forceinline__ double TT(int i, int j, int H) {

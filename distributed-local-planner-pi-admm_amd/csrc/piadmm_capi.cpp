@@ -69,7 +69,7 @@ struct piadmm_ctx {
   int chunk_guess = 2;
   bool host_decide = false;
   // near-tie log (piadmm_get_near_ties): tolerance, and the ties of stop decisions the host takes
-  double tie_tol = 1e-9;
+  double tie_tol = 0.0;         // 0: the log is off (piadmm_set_tie_tolerance turns it on)
   std::vector<piadmm_near_tie_t> host_ties;
   unsigned long long host_tie_cnt[PIADMM_TIE_KINDS] = {};
   // MPC steps per persistent launch agreed over the job's ranks (the fixed-iteration residual
@@ -90,7 +90,7 @@ int fail(piadmm_ctx* h, int code, const std::string& msg) {
 // A stop / distance decision the host takes within tie_tol of its threshold (the device kernels
 // log their own, pd::scalar_tie).
 void host_tie(piadmm_ctx* h, int t, int it, int kind, int id, int idx, double v, double thr) {
-  if (!(std::fabs(v - thr) <= h->tie_tol * std::fabs(thr))) return;
+  if (!(h->tie_tol > 0.0) || !(std::fabs(v - thr) <= h->tie_tol * std::fabs(thr))) return;
   ++h->host_tie_cnt[kind];
   piadmm_near_tie_t ev{};
   ev.step = t;
@@ -344,6 +344,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   // neighbour id (the order of the x-step's consensus sum)
   std::vector<int> g_aptr, g_alist, g_eptr, g_elist, g_nptr, g_nedge, g_ndir;
   std::vector<int> s_cptr, s_elist;     // split: pairs per original component (the residual-sum order)
+  std::vector<int> pair_block;          // split: the block (workgroup) that owns each pair
   if (simple) {
     for (int a = 0; a < N;) {
       const int e = pair_of[a];
@@ -377,7 +378,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     }
     // Components of more than `block` agents (PIADMM_GRAPH_BLOCK, default 4; 0: never) span
     // several workgroups under the global scope: blocks of `block` consecutive agents (in index
-    // order, numbered by first agent), a pair owned by the block of its first agent.  The x-step
+    // order, numbered by first agent), the component's pairs dealt round-robin over its blocks.  The x-step
     // of an agent reads the hat / lam of pairs other blocks own and a pair reads positions of
     // agents other blocks own, so the X and Z phases run as separate launches (the kernel boundary
     // orders them); the stop test sums the blocks' partials (one job-wide decision).
@@ -396,18 +397,34 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
           s_cptr.assign(C + 1, 0);
           for (int e = 0; e < n_edges; ++e) ++s_cptr[comp[edges[2 * e]] + 1];
           for (int k = 0; k < C; ++k) s_cptr[k + 1] += s_cptr[k];
-          s_elist.resize(n_edges);
+          s_elist.resize(n_edges);      // (here: the pair's position in the sum order)
           {
             std::vector<int> fill(s_cptr.begin(), s_cptr.end() - 1);
-            for (int e = 0; e < n_edges; ++e) s_elist[fill[comp[edges[2 * e]]]++] = e;
+            for (int e = 0; e < n_edges; ++e) s_elist[e] = fill[comp[edges[2 * e]]]++;
           }
-          std::vector<int> seen(C, 0), cur(C, -1), nb;
+          const std::vector<int> ocomp = comp;      // original component of each agent
+          std::vector<int> seen(C, 0), cur(C, -1);
+          std::vector<std::vector<int>> blocks_of(C);
           int NB = 0;
           for (int a = 0; a < N; ++a) {
             const int k = comp[a];
-            if (seen[k] % block == 0) cur[k] = NB++;     // a new block of component k
+            if (seen[k] % block == 0) {                  // a new block of component k
+              cur[k] = NB++;
+              blocks_of[k].push_back(cur[k]);
+            }
             ++seen[k];
             comp[a] = cur[k];
+          }
+          // pairs dealt round-robin over the component's blocks (in pair order), so the pair QPs of
+          // a densely coupled component -- an all-pairs crossing: 6 pairs of 4 agents -- run on
+          // several workgroups at once instead of queueing on the first agents' blocks
+          pair_block.assign(n_edges, 0);
+          {
+            std::vector<int> dealt(C, 0);
+            for (int e = 0; e < n_edges; ++e) {
+              const int k = ocomp[edges[2 * e]];
+              pair_block[e] = blocks_of[k][dealt[k]++ % blocks_of[k].size()];
+            }
           }
           C = NB;
           h->split = true;
@@ -417,7 +434,8 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     g_aptr.assign(C + 1, 0);
     g_eptr.assign(C + 1, 0);
     for (int a = 0; a < N; ++a) ++g_aptr[comp[a] + 1];
-    for (int e = 0; e < n_edges; ++e) ++g_eptr[comp[edges[2 * e]] + 1];
+    auto owner = [&](int e) { return h->split ? pair_block[e] : comp[edges[2 * e]]; };
+    for (int e = 0; e < n_edges; ++e) ++g_eptr[owner(e) + 1];
     for (int k = 0; k < C; ++k) {
       g_aptr[k + 1] += g_aptr[k];
       g_eptr[k + 1] += g_eptr[k];
@@ -427,7 +445,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     {
       std::vector<int> fa(g_aptr.begin(), g_aptr.end() - 1), fe(g_eptr.begin(), g_eptr.end() - 1);
       for (int a = 0; a < N; ++a) g_alist[fa[comp[a]]++] = a;
-      for (int e = 0; e < n_edges; ++e) g_elist[fe[comp[edges[2 * e]]]++] = e;
+      for (int e = 0; e < n_edges; ++e) g_elist[fe[owner(e)]++] = e;
     }
     std::vector<std::vector<std::array<int, 3>>> adj(N);
     for (int e = 0; e < n_edges; ++e) {
@@ -541,6 +559,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   rc |= dalloc(h, &A.tie_mg, (size_t)PIADMM_TIE_CAP);
   A.tie_cap = PIADMM_TIE_CAP;
   A.tie_tol = h->tie_tol;
+  A.tie_on = h->tie_tol > 0.0 ? 1 : 0;
   int *d_scp = nullptr, *d_sel = nullptr;
   if (h->split) {
     rc |= dalloc(h, &A.eterm, E * 2);
@@ -617,7 +636,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     HIPCHK(h, hipMemcpyAsync(d_scp, hc.data(), hc.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
     if (E) HIPCHK(h, hipMemcpyAsync(d_sel, he.data(), he.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
     A.sum_cptr = d_scp;
-    A.sum_elist = d_sel;
+    A.sum_pos = d_sel;
     A.sum_C = (int)hc.size() - 1;
   }
   if (sharded) {
@@ -1267,6 +1286,7 @@ int32_t piadmm_set_tie_tolerance(piadmm_handle_t h, double tol) {
   if (!(tol >= 0.0) || !std::isfinite(tol)) return fail(h, PIADMM_E_ARG, "tie tolerance must be finite and >= 0");
   h->tie_tol = tol;
   h->a.tie_tol = tol;          // (the kernels take DevArgs by value: from the next launch on)
+  h->a.tie_on = tol > 0.0 ? 1 : 0;
   return PIADMM_OK;
 }
 

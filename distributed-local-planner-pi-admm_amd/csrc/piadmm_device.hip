@@ -57,6 +57,7 @@ struct LoopCtl {
 
 // collision graph (casadi/main.py:110-118), computed by every wave from this iteration's positions
 // (the pair wave logs a near tie, piadmm_get_near_ties: every wave runs the test in the plain loop)
+template <bool TIES>
 __device__ __forceinline__ bool collide(const DevArgs& A, const StepCtx& X, const double* pos, int it) {
   if (X.e < 0 || X.na != 2) return false;
   bool hit = false;
@@ -67,7 +68,8 @@ __device__ __forceinline__ bool collide(const DevArgs& A, const StepCtx& X, cons
     d2 = dx * dx + dy * dy;
     hit = d2 < X.thr;
   }
-  if (X.w == PW) collide_tie(A, X.t, it, X.e, d2, X.l <= X.H, X.thr);
+  if constexpr (TIES)
+    if (X.w == PW) collide_tie(A, X.t, it, X.e, d2, X.l <= X.H, X.thr);
   return wany(hit);
 }
 
@@ -75,13 +77,14 @@ __device__ __forceinline__ bool collide(const DevArgs& A, const StepCtx& X, cons
 // barrier B when the pair's z-step ran: the residuals in S.sc, the component's stop test, and --
 // single rank, natural global termination -- the in-kernel stop test over all components behind
 // a grid barrier.  Returns true when the component's step ends here.
+template <bool TIES>
 __device__ __forceinline__ bool iter_tail(const DevArgs& A, const StepCtx& X, LoopCtl& L, int it, int& nbar) {
   const piadmm_config_t& c = A.cfg;
   const CompLds& S = X.S;
   const double rk = L.act ? S.sc[0] : 0.0;
   const double sk = L.act ? S.sc[1] : 0.0;
   if (L.act) L.dis_chk = S.sc[2];
-  if (!c.fixed_iters && !X.global && X.w == PW && X.l == 0) {   // near ties of the stop test (one wave)
+  if (TIES && !c.fixed_iters && !X.global && X.w == PW && X.l == 0) {   // near ties of the stop test (one wave)
     scalar_tie(A, X.t, it, PIADMM_TIE_STOP, X.ci, 0, rk, c.eps_pri);
     scalar_tie(A, X.t, it, PIADMM_TIE_STOP, X.ci, 1, sk, c.eps_dual);
   }
@@ -146,7 +149,7 @@ __device__ __forceinline__ bool iter_tail(const DevArgs& A, const StepCtx& X, Lo
       A.ghist[((size_t)X.slot * c.max_outer + it) * 2 + 1] = tsk;
     }
     const bool dist_ok = tseen > 0.0 && tbad == 0.0;
-    if (ci == 0 && threadIdx.x == 0) {
+    if (TIES && ci == 0 && threadIdx.x == 0) {
       scalar_tie(A, X.t, it, PIADMM_TIE_STOP, -1, 0, trk, c.eps_pri);
       scalar_tie(A, X.t, it, PIADMM_TIE_STOP, -1, 1, tsk, c.eps_dual);
     }
@@ -169,7 +172,7 @@ struct WaveCnt {
 // Wave w < na solves agent a0 + w's x-step every outer iteration (casadi/main.py:81-106); its
 // QP state (tables, labels, warm ADMM state) stays in this wave's registers and LDS regions for
 // the whole step.  The pair's state never lives here: the pair wave owns it.
-template <bool BIG>
+template <bool BIG, bool TIES>
 __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
   extern __shared__ double lds[];
   const piadmm_config_t& c = A.cfg;
@@ -331,7 +334,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       n.inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
       warm_x = true;
       const double u = around(ustar[0], c.round_decimals);
-      if (c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
+      if (TIES && c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
       double px, py, pth;
       rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
       if (l <= H) {
@@ -342,7 +345,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       STAMP_ADD(ST_XSTEP, t_xs);
     }
     __syncthreads();                                     // A: every agent's positions
-    L.act = collide(A, X, pos, it);
+    L.act = collide<TIES>(A, X, pos, it);
     if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
       L.stopped = true;
       break;
@@ -352,7 +355,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       __syncthreads();                                   // B: hat, lam, S, D, last, S.sc
       load_cp();
     }
-    if (iter_tail(A, X, L, it, nbar)) break;
+    if (iter_tail<TIES>(A, X, L, it, nbar)) break;
   }
   } else {
   bool have = false;          // the x-step of iteration `it` is already in U (a kept speculation)
@@ -391,7 +394,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       warm_x = true;
       unsigned long long t_rd = STAMP_T();
       const double u = around(ustar[0], c.round_decimals);
-      if (c.round_decimals >= 0) round_ties(A, t, tgt, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
+      if (TIES && c.round_decimals >= 0) round_ties(A, t, tgt, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
       STAMP_ADD(ST_ROUND, t_rd);
       if (l < H) S.u[(tgt & 1) * 2 * H + w * H + l] = u;
       STAMP_ADD(ST_XSTEP, t_xs);
@@ -483,7 +486,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
 // Wave PW owns the component's pair (when it has one): the per-step pair setup (concurrent with
 // the agents' setups), the z-step QP, the hat rollouts, the dual update and the residuals
 // (casadi/main.py:121-181).  Its QP state stays in this wave's registers for the whole step.
-template <bool BIG>
+template <bool BIG, bool TIES>
 __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
   extern __shared__ double lds[];
   const piadmm_config_t& c = A.cfg;
@@ -639,7 +642,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
         }
       wsync();
     }
-    L.act = collide(A, X, pos, it);
+    L.act = collide<TIES>(A, X, pos, it);
     if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
       L.stopped = true;
       if (specm) {
@@ -686,7 +689,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       double hx[2], hy[2], hth;
       for (int v = 0; v < 2; ++v) {
         const double uv = (l < H) ? around(uh[v], c.round_decimals) : 0.0;
-        if (c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_UHAT, e, v * H, uh[v], l < H);
+        if (TIES && c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_UHAT, e, v * H, uh[v], l < H);
         rollout(S.xt + 3 * v, A.spd[X.a0 + v], uv, c, H, true, hx[v], hy[v], hth);
       }
       // dual update (plain :161-162 / PI + anti-windup MATLAB :156-188)
@@ -750,7 +753,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
         S.sc[0] = 2.0 * sqrt(rr);
         S.sc[1] = L.aliased ? 0.0 : 2.0 * sqrt(ss);
         S.sc[2] = rdl(dist, 1);
-        if (c.term_dist_check) scalar_tie(A, t, it, PIADMM_TIE_DIST, e, 0, S.sc[2], X.deff);
+        if (TIES && c.term_dist_check) scalar_tie(A, t, it, PIADMM_TIE_DIST, e, 0, S.sc[2], X.deff);
       }
       STAMP_ADD(ST_ZSTEP, t_z);
     }
@@ -778,7 +781,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     if (specm) {
       // the stop decision here (iter_tail without a grid barrier), published with the iteration's
       // flags before barrier B; the agents adopt it from X.vd
-      const bool stop = iter_tail(A, X, L, it, nbar);
+      const bool stop = iter_tail<TIES>(A, X, L, it, nbar);
       if (l == 0) {
         X.vd[0] = L.act ? 1 : 0;
         X.vd[1] = stop ? 1 : 0;
@@ -795,7 +798,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     unsigned long long t_sb = STAMP_T();
     if (__builtin_expect(L.act, 0)) __syncthreads();     // B
     STAMP_ADD(ST_SYNC_B, t_sb);
-    if (iter_tail(A, X, L, it, nbar)) break;
+    if (iter_tail<TIES>(A, X, L, it, nbar)) break;
   }
   n.warm = e >= 0 && warm_e;
   if (e >= 0) {
@@ -860,7 +863,7 @@ __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
 // iterations for the outputs and the propagation.
 // Wave layout: waves 0 and 1 run the agents' x-steps (agent_part), wave 2 the pair
 // (pair_part); the two loops take the same barriers and stop decisions.
-template <bool BIG>
+template <bool BIG, bool TIES>
 __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
                                               int& nbar) {
   extern __shared__ double lds[];
@@ -939,9 +942,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     S.seed[2 * threadIdx.x + 0] = around(sx, c.round_decimals);
     S.seed[2 * threadIdx.x + 1] = around(sy, c.round_decimals);
     double m;   // near ties of the seeds' rounding, logged once per step (the first launch)
-    if ((flags & F_FIRST) && c.round_decimals >= 0 && round_near(sx, c.round_decimals, A.tie_tol, &m))
+    if (TIES && (flags & F_FIRST) && c.round_decimals >= 0 && round_near(sx, c.round_decimals, A.tie_tol, &m))
       tie_record(A, t, -1, PIADMM_TIE_ROUND_SEED, a, 0, m);
-    if ((flags & F_FIRST) && c.round_decimals >= 0 && round_near(sy, c.round_decimals, A.tie_tol, &m))
+    if (TIES && (flags & F_FIRST) && c.round_decimals >= 0 && round_near(sy, c.round_decimals, A.tie_tol, &m))
       tie_record(A, t, -1, PIADMM_TIE_ROUND_SEED, a, 1, m);
   }
   for (int i = threadIdx.x; i < 32; i += blockDim.x) S.sc[i] = 0.0;
@@ -994,8 +997,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   L.act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
   L.dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
   WaveCnt n;
-  if (X.w < NW) agent_part<BIG>(A, X, L, nbar, n);
-  else if (X.w == PW) pair_part<BIG>(A, X, L, nbar, n);
+  if (X.w < NW) agent_part<BIG, TIES>(A, X, L, nbar, n);
+  else if (X.w == PW) pair_part<BIG, TIES>(A, X, L, nbar, n);
   else roll_part(A, X);
   __syncthreads();
   STAMP_ADD(ST_KERNEL, t_k);
@@ -1058,7 +1061,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 // waits for the slowest one of each step: the launch takes max_c sum_t instead of
 // sum_t max_c.  The step-to-step state (xt, labels, caches) goes through HBM inside one
 // workgroup (same CU: the barrier's workgroup-scope fences order it).
-template <bool BIG>
+template <bool BIG, bool TIES>
 __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
 #ifdef PIADMM_STAMPS
   if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
@@ -1074,7 +1077,7 @@ __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int 
   }
   int nbar = 0;   // grid barriers so far (coop): parity of the termination partials
   for (int k = 0; k < nsteps; ++k) {
-    mpc_step_body<BIG>(A, t0 + k, it0, it1, flags, k, nbar);
+    mpc_step_body<BIG, TIES>(A, t0 + k, it0, it1, flags, k, nbar);
     __syncthreads();
   }
 #ifdef PIADMM_STAMPS
@@ -1156,6 +1159,13 @@ __global__ void k_pair_deff(DevArgs A) {
   A.deff[e] = d;
 }
 
+// The kernel instantiation: matrices in LDS / HBM (BIG), near-tie log compiled in or out (TIES: the log
+// costs 3-10 % of the fused kernel's time, so it is a separate instantiation, on when a handle asks for it)
+static const void* mpc_fn(bool big, bool ties) {
+  if (big) return ties ? (const void*)k_mpc_step<true, true> : (const void*)k_mpc_step<true, false>;
+  return ties ? (const void*)k_mpc_step<false, true> : (const void*)k_mpc_step<false, false>;
+}
+
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s) {
   const size_t sh = lds_bytes(a.cfg.H, a.cfg.precision);
   const bool big = a.cfg.H > HMAX;
@@ -1166,7 +1176,7 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     last = a.stamps;
   }
 #endif
-  const void* fn = big ? (const void*)k_mpc_step<true> : (const void*)k_mpc_step<false>;
+  const void* fn = mpc_fn(big, a.tie_on != 0);
   // the dynamic-LDS limit is a per-device function attribute: set it on every launch (cheap),
   // so handles on several devices of one process each get it
   if (launch_rc(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)) != 0) return -1;
@@ -1186,11 +1196,9 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     return e && e[0] == '1';
   }();
   const int nt = (a.cfg.pos_model != 0 && !no_roller ? NWA : NWT) * WAVE;
-  if (big)
-    hipLaunchKernelGGL(k_mpc_step<true>, dim3(a.C), dim3(nt), sh, s, a, t, nsteps, it0, it1, flags);
-  else
-    hipLaunchKernelGGL(k_mpc_step<false>, dim3(a.C), dim3(nt), sh, s, a, t, nsteps, it0, it1, flags);
-  return launch_rc(hipGetLastError());
+  DevArgs aa = a;
+  void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
+  return launch_rc(hipLaunchKernel(fn, dim3(a.C), dim3(nt), args, sh, s));
 }
 
 // Can every workgroup of a k_mpc_step launch be resident at once (cooperative launch)?
@@ -1201,7 +1209,7 @@ bool coop_fits(const DevArgs& a, int device) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return false;
   const size_t sh = lds_bytes(a.cfg.H, a.cfg.precision);
   const bool big = a.cfg.H > HMAX;
-  const void* fn = big ? (const void*)k_mpc_step<true> : (const void*)k_mpc_step<false>;
+  const void* fn = mpc_fn(big, a.tie_on != 0);
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return false;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NWT * WAVE, sh) != hipSuccess) return false;
   return (long long)per * ncu >= (long long)a.C;
@@ -1231,7 +1239,7 @@ __global__ void k_decide(DevArgs A, int t, int it, const double* part) {
   g[3] = 1;
   A.ghist[2 * it + 0] = rk;
   A.ghist[2 * it + 1] = sk;
-  if (!c.fixed_iters) {
+  if (A.tie_on && !c.fixed_iters) {
     scalar_tie(A, t, it, PIADMM_TIE_STOP, -1, 0, rk, c.eps_pri);
     scalar_tie(A, t, it, PIADMM_TIE_STOP, -1, 1, sk, c.eps_dual);
   }

@@ -47,7 +47,7 @@ struct GCnt {
 };
 
 // -------------------------------------------------------------------- X phase: one agent
-template <bool BIG>
+template <bool BIG, bool TIES>
 __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, int it, const GWave& W, GCnt& n) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, l = lid();
@@ -137,7 +137,7 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, int it, 
   n.inexact += (st & PIADMM_QP_INEXACT) ? 1 : 0;
   // round (casadi/main.py:103), pos_old = dynamic_update_local (:105)
   const double u = around(ustar[0], c.round_decimals);
-  if (c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_U, a, 0, ustar[0], l < H);
+  if (TIES && c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_U, a, 0, ustar[0], l < H);
   double px, py, pth;
   rollout_r(xt3[0], xt3[1], xt3[2], s, s / c.L, (l < H) ? u : 0.0, c, H, c.pos_model != 0, px, py, pth);
   double* po = A.pos_old + (size_t)a * 2 * H1;
@@ -179,6 +179,7 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, int it, 
 // -------------------------------------------------------------------- Z phase: one pair
 // Returns nothing; writes edge_active, and when the pair collides hat, lam, S, D, eres, dischk.
 // The collision test of pair e (casadi/main.py:110-113): writes edge_active, returns it.
+template <bool TIES>
 __device__ __forceinline__ bool g_ztest(const DevArgs& A, int e, int t, int it) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, l = lid();
@@ -196,7 +197,7 @@ __device__ __forceinline__ bool g_ztest(const DevArgs& A, int e, int t, int it) 
     hit = d2 < thr;
   }
   // the global-PI script has no collision test: its edge problem runs every iteration
-  if (!c.no_collision_gate) collide_tie(A, t, it, e, d2, tl, thr);
+  if (TIES && !c.no_collision_gate) collide_tie(A, t, it, e, d2, tl, thr);
   const bool act = c.no_collision_gate ? true : wany(hit);
   if (l == 0) A.edge_active[e] = act ? 1 : 0;
   return act;
@@ -204,7 +205,7 @@ __device__ __forceinline__ bool g_ztest(const DevArgs& A, int e, int t, int it) 
 
 // The z-step of a colliding pair e: the pair QP, the hat rollouts, the dual update and the pair's
 // residual terms (casadi/main.py:121-173).
-template <bool BIG>
+template <bool BIG, bool TIES>
 __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, const GWave& W, GCnt& n) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, l = lid();
@@ -315,7 +316,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
   double hx[2], hy[2], hth;
   for (int v = 0; v < 2; ++v) {
     const double uv = (l < H) ? around(uh[v], c.round_decimals) : 0.0;
-    if (c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_UHAT, e, v * H, uh[v], l < H);
+    if (TIES && c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_UHAT, e, v * H, uh[v], l < H);
     rollout(v ? xb : xa, A.spd[v ? v2 : v1], uv, c, H, true, hx[v], hy[v], hth);
   }
   double rr = 0.0, ss = 0.0, dchk;
@@ -442,7 +443,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
     qw[(7 + q) * WAVE + l] = qe.E[q] * ys[q];
     lw[q * WAVE + l] = lab[q];
   }
-  if (c.term_dist_check && l == 0) scalar_tie(A, t, it, PIADMM_TIE_DIST, e, 0, dchk, deff);
+  if (TIES && c.term_dist_check && l == 0) scalar_tie(A, t, it, PIADMM_TIE_DIST, e, 0, dchk, deff);
   if (l == 0) {
     A.eres[2 * e] = rfac * sqrt(rr);
     A.eres[2 * e + 1] = rfac * sqrt(ss);
@@ -456,6 +457,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
 // -------------------------------------------------------------------- step init / final
 // Seeds (casadi/main.py:48-49), the per-step reset of hat, lam and the PI accumulators (:52-63;
 // shifted one slot with warm_duals, optimizer.py:337-344), the warm labels of the previous step.
+template <bool TIES>
 __device__ __forceinline__ void g_step_init(const DevArgs& A, int ci, int w, int t) {
   const piadmm_config_t& c = A.cfg;
   const int H = c.H, H1 = H + 1, l = lid();
@@ -467,9 +469,9 @@ __device__ __forceinline__ void g_step_init(const DevArgs& A, int ci, int w, int
       A.seed_g[2 * a] = around(sx, c.round_decimals);
       A.seed_g[2 * a + 1] = around(sy, c.round_decimals);
       double m;
-      if (c.round_decimals >= 0 && round_near(sx, c.round_decimals, A.tie_tol, &m))
+      if (TIES && c.round_decimals >= 0 && round_near(sx, c.round_decimals, A.tie_tol, &m))
         tie_record(A, t, -1, PIADMM_TIE_ROUND_SEED, a, 0, m);
-      if (c.round_decimals >= 0 && round_near(sy, c.round_decimals, A.tie_tol, &m))
+      if (TIES && c.round_decimals >= 0 && round_near(sy, c.round_decimals, A.tie_tol, &m))
         tie_record(A, t, -1, PIADMM_TIE_ROUND_SEED, a, 1, m);
     }
     // the previous step's final labels shifted by one time slot: a guess for the first polish
@@ -542,7 +544,7 @@ __device__ __forceinline__ void g_step_final(const DevArgs& A, int ci, int w) {
 }
 
 // -------------------------------------------------------------------- one MPC step
-template <bool BIG>
+template <bool BIG, bool TIES>
 __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
                                                 int& nbar) {
   extern __shared__ double lds[];
@@ -589,7 +591,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
 
   unsigned long long t_body = STAMP_T();
   if (first) {
-    g_step_init(A, ci, w, t);
+    g_step_init<TIES>(A, ci, w, t);
     for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) resid[i] = NAN;   // "not evaluated"
     if (coop && ci == 0)
       for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) A.ghist[(size_t)slot * 2 * M + i] = NAN;
@@ -625,7 +627,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       unsigned long long t_xp = STAMP_T();
       for (int i = a0 + w; i < a1; i += GW) {
         const int a = A.comp_alist[i];
-        if (!A.owned || A.owned[a]) g_xstep<BIG>(A, a, t, it, W, n);
+        if (!A.owned || A.owned[a]) g_xstep<BIG, TIES>(A, a, t, it, W, n);
       }
       STAMP_ADD(ST_XSTEP, t_xp);
       unsigned long long t_sa = STAMP_T();
@@ -655,7 +657,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
     const bool deal = e1 - e0 <= GZMAX;
     if (deal) {
       for (int j = e0 + w; j < e1; j += GW) {
-        const bool act = g_ztest(A, A.comp_elist[j], t, it);
+        const bool act = g_ztest<TIES>(A, A.comp_elist[j], t, it);
         if (l == 0) s_zact[j - e0] = act ? 1 : 0;
       }
       __syncthreads();
@@ -670,9 +672,9 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
           mine = act && (k % GW == w);
           k += act ? 1 : 0;
         } else {
-          mine = g_ztest(A, e, t, it);
+          mine = g_ztest<TIES>(A, e, t, it);
         }
-        if (mine) g_zstep<BIG>(A, e, t, it, W, n);
+        if (mine) g_zstep<BIG, TIES>(A, e, t, it, W, n);
       }
     }
     STAMP_ADD(ST_ZSTEP, t_zp);
@@ -699,8 +701,9 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
         // split component: the pair's terms of this iteration's sum, added in the reference's
         // order over the whole original component by k_graph_partials
         if (A.eterm && in) {
-          A.eterm[2 * e] = r0;
-          A.eterm[2 * e + 1] = aliased ? 0.0 : r1;
+          const int sp = A.sum_pos[e];
+          A.eterm[sp] = r0;
+          A.eterm[A.E + sp] = aliased ? 0.0 : r1;
         }
         const unsigned long long bseen = __ballot(seen), bbad = __ballot(bad), bact = __ballot(act);
         const int npr = min(WAVE, e1 - j0);
@@ -746,7 +749,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       resid[2 * it + 1] = sk;
     }
     bool stop = !c.fixed_iters && !global && rk <= c.eps_pri && sk <= c.eps_dual && (!c.term_dist_check || dist_ok);
-    if (!c.fixed_iters && !global && threadIdx.x == 0) {
+    if (TIES && !c.fixed_iters && !global && threadIdx.x == 0) {
       scalar_tie(A, t, it, PIADMM_TIE_STOP, ci, 0, rk, c.eps_pri);
       scalar_tie(A, t, it, PIADMM_TIE_STOP, ci, 1, sk, c.eps_dual);
     }
@@ -789,7 +792,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
         A.ghist[((size_t)slot * M + it) * 2 + 0] = trk;
         A.ghist[((size_t)slot * M + it) * 2 + 1] = tsk;
       }
-      if (ci == 0 && threadIdx.x == 0) {
+      if (TIES && ci == 0 && threadIdx.x == 0) {
         scalar_tie(A, t, it, PIADMM_TIE_STOP, -1, 0, trk, c.eps_pri);
         scalar_tie(A, t, it, PIADMM_TIE_STOP, -1, 1, tsk, c.eps_dual);
       }
@@ -840,7 +843,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   STAMP_ADD(ST_KERNEL, t_body);
 }
 
-template <bool BIG>
+template <bool BIG, bool TIES>
 __global__ void __launch_bounds__(GW * WAVE) k_graph_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
   if (flags & F_DEVSTOP) {      // device-decided global stop (uniform: every thread reads it)
     if (!(flags & F_LAST)) {
@@ -856,7 +859,7 @@ __global__ void __launch_bounds__(GW * WAVE) k_graph_step(DevArgs A, int t0, int
 #endif
   int nbar = 0;
   for (int k = 0; k < nsteps; ++k) {
-    graph_step_body<BIG>(A, t0 + k, it0, it1, flags, k, nbar);
+    graph_step_body<BIG, TIES>(A, t0 + k, it0, it1, flags, k, nbar);
     __syncthreads();
   }
 #ifdef PIADMM_STAMPS
@@ -892,22 +895,48 @@ __global__ void __launch_bounds__(GW * WAVE) k_graph_partials(DevArgs A, double*
     out[threadIdx.x] = tot;
   }
   if (split) {
+    // Every term is >= 0 and x + 0.0 == x, so the zero terms (inactive pairs: nearly all) and the
+    // components without a nonzero term are skipped exactly: the terms are loaded 16 per lane at a
+    // time (coalesced: eterm is in sum order), and only the nonzero ones are added, in order.
     const int q = threadIdx.x >> 6;            // wave 0: rk, wave 1: sk
     const int l = lid();
-    double tot = 0.0;
-    for (int k = 0; k < A.sum_C; ++k) {
-      const int j1 = A.sum_cptr[k + 1];
-      double cs = 0.0;
-      for (int j0 = A.sum_cptr[k]; j0 < j1; j0 += WAVE) {
-        const int j = j0 + l;
-        const double r = j < j1 ? A.eterm[2 * A.sum_elist[j] + q] : 0.0;
-        const int n = min(WAVE, j1 - j0);
-        for (int i = 0; i < n; ++i) cs += rdl(r, i);
+    const double* et = A.eterm + (size_t)q * A.E;
+    double tot = 0.0, cs = 0.0;
+    int k = 0, kend = A.sum_cptr[1];
+    constexpr int PB = 16;
+    for (int base = 0; base < A.E; base += PB * WAVE) {
+      double r[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int j = base + u * WAVE + l;
+        r[u] = j < A.E ? et[j] : 0.0;
       }
-      tot += cs;
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        unsigned long long nz = __ballot(r[u] != 0.0);
+        while (nz) {
+          const int i = __ffsll(nz) - 1;
+          nz &= nz - 1;
+          const int j = base + u * WAVE + i;
+          while (j >= kend) {                   // a component boundary: its sum joins the total
+            tot += cs;
+            cs = 0.0;
+            ++k;
+            kend = A.sum_cptr[k + 1];
+          }
+          cs += rdl(r[u], i);
+        }
+      }
     }
+    tot += cs;
     if (l == 0) out[q] = tot;
   }
+}
+
+// The kernel instantiation: big-mode layout (BIG) and the near-tie log compiled in or out (TIES).
+static const void* graph_fn(bool big, bool ties) {
+  if (big) return ties ? (const void*)k_graph_step<true, true> : (const void*)k_graph_step<true, false>;
+  return ties ? (const void*)k_graph_step<false, true> : (const void*)k_graph_step<false, false>;
 }
 
 int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s) {
@@ -920,7 +949,7 @@ int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int
   }
 #endif
   const bool big = a.cfg.H > HMAX;
-  const void* fn = big ? (const void*)k_graph_step<true> : (const void*)k_graph_step<false>;
+  const void* fn = graph_fn(big, a.tie_on != 0);
   if (launch_rc(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)) != 0) return -1;
   if (flags & F_COOP) {
     DevArgs aa = a;
@@ -929,11 +958,9 @@ int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int
     return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(GW * WAVE), args, (unsigned)sh, s));
   }
   (void)hipGetLastError();   // a stale error of an earlier runtime call is not this launch's
-  if (big)
-    hipLaunchKernelGGL(k_graph_step<true>, dim3(a.C), dim3(GW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
-  else
-    hipLaunchKernelGGL(k_graph_step<false>, dim3(a.C), dim3(GW * WAVE), sh, s, a, t, nsteps, it0, it1, flags);
-  return launch_rc(hipGetLastError());
+  DevArgs aa = a;
+  void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
+  return launch_rc(hipLaunchKernel(fn, dim3(a.C), dim3(GW * WAVE), args, sh, s));
 }
 
 bool graph_coop_fits(const DevArgs& a, int device) {
@@ -942,7 +969,7 @@ bool graph_coop_fits(const DevArgs& a, int device) {
     return false;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return false;
   const size_t sh = graph_lds_bytes(a.cfg.H);
-  const void* fn = a.cfg.H > HMAX ? (const void*)k_graph_step<true> : (const void*)k_graph_step<false>;
+  const void* fn = graph_fn(a.cfg.H > HMAX, a.tie_on != 0);
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return false;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, GW * WAVE, sh) != hipSuccess) return false;
   return (long long)per * ncu >= (long long)a.C;

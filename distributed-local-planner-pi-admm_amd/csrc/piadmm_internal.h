@@ -128,9 +128,10 @@ struct DevArgs {
   // reference's order -- per ORIGINAL connected component its pairs in increasing pair order, then
   // the components in order (casadi/main.py:165-173; the oracle's comp_r sum) -- instead of the
   // blocks' partial sums.  The T phase writes each pair's effective terms, k_graph_partials sums them.
-  double* eterm;            // E*2 (rk_e, sk_e) of this iteration's sum (0: inactive / not counted / aliased)
-  const int* sum_cptr;      // sum_C+1 pairs of original component k: sum_elist[sum_cptr[k] .. sum_cptr[k+1])
-  const int* sum_elist;     // E
+  double* eterm;            // 2*E: rk terms | sk terms of this iteration, in the sum order (0: inactive /
+                            //   not counted / aliased)
+  const int* sum_cptr;      // sum_C+1 original component k = sum positions [sum_cptr[k], sum_cptr[k+1])
+  const int* sum_pos;       // E   the pair's position in the sum order
   int sum_C;                // 0: no split (the blocks ARE the components)
   // ---- near-tie log (piadmm_get_near_ties): the reference's discrete decisions taken within
   // tie_tol of their threshold -- rounding (casadi/main.py:48-49,103,153), the collision test
@@ -141,6 +142,7 @@ struct DevArgs {
   int* tie_ev;                   // tie_cap x 6 ints: step, iter, kind, id, index, 0
   double* tie_mg;                // tie_cap margins
   int tie_cap;
+  int tie_on;                    // the log is on (tie_tol > 0): the kernels' TIES instantiation
   double tie_tol;
 };
 

@@ -205,7 +205,8 @@ class PI_ADMM_MI355X:
         self._check(self.lib.piadmm_reset_counters(self._h))
 
     def set_tie_tolerance(self, tol: float):
-        """Tolerance of the near-tie log (default 1e-9; piadmm_set_tie_tolerance)."""
+        """Turn the near-tie log on with this tolerance (e.g. 1e-9), or off with 0 (the default:
+        the log's kernel instantiation costs 3-10 % of a step; piadmm_set_tie_tolerance)."""
         self._check(self.lib.piadmm_set_tie_tolerance(self._h, float(tol)))
 
     def near_ties(self):

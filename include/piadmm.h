@@ -215,7 +215,9 @@ int32_t piadmm_get_component_counters(piadmm_handle_t h, uint64_t* out, int32_t 
  * dis_vec(2) > dis_thres (ADMM_CVX_..._PI_antiwindup.m:202).  Two exact implementations (this
  * library, a CPU port, the reference) agree on every continuous value to rounding, so their
  * trajectories can part only where such a decision falls within rounding of its threshold.  The
- * library records every decision taken within `tol` of its threshold (default 1e-9):
+ * library records, once piadmm_set_tie_tolerance(h, tol > 0) has turned the log on, every decision
+ * taken within `tol` of its threshold (1e-9 is a good choice; tol = 0, the default, turns it off:
+ * the kernels then run an instantiation without the checks -- the log costs 3-10 % of a step):
  *   PIADMM_TIE_ROUND_U     an x-step control        id = agent, index = horizon slot k
  *   PIADMM_TIE_ROUND_UHAT  a pair (edge) control    id = pair,  index = side * H + k
  *   PIADMM_TIE_ROUND_SEED  a seed                   id = agent, index = 0 (x) / 1 (y)

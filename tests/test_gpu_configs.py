@@ -159,6 +159,7 @@ def test_gpu_equals_bopt_on_the_crossing_workload(Solver, kw, n_steps):
     pert = cpu_bopt.run(cfg, at(scn.xt0 * (1.0 + 1e-12)), n_steps, threads=8)
     resync, env1, free, env = [], [], [], []
     with Solver(cfg, scn) as s:
+        s.set_tie_tolerance(1e-9)
         xt_prev = scn.xt0.copy()
         for k in range(n_steps):
             rg = s.mpc_step()
