@@ -182,7 +182,7 @@ def cpu_baseline(wl: dict, budget_s: float, K: int) -> dict:
 
 
 def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_rank: int, dist, split="components",
-        share: int = 0):
+        share: int = 0, precision: int = 0):
     """Time K MPC steps of workload wl on this rank; returns (metrics, counters, solver info).
     share > 1 (strong scaling, one process): rank 0's share of a share-rank job alone on this GPU --
     its agents (and, interleaved, its ghosts), every collective a no-op (SURVEY.md 8e readiness)."""
@@ -191,7 +191,7 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
     from piadmm.solver import PI_ADMM_MI355X
     H, M = wl["H"], wl["max_outer"]
     cfg = config.PRESETS[wl["preset"]](H=H, fixed_iters=0 if natural else 1, max_outer=M, term_global=1,
-                                       tighten=wl["tighten"])
+                                       tighten=wl["tighten"], precision=precision)
     n_steps = max(K, W, 1)
     shard = None
     if wl["scaling"] == "strong":
@@ -411,6 +411,9 @@ def main():
     ap.add_argument("--obca-batch", type=int, default=4096, help="--obca: local problems per GPU")
     ap.add_argument("--split", choices=("components", "interleaved"), default="components",
                     help="--strong: whole tiles per rank, or every tile across two ranks (boundary exchange)")
+    ap.add_argument("--precision", type=int, default=0, choices=(0, 1, 2),
+                    help="piadmm_config_t.precision: 2 = the x-step tables read in fp32 + one fp64 refinement "
+                         "(where they live in HBM: --config5's H = 50), the configs[4] fp32 study")
     ap.add_argument("--share", type=int, default=0,
                     help="--strong on one GPU: time rank 0's share of a SHARE-rank job alone, collectives as "
                          "no-ops (interleaved: the exchange is a device copy, ghosts read zeros) -- the "
@@ -448,7 +451,7 @@ def main():
     K, W = args.steps, args.warmup
     if args.share and (not args.strong or world != 1):
         raise SystemExit("bench.py: --share needs --strong on one GPU")
-    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist, args.split, args.share)
+    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist, args.split, args.share, args.precision)
 
     # value = units all ranks processed / the max-over-ranks wall time.  Weak scaling: one unit =
     # one outer iteration of a rank's (256-agent) block, so all ranks processed world x job
@@ -481,7 +484,7 @@ def main():
         "higher_is_better": True,
         "scaling": wl["scaling"],
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f64" if args.precision != 2 else "f64 (x-step tables read as f32, one f64 refinement)",
         "data": (f"synthetic: seeded four-vehicle all-pairs crossings (lanes 0, 1 = the reference's 2-vehicle "
                  f"intersection; {agents_job} agents in the job)" if wl.get("kind") == "crossing" else
                  f"synthetic: one seeded {agents_job}-vehicle chain on the crossing's lanes (candidate pairs (k, k+1))"
@@ -555,7 +558,7 @@ def main():
     line["latency"] = lat
 
     if not args.natural and not args.no_natural:
-        mn, cn = run(wl, True, K, W, rank, world, local_rank, dist, args.split, args.share)
+        mn, cn = run(wl, True, K, W, rank, world, local_rank, dist, args.split, args.share, args.precision)
         line["natural"] = {
             "ms_per_step": mn["wall"] / K * 1e3,
             "outer_iters_per_step": mn["job_iters"] / K,

@@ -58,6 +58,8 @@ struct QP {
   int tstep;              // MPC step index (warm-set bookkeeping)
   int pre_m = -1;         // pair: rows of the stored active set already appended (gi_solve prebuild), -1: none
   int pre_wbits = 0;
+  float* t32 = nullptr;   // x-step, precision 2 (tables in HBM): fp32 copies of the UNFOLDED G (H x H) and
+                          // X' (H rows, stride XLDG) -- the hit path's tables, refined once in fp64
 
   __device__ __forceinline__ bool hinge(int s) const { return NV == 2 && s == 4; }
   // Row s of vehicle v = s / 2: even = box (lanes < H), odd = rate (lanes < H-1), 4 = hinge
@@ -841,6 +843,16 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
     if (l < H) Gp[H * H + l] = gacc;
     if (P.gmem) gsync();
     else wsync();
+    if (P.t32) {
+      // precision 2: fp32 images of the unfolded G and X' (the fp64 tables stay: the fallback)
+      float* G32 = P.t32;
+      float* X32 = P.t32 + H * H;
+      for (int k = 0; k < H; ++k) {
+        if (l < H) G32[k * H + l] = (float)Gp[k * H + l];
+        if (l < m) X32[k * XLDG + l] = (float)XTp[k * P.xld + l];
+      }
+      gsync();
+    }
   }
   // fold q = T'-apply(w') into the tables: row k of G T' (and X T') is
   // sum_{j<k} (k - j) row j -- two running sums per lane, in place (read before write)
@@ -864,6 +876,115 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   if (in_lds(XT)) tables(lds_ptr(XT), lds_ptr(P.G));
   else tables(gbl_ptr(XT), gbl_ptr(P.G));
   return true;
+}
+
+// ---- precision 2: the parametric hit from fp32 tables, refined once in fp64 (configs[4] study).
+// s_g = sum_j G32[j][lane] a_j (lane < H), s_x = sum_j X32[j][lane] b_j (lane < m): fp32 table entries,
+// fp64 products and sums; a, b broadcast from LDS (zero-padded to 64).
+template <int XU>
+__device__ __forceinline__ void pass32(const QP<1>& P, int m, const ldsd* va, const ldsd* vbv, double& sg, double& sx) {
+  const int l = lid(), H = P.H;
+  const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
+  const float* gp = P.t32 + lc;
+  const float* xp = P.t32 + H * H + la;
+  double ag = 0.0, ax = 0.0;
+  for (int j0 = 0; j0 < H; j0 += XU) {
+    float gv[XU], xv[XU];
+    double av[XU], bv[XU];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int j = min(j0 + u, H - 1);
+      gv[u] = gp[j * H];
+      xv[u] = xp[j * XLDG];
+      av[u] = va[j0 + u];
+      bv[u] = vbv[j0 + u];
+    }
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      ag += (double)gv[u] * av[u];
+      ax += (double)xv[u] * bv[u];
+    }
+  }
+  sg = ag;
+  sx = ax;
+}
+
+// The hit with fp32 G, X' (unfolded) and ONE step of iterative refinement in fp64 against the exact
+// KKT residual of the working set: x0 = g - G32 q, lam0 = -X32 q - beta; r1 = P x0 + q + A_W' lam0,
+// r2 = A_W x0 - b (matrix-free P, stencil A); d = X32' r2; dx = -G32 r1 - d,
+// dlam = -X32 (r1 - P d) (S^-1 = X P X', so S^-1 r2 = X P d).  g and beta stay fp64.  The answer goes
+// to the same KKT certificate as every other solve (a failure falls back to the fp64 paths).
+template <int XU>
+__device__ __forceinline__ void hit32(const QP<1>& P, int m, const bool* inW, const int* pos, const signed char* lab,
+                                      double* x, double* y) {
+  const int l = lid(), H = P.H;
+  const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
+  ldsd* va = lds_ptr(P.vb + 256);
+  ldsd* vbv = lds_ptr(P.vb + 320);
+  ldsd* vr2 = lds_ptr(P.vb + 384);
+  const double gfix = P.G[H * H + lc];                         // g (fp64, row H of the table)
+  const double bfix = P.XT[H * P.xld + la];                    // beta (fp64, row H of X')
+  const double q = Tt_apply(P.wq);
+  const double qv = (l < H) ? q : 0.0;
+  va[l] = qv;
+  vbv[l] = qv;
+  wsync();
+  double sg, sx;
+  pass32<XU>(P, m, va, vbv, sg, sx);
+  double x0[1] = {(l < H) ? gfix - sg : 0.0};
+  const double lam0 = (l < m) ? -sx - bfix : 0.0;
+  wsync();
+  vr2[l] = lam0;                                               // (W-row multipliers, lane a)
+  wsync();
+  double y0[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) y0[s] = inW[s] ? vr2[pos[s]] : 0.0;
+  // r1 = P x0 + q + A_W' lam0 (var lanes), r2 = A_W x0 - b (W rows)
+  double px[1], aty[1], ax[2];
+  P_mul(P, x0, px);
+  At_mul(P, y0, aty);
+  A_mul(P, x0, ax);
+  const double r1 = (l < H) ? px[0] + qv + aty[0] : 0.0;
+  wsync();
+  vr2[l] = 0.0;
+  wsync();
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    if (inW[s]) vr2[pos[s]] = ax[s] - ((lab[s] == LOWER) ? P.lo(s) : P.hi(s));
+  wsync();
+  // d = X32' r2 (lane j = variable: its own row of X')
+  double dd = 0.0;
+  {
+    const int mu = unif(m);
+    const float* xr = P.t32 + H * H + lc * XLDG;
+    for (int a0 = 0; a0 < mu; a0 += XU) {
+      float xv[XU];
+      double rv[XU];
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        xv[u] = xr[min(a0 + u, mu - 1)];
+        rv[u] = (a0 + u < mu) ? vr2[a0 + u] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < XU; ++u) dd += (double)xv[u] * rv[u];
+    }
+    if (l >= H) dd = 0.0;
+  }
+  double dv[1] = {dd}, pd[1];
+  P_mul(P, dv, pd);
+  wsync();
+  va[l] = r1;
+  vbv[l] = (l < H) ? r1 - pd[0] : 0.0;
+  wsync();
+  pass32<XU>(P, m, va, vbv, sg, sx);
+  x[0] = (l < H) ? x0[0] - sg - dd : 0.0;
+  const double lam = (l < m) ? lam0 - sx : 0.0;
+  wsync();
+  vr2[l] = lam;
+  wsync();
+#pragma unroll
+  for (int s = 0; s < 2; ++s) y[s] = inW[s] ? vr2[pos[s]] : 0.0;
+  wsync();
 }
 
 template <int XU>
@@ -916,6 +1037,10 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
   (void)cids;
   wsync();
   STAMP_ADD(ST_RSX_PRE, t_pre);
+  if (P.t32) {                       // precision 2: fp32 tables + one fp64 refinement step
+    hit32<XU>(P, m, inW, pos, lab, x, y);
+    return true;
+  }
   unsigned long long t_rs = STAMP_T();
   // one fused pass: x = -G q + g (lane = variable), lam = -X q - beta (lane = W row)
   double ag = 0.0, ax = 0.0;

@@ -142,7 +142,8 @@ int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
   if (c.max_inner <= 0 || c.polish_every <= 0) return fail(h, PIADMM_E_ARG, "max_inner, polish_every must be > 0");
   if (c.round_decimals > 12) return fail(h, PIADMM_E_ARG, "round_decimals must be <= 12");
   if (c.tighten && !(c.tight_p > 0 && c.tight_p < 1)) return fail(h, PIADMM_E_ARG, "tight_p must be in (0, 1)");
-  if (c.precision != 0 && c.precision != 1) return fail(h, PIADMM_E_ARG, "precision must be 0 (fp64) or 1 (fp32 ADMM matrices)");
+  if (c.precision < 0 || c.precision > 2)
+    return fail(h, PIADMM_E_ARG, "precision must be 0 (fp64), 1 (fp32 ADMM matrices) or 2 (fp32 x-step tables)");
   if (pd::lds_bytes(c.H, c.precision) + pd::STATIC_LDS > pd::MAX_LDS)
     return fail(h, PIADMM_E_ARG, "the workgroup's LDS exceeds 160 KB (precision 1 keeps the pair's fp32 "
                                   "K_s^-1 in LDS: H <= 55 in big mode)");
@@ -529,6 +530,8 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   A.ke_stride = A.graph ? std::max(4 * H * H, 2 * H * pd::WAVE) : 4 * H * H;
   rc |= dalloc(h, &A.Ke_g, big ? E * A.ke_stride : 1);
   rc |= dalloc(h, &A.Yx_g, big ? (size_t)N * pd::WAVE * H : 1);
+  if (h->cfg.precision == 2 && big)
+    rc |= dalloc(h, &A.T32_g, (size_t)N * (H * H + H * pd::XLDG));
   rc |= dalloc(h, &A.tab_e, E * 8 * H * H);
   rc |= dalloc(h, &A.warm_ok, (size_t)N);
   rc |= dalloc(h, &A.Sacc, E * 4 * H1);

@@ -233,6 +233,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     // (LDS mode; K_s^-1 is reloaded from its HBM copy if ADMM runs later)
     qx.gws = nullptr;
     qx.tstep = t;
+    qx.t32 = (big && A.T32_g) ? A.T32_g + (size_t)a * (H * H + H * XLDG) : nullptr;
     // (big mode: a per-agent HBM buffer, K_s^-1 stays intact)
     qx.Y = big ? A.Yx_g + (size_t)a * WAVE * H : (f32 ? (double*)(Kxf + w * kxf_stride(H)) : Kx + w * H * H);
     qx.ycap = !A.x_gi ? 0 : (big ? WAVE : (f32 ? (H * H / 2) / H : H));

@@ -77,6 +77,7 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, int it, 
   qx.mmax = xrows(H);
   qx.gws = nullptr;
   qx.tstep = t;
+  qx.t32 = A.T32_g ? A.T32_g + (size_t)a * (H * H + H * XLDG) : nullptr;
   // the dual active set's columns: LDS when they fit (H <= HMAX), else the agent's HBM buffer
   qx.Y = W.ylds ? W.ylds : A.Yx_g + (size_t)a * WAVE * H;
   qx.ycap = A.x_gi ? (W.ylds ? GYCAP : WAVE) : 0;

@@ -67,6 +67,7 @@ struct DevArgs {
   double* XT_g;             // N*(H+1)*XLDG  x-step X' | beta
   double* Ke_g;             // E*4*H*H     pair K_s^-1
   double* Yx_g;             // N*64*H      x-step dual active-set columns P^-1 n_a (big mode)
+  float* T32_g;             // precision 2: N*(H*H + H*XLDG) fp32 images of the x-step G | X' (unfolded)
   double* tab_e;            // E * 8H^2 polish tables per edge, one block each:
                             //   [0, 4H^2) P^-1 (2H x 2H, block-diagonal), [4H^2, 6H^2) PGt (H x 2H,
                             //   row k = P_v^-1 T(k+1,.)'), [6H^2, 8H^2) GPG (Z_v = T P_v^-1 T')

@@ -87,7 +87,11 @@ typedef struct piadmm_config {
   int32_t tighten;           /* 1: delay-tightened safety distance d_eff = dis_thres + |delta_i| + |delta_j|
                                 (compute_square_halfspaces_ca_prob, decentralized/util.py:70-101) */
   int32_t precision;         /* 0: fp64; 1: ADMM iteration matrices K_s^-1 stored fp32 (half the LDS),
-                                polish and certificate fp64 -- answers unchanged (configs[4] study) */
+                                polish and certificate fp64 -- answers unchanged; 2 (ABI 6): the x-step's
+                                parametric tables G, X' read in fp32 where they live in HBM (H > 32, or
+                                the graph kernel), fp64 accumulation and ONE fp64 refinement step
+                                against the exact KKT residual, then the same certificate -- answers
+                                move at the 1e-7..1e-9 level (configs[4] fp32 tolerance study) */
   double tight_p, avg_delay, var_delay;   /* VehicleConfig prob / avg_delay / var_delay (veh_config.py:25-27) */
   /* ABI 3: PIADMM_DUAL_PI_GLOBAL (casadi_old_PI_ADMM/main.py:133-151), per pair from the minimum
    * distance d of the x-step plans (nonlinear rollouts): rho = clamp(rho_num / d, rho_min, rho_max)
