@@ -38,6 +38,7 @@ Prints ONE JSON line (rank 0) with roofline, latency and cpu_baseline objects.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import glob
 import json
 import os
@@ -186,6 +187,7 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
     """Time K MPC steps of workload wl on this rank; returns (metrics, counters, solver info).
     share > 1 (strong scaling, one process): rank 0's share of a share-rank job alone on this GPU --
     its agents (and, interleaved, its ghosts), every collective a no-op (SURVEY.md 8e readiness)."""
+    import numpy as np
     from piadmm import config, scenario
     from piadmm import dist as pdist
     from piadmm.solver import PI_ADMM_MI355X
@@ -200,11 +202,22 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
         if split == "interleaved":
             shard = pdist.shard_graph(full, srank, sworld, pdist.owners_interleaved(full.n_agents, sworld))
             scn = shard.scn
+            n_own = int(shard.owned.sum())
+            if share > 1:
+                # one rank alone: no other rank fills the ghosts' exchange slots, so the share
+                # solves its ghosts' x-steps itself, on the component's second wave (a tile's two
+                # agents run on its two waves at once) -- the pair QPs see the positions the
+                # owners would send; the exchange stays (X, device copy, Z + X per iteration)
+                shard = dataclasses.replace(shard, owned=np.ones_like(shard.owned))
         else:
             scn = pdist.shard(full, srank, sworld)
     else:
         scn = make_scenario(wl, n_steps, rank)
     from piadmm.solver import device_count
+    if share > 1:
+        # a rank of a multi-rank job decides the natural stop on the device after an all-reduce
+        # per outer iteration (devstop_step), never in a single-rank cooperative launch
+        os.environ["PIADMM_NO_COOP"] = "1"
     solver = PI_ADMM_MI355X(cfg, scn, device=local_rank % max(device_count(), 1), shard=shard)
     try:
         if dist is not None and os.environ.get("PIADMM_BENCH_TRANSPORT") == "host":
@@ -241,7 +254,7 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
             dist.barrier()
         cnt = solver.counters()
         spl, C = solver.steps_per_launch(), max(solver.C, 1)
-        N = int(shard.owned.sum()) if shard is not None else solver.N
+        N = n_own if shard is not None else solver.N
         # pairs across ranks (an X and a Z launch per outer iteration), or one component split over
         # workgroups (the same two launches, no exchange)
         xchg = (shard is not None and shard.n_slots > 0) or wl.get("kind") == "chain"
@@ -256,7 +269,11 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
     # step-kernel launches in the timed region: one persistent launch per steps_per_launch() steps,
     # or (natural termination across ranks) one per outer iteration plus one per step, or (pairs
     # across ranks) an X and a Z launch per outer iteration plus one per step
-    if xchg:
+    if xchg and shard is not None and not natural:
+        # fixed iterations of a sharded job: X(0), a fused Z(it) + X(it+1) launch per iteration,
+        # Z(M-1), the step's last launch (piadmm_capi.cpp run_steps_phases)
+        n_launch = K * (M + 1) + K
+    elif xchg:
         n_launch = 2 * int(job_iters) + K
     else:
         n_launch = -(-K // spl) if spl > 1 else int(job_iters) + K

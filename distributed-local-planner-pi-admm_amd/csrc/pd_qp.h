@@ -58,6 +58,8 @@ struct QP {
   int tstep;              // MPC step index (warm-set bookkeeping)
   int pre_m = -1;         // pair: rows of the stored active set already appended (gi_solve prebuild), -1: none
   int pre_wbits = 0;
+  double* wide = nullptr; // pair: HBM scratch of the wide dual active set (gi_solve_wide), nullptr: none
+  bool gi_full = false;   // pair: the last gi_solve stopped at its working-set capacity
   float* t32 = nullptr;   // x-step, precision 2 (tables in HBM): fp32 copies of the UNFOLDED G (H x H) and
                           // X' (H rows, stride XLDG) -- the hit path's tables, refined once in fp64
 
@@ -1333,6 +1335,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   ldsd* vbl = lds_ptr(vbuf);
   double* Y = P.Y;
   const int cap = min(P.mmax - 1, P.ycap);
+  P.gi_full = false;
   if (P.y_in_k) P.kready = false;  // Y overwrites the K_s^-1 region
   if (l == 0) P.fstate[0] = -1;    // and S^-1 the cached PDAS factor
   P.csig = -1;                     // (x-step: the factor scratch the parametric tables were built in)
@@ -1721,6 +1724,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       if (t2 <= t1) {
         if (m >= cap) {
           GI_DBG("GI fail: full m=%d cap=%d\n", m, cap);
+          P.gi_full = true;
           fail_labels();
           return false;
         }
@@ -1780,6 +1784,390 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     }
     wsync();
   }
+  return true;
+}
+
+// ---- Wide dual active set: pair QPs whose working set outgrows one row per lane (saturated
+// coupled pairs at H > 31: both vehicles' controls and rates at their bounds plus the hinge
+// kinks, 78-79 active rows at H = 40-50 on the 4-vehicle crossings).  The same Goldfarb-Idnani
+// method as gi_solve, cold-started, with two active rows per lane (rows a and a + 64 on lane
+// a & 63): the multipliers and codes in registers, S^-1 (up to 126 x 126, symmetric, stored
+// full) and the Y columns P^-1 n_a in the pair's HBM scratch (L2-resident), the broadcast
+// operands in the wave's LDS factor region (free: S^-1 is in HBM).  Certified by kkt_check.
+// (GIW_LD, GIW_CAP, giw_stride: piadmm_internal.h -- the host sizes the scratch)
+constexpr int GIW_MAX_STEPS = 4096;
+__device__ __forceinline__ bool gi_solve_wide(QP<2>& P, signed char* lab, double* x, double* y, int& nsteps) {
+  constexpr int NV = 2, NR = QP<2>::NR;
+  const int l = lid(), H = P.H, H2 = NV * H;
+  gbld* S = gbl_ptr(P.wide);
+  gbld* Yg = gbl_ptr(P.wide + (size_t)GIW_LD * GIW_LD);
+  ldsd* B = lds_ptr(P.fac);                  // 128-double broadcast operand
+  double* vb_ax = P.vb + 192;                // (A v) by row id, as gi_solve
+  const int cap = min(GIW_CAP, H2);          // at most n independent rows
+  if (l == 0) P.fstate[0] = -1;              // the LDS factor region is overwritten
+  P.csig = -1;
+  double x0[NV], xc[NV];
+  int m = 0, wbits = 0;
+  double ua[2] = {0.0, 0.0};                 // multipliers of active rows l, l + 64
+  int wc[2] = {0, 0};                        // their codes 2*row + side
+  bool lin = false;                          // this lane's hinge row in its linear regime
+  auto start = [&]() {
+    double qt[NV] = {P.q[0], P.q[1]};
+    const double tt = Tt_apply((P.valid(4) && lin) ? 1.0 : 0.0);
+    if (l < H) {
+      qt[0] -= P.beta * P.g1 * tt;
+      qt[1] -= P.beta * P.g2 * tt;
+    }
+    gemv_sym<true>(P, P.Pinv, qt, x0);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xc[v] = x0[v] = -x0[v];
+  };
+  // B[a] = v_a over the active rows (0 beyond m, up to 127)
+  auto put2 = [&](double v0, double v1) {
+    B[l] = (l < m) ? v0 : 0.0;
+    B[WAVE + l] = (WAVE + l < m) ? v1 : 0.0;
+    wsync();
+  };
+  // r = S^-1 v: lane owns columns l and l + 64
+  auto sinv2 = [&](double v0, double v1, double* r) {
+    put2(v0, v1);
+    const int mu = unif(m);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cl = l + h * WAVE;
+      const gbld* col = S + ((cl < mu) ? cl : 0);
+      double a0 = 0.0, a1 = 0.0;
+      if (h * WAVE < mu) {
+        for (int j0 = 0; j0 < mu; j0 += SINV_U) {
+          double sv[SINV_U], bv[SINV_U];
+#pragma unroll
+          for (int u = 0; u < SINV_U; ++u) {
+            sv[u] = col[unif(min(j0 + u, mu - 1) * GIW_LD)];
+            bv[u] = B[j0 + u];
+          }
+#pragma unroll
+          for (int u = 0; u < SINV_U; u += 2) {
+            a0 += sv[u] * bv[u];
+            a1 += sv[u + 1] * bv[u + 1];
+          }
+        }
+      }
+      r[h] = (cl < mu) ? a0 + a1 : 0.0;
+    }
+    wsync();
+  };
+  // z[v] -= sum_a c_a Y[a][v]
+  auto yaxpy2 = [&](double c0, double c1, double* z) {
+    put2(c0, c1);
+    const int mu = unif(m);
+    const int lc = (l < H) ? l : 0;
+    for (int a0 = 0; a0 < mu; a0 += SINV_U) {
+      double yv[SINV_U][NV], cv[SINV_U];
+#pragma unroll
+      for (int u = 0; u < SINV_U; ++u) {
+        const int a = unif(min(a0 + u, mu - 1));
+        cv[u] = B[a0 + u];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) yv[u][v] = Yg[unif(a * H2 + v * H) + lc];
+      }
+#pragma unroll
+      for (int u = 0; u < SINV_U; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) z[v] -= cv[u] * yv[u][v];
+    }
+    wsync();
+  };
+  auto prep = [&](int pc, double* yp) -> double {
+    const int prow = pc >> 1;
+    const double sgp = (pc & 1) ? -1.0 : 1.0;
+    pinv_row(P, prow, sgp, yp);
+    double ay[NR];
+    A_mul(P, yp, ay);
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ay[s];
+    }
+    wsync();
+    return sgp * vb_ax[prow];
+  };
+  auto nvec = [&](double* va) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool in = l + h * WAVE < m;
+      const int c = in ? wc[h] : 0;
+      va[h] = in ? ((c & 1) ? -1.0 : 1.0) * vb_ax[c >> 1] : 0.0;
+    }
+  };
+  auto append = [&](int pc, const double* yp, const double* r, double delta, double u0) {
+    const int prow = pc >> 1, ps = prow / H, pk = prow - ps * H;
+    const double id = 1.0 / delta;
+    put2(r[0], r[1]);
+    const int mu = unif(m);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cl = l + h * WAVE;
+      if (cl < mu) {
+        const double rl = r[h] * id;
+        gbld* col = S + cl;
+        for (int j0 = 0; j0 < mu; j0 += SINV_U) {
+          double sv[SINV_U], rv[SINV_U];
+#pragma unroll
+          for (int u = 0; u < SINV_U; ++u) {
+            sv[u] = col[unif(min(j0 + u, mu - 1) * GIW_LD)];
+            rv[u] = B[j0 + u];
+          }
+#pragma unroll
+          for (int u = 0; u < SINV_U; ++u)
+            if (j0 + u < mu) col[unif((j0 + u) * GIW_LD)] = sv[u] + rv[u] * rl;
+        }
+        S[mu * GIW_LD + cl] = -rl;      // row m, column cl
+        S[cl * GIW_LD + mu] = -rl;      // row cl, column m
+      }
+    }
+    if (l == (mu & (WAVE - 1))) {
+      S[mu * GIW_LD + mu] = id;
+      if (mu < WAVE) { ua[0] = u0; wc[0] = pc; }
+      else { ua[1] = u0; wc[1] = pc; }
+    }
+    if (l < H) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) Yg[mu * H2 + v * H + l] = yp[v];
+    }
+    if (l == pk) wbits |= 1 << (2 * ps + (pc & 1));
+    ++m;
+    gsync();
+  };
+  auto drop = [&](int k) {
+    const int kh = k >> 6, kl = k & (WAVE - 1);
+    const int kc = rdli(kh ? wc[1] : wc[0], kl);
+    if (l == (kc >> 1) % H) wbits &= ~(1 << (2 * ((kc >> 1) / H) + (kc & 1)));
+    const int mu = unif(m);
+    double c[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cl = l + h * WAVE;
+      c[h] = (cl < mu) ? S[k * GIW_LD + cl] : 0.0;   // column k (symmetric)
+    }
+    const double d = rdl(kh ? c[1] : c[0], kl);
+    put2(c[0], c[1]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cl = l + h * WAVE;
+      if (cl < mu && cl != k) {
+        const double cf = c[h] / d;
+        gbld* col = S + cl;
+        for (int j0 = 0; j0 < mu; j0 += SINV_U) {
+          double sv[SINV_U], bv[SINV_U];
+#pragma unroll
+          for (int u = 0; u < SINV_U; ++u) {
+            sv[u] = col[unif(min(j0 + u, mu - 1) * GIW_LD)];
+            bv[u] = B[j0 + u];
+          }
+#pragma unroll
+          for (int u = 0; u < SINV_U; ++u)
+            if (j0 + u < mu) col[unif((j0 + u) * GIW_LD)] = sv[u] - bv[u] * cf;
+        }
+      }
+    }
+    gsync();
+    const int last = mu - 1;
+    if (k != last) {
+      // row last -> row k (column k takes the diagonal of last), then column last -> column k
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int cl = l + h * WAVE;
+        if (cl < last) S[k * GIW_LD + cl] = S[last * GIW_LD + (cl == k ? last : cl)];
+      }
+      gsync();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int cl = l + h * WAVE;
+        if (cl < last && cl != k) S[cl * GIW_LD + k] = S[cl * GIW_LD + last];
+      }
+      const int lh = last >> 6, ll = last & (WAVE - 1);
+      const int clast = rdli(lh ? wc[1] : wc[0], ll);
+      const double ulast = rdl(lh ? ua[1] : ua[0], ll);
+      if (l < H) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) Yg[k * H2 + v * H + l] = Yg[last * H2 + v * H + l];
+      }
+      if (l == kl) {
+        if (kh) { wc[1] = clast; ua[1] = ulast; }
+        else { wc[0] = clast; ua[0] = ulast; }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (l + h * WAVE >= last) ua[h] = 0.0;
+    --m;
+    gsync();
+  };
+  // multipliers of the equality-constrained minimiser on the active set: lam = S^-1 (N xv - b)
+  auto eqp_lam = [&](const double* xv, double* lam) {
+    double ax0[NR];
+    A_mul(P, xv, ax0);
+    if (l < H) {
+#pragma unroll
+      for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = ax0[s] - P.lo(s);
+    }
+    wsync();
+    double rhs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      rhs[h] = 0.0;
+      if (l + h * WAVE < m) {
+        const int myc = wc[h], rw = myc >> 1, rs = rw / H;
+        const double blo = P.hinge(rs) ? 0.0 : ((rs & 1) ? -P.dumax : -P.umax);
+        rhs[h] = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
+      }
+    }
+    sinv2(rhs[0], rhs[1], lam);
+  };
+  auto x_of = [&](const double* lam) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xc[v] = x0[v];
+    yaxpy2(lam[0], lam[1], xc);
+  };
+  // first active row (by index) among lanes where pred holds for row l (h = 0) or l + 64 (h = 1)
+  auto first_of = [&](bool p0, bool p1) -> int {
+    const unsigned long long b0 = __ballot(p0);
+    if (b0) return __ffsll(b0) - 1;
+    return WAVE + __ffsll(__ballot(p1)) - 1;
+  };
+
+  start();
+  while (true) {
+    // ---- most violated constraint outside the active set
+    double ax[NR];
+    A_mul(P, xc, ax);
+    double best = 0.0;
+    int code = -1;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      if (!P.valid(s)) continue;
+      const bool hl = P.hinge(s) && lin;
+      const double tp = P.tol * (1.0 + fabs(P.lo(s)));
+      if (!hl && !((wbits >> (2 * s)) & 1)) {
+        const double sv = ax[s] - P.lo(s);
+        if (sv < -tp && sv < best) { best = sv; code = 2 * (s * H + l); }
+      }
+      if ((hl || !P.hinge(s)) && !((wbits >> (2 * s + 1)) & 1)) {
+        const double sv = (hl ? P.lo(s) : P.hi(s)) - ax[s];
+        if (sv < -tp && sv < best) { best = sv; code = 2 * (s * H + l) + 1; }
+      }
+    }
+    const double bmin = wmin(best);
+    if (!(bmin < 0.0)) break;
+    const int pl = __ffsll((unsigned long long)__ballot(code >= 0 && best == bmin)) - 1;
+    const int pc = rdli(code, pl);
+    const int prow = pc >> 1, pside = pc & 1, ps = prow / H, pk = prow - ps * H;
+    const bool phinge = P.hinge(ps);
+    double sp = rdl(pside ? (phinge ? P.lo(ps) : P.hi(ps)) - ax[ps] : ax[ps] - P.lo(ps), pk);
+    double yp[NV];
+    const double spp = prep(pc, yp);
+    double up = 0.0;
+    while (true) {
+      if (++nsteps > GIW_MAX_STEPS) return false;
+      double va[2], r[2];
+      nvec(va);
+      sinv2(va[0], va[1], r);
+      double z[NV] = {yp[0], yp[1]};
+      yaxpy2(r[0], r[1], z);
+      const double lpp2 = spp - wsum(va[0] * r[0] + va[1] * r[1]);
+      const double t2 = (lpp2 > DEP_TOL * spp) ? -sp / lpp2 : INFINITY;
+      double tdrop[2], tcap[2];
+      bool hin[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool in = l + h * WAVE < m;
+        hin[h] = in && P.hinge((wc[h] >> 1) / H);
+        tdrop[h] = (in && r[h] > 0.0) ? ua[h] / r[h] : INFINITY;
+        tcap[h] = (hin[h] && r[h] < 0.0) ? (P.beta - ua[h]) / (-r[h]) : INFINITY;
+      }
+      const double t1 = wmin(fmin(tdrop[0], tdrop[1]));
+      const double tca = wmin(fmin(tcap[0], tcap[1]));
+      const double tc = fmin(tca, phinge ? P.beta - up : INFINITY);
+      const double t = fmin(t1, t2);
+      if (tc <= t) {
+        const bool entering = phinge && P.beta - up <= tca;
+        if (t2 < INFINITY) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) xc[v] += tc * z[v];
+          sp += tc * lpp2;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (l + h * WAVE < m) ua[h] -= tc * r[h];
+        up += tc;
+        if (entering) {
+          if (l == pk) lin = pside == 0;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) x0[v] += P.beta * yp[v];
+          break;
+        }
+        const int k = first_of(hin[0] && tcap[0] == tca, hin[1] && tcap[1] == tca);
+        const int kc = rdli((k >> 6) ? wc[1] : wc[0], k & (WAVE - 1)), krow = kc >> 1;
+        if (l == krow - 4 * H) lin = (kc & 1) == 0;
+        {
+          const int lc = (l < H) ? l : 0;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) x0[v] += P.beta * Yg[k * H2 + v * H + lc];
+        }
+        drop(k);
+        continue;
+      }
+      if (!(t < INFINITY)) return false;
+      if (t2 < INFINITY) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xc[v] += t * z[v];
+        sp += t * lpp2;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (l + h * WAVE < m) ua[h] -= t * r[h];
+      up += t;
+      if (t2 <= t1) {
+        if (m >= cap) return false;
+        append(pc, yp, r, lpp2, up);
+        break;
+      }
+      drop(first_of(l < m && tdrop[0] == t1, l + WAVE < m && tdrop[1] == t1));
+    }
+  }
+  // ---- the final active set's exact solution, three refinement steps, kernel multipliers
+  double lam[2];
+  eqp_lam(x0, lam);
+  x_of(lam);
+#pragma unroll 1
+  for (int rf = 0; rf < 3; ++rf) {
+    double dl[2];
+    eqp_lam(xc, dl);
+    yaxpy2(dl[0], dl[1], xc);
+    lam[0] += dl[0];
+    lam[1] += dl[1];
+  }
+  wsync();
+  if (l < H) {
+#pragma unroll
+    for (int s = 0; s < NR; ++s) vb_ax[s * H + l] = 0.0;
+  }
+  wsync();
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (l + h * WAVE < m) vb_ax[wc[h] >> 1] = (wc[h] & 1) ? -lam[h] : lam[h];
+  wsync();
+#pragma unroll
+  for (int v = 0; v < NV; ++v) x[v] = (l < H) ? xc[v] : 0.0;
+#pragma unroll
+  for (int s = 0; s < NR; ++s) {
+    const bool lo_in = (wbits >> (2 * s)) & 1, hi_in = (wbits >> (2 * s + 1)) & 1;
+    y[s] = (P.valid(s) && l < H && (lo_in || hi_in)) ? vb_ax[s * H + l] : 0.0;
+    if (P.hinge(s) && lin && P.valid(s)) y[s] = hi_in ? y[s] - P.beta : -P.beta;
+    if (P.hinge(s)) lab[s] = (lo_in || hi_in) ? HKINK : (lin ? HLINEAR : HZERO);
+    else lab[s] = lo_in ? LOWER : (hi_in ? UPPER : FREE);
+    if (!P.valid(s)) lab[s] = 0;
+  }
+  wsync();
   return true;
 }
 
@@ -1949,6 +2337,18 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         for (int s = 0; s < NR; ++s) lab[s] = glab[s];
         if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
         GI_DBG("  after pdas ok=%d\n", (int)ok);
+      } else if (TWO && P.gi_full && P.wide) {
+        // the working set outgrew one row per lane: the wide dual active set (two per lane;
+        // big mode only -- H > 32, where a pair QP's 2H variables can hold more than 63 rows)
+        if constexpr (NV == 2 && TWO) {
+          if (gi_solve_wide(P, glab, x, y, ngi)) {
+            signed char nl[NR];
+            ok = kkt_check(P, glab, x, y, nl);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < NR; ++s) lab[s] = ok ? glab[s] : clab[s];
+        if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 4 * PDAS_STEPS);
       } else {
         // GI stopped (typically a hinge multiplier at its cap beta: that hinge is linear at the
         // optimum, which the dual active set does not model): polish from its working set with

@@ -190,7 +190,8 @@ int allreduce(piadmm_ctx* h, const double* send, double* recv, size_t n) {
     HIPCHK(h, hipMemcpyAsync(recv, h->h_x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
     return 0;
   }
-  if (send != recv) HIPCHK(h, hipMemcpyAsync(recv, send, n * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+  if (send != recv && pd::launch_copy(recv, send, n, h->stream) != 0)
+    return fail(h, PIADMM_E_HIP, std::string("copy kernel: ") + hipGetErrorString(pd::g_launch_err));
   return 0;
 }
 
@@ -552,6 +553,11 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   rc |= dalloc(h, &A.xcache_rho, (size_t)N);
   rc |= dalloc(h, &A.ecache, E);
   rc |= dalloc(h, &A.gi_ws, E * (2 + pd::WAVE));
+  // the wide dual active set's scratch (pair working sets beyond 63 rows, H >= 32): one region
+  // per wave that solves pair QPs -- the graph kernel's GW waves, the fused kernel's pair wave
+  A.gi_wide_stride = pd::giw_stride(H);
+  if (E > 0 && A.pair_gi && 2 * H > pd::WAVE - 1)
+    rc |= dalloc(h, &A.gi_wide, C * (A.graph ? pd::GW : 1) * A.gi_wide_stride);
   rc |= dalloc(h, &A.gpart, (size_t)2 * C * 5);
   rc |= dalloc(h, &A.ghist, (size_t)h->step_cap * std::max(h->cfg.max_outer, 1) * 2);
   rc |= dalloc(h, &A.giters, (size_t)h->step_cap);
@@ -839,6 +845,15 @@ static int32_t global_iteration(piadmm_handle_t h, int32_t tk, int it, int& flag
   return PIADMM_OK;
 }
 
+// PIADMM_NO_ZX=1: a sharded job's fixed iterations as separate X and Z launches (A/B check)
+static bool no_zx() {
+  static const bool v = [] {
+    const char* e = std::getenv("PIADMM_NO_ZX");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // MPC steps of a job whose iterations are split into X and Z launches (a sharded graph with pairs
 // across ranks, or a component split over workgroups), one step at a time.  Fixed iterations: the
 // steps' residual histories are all-reduced ONCE for the n steps (n x 2 x max_outer doubles), the
@@ -856,6 +871,21 @@ static int32_t run_steps_phases(piadmm_handle_t h, int32_t t, int32_t n, bool sy
     }
     h->ghist.assign((size_t)2 * M, NAN);
     int flag = 0, nit = 0, nanlast = 0;
+    if (c.fixed_iters && h->xchg && !h->split && M > 1 && !no_zx()) {
+      // a sharded job's fixed iterations, one launch between two exchanges: X(0), then per
+      // iteration it the Z phase of it and the X phase of it+1 in ONE launch (a component is one
+      // workgroup: its x-steps read only its own pairs' hat / lam), then Z(M-1) -- M + 1 launches
+      // and M all-reduces per step instead of 2M launches
+      const size_t nx = (size_t)h->n_slots * 3 * (c.H + 1);
+      LAUNCH(h, launch_step(h->a, tk, 1, 0, 1, pd::F_FIRST | pd::F_GLOBAL | pd::F_XONLY, s));
+      if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
+      for (int it = 0; it + 1 < M; ++it) {
+        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 2, pd::F_GLOBAL | pd::F_ZONLY | pd::F_XONLY, s));
+        if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
+      }
+      LAUNCH(h, launch_step(h->a, tk, 1, M - 1, M, pd::F_GLOBAL | pd::F_ZONLY, s));
+      nit = M;
+    } else
     for (int it = 0; it < M; ++it) {
       nit = it + 1;
       if (c.fixed_iters) {
@@ -940,6 +970,21 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
     LAUNCH(h, pd::launch_pair_deff(h->a, s));
     h->ghist.assign((size_t)2 * M, NAN);
     int flag = 0, nit = 0, nanlast = 0;
+    if (c.fixed_iters && h->xchg && !h->split && M > 1 && !no_zx()) {
+      // a sharded job's fixed iterations, one launch between two exchanges: X(0), then per
+      // iteration it the Z phase of it and the X phase of it+1 in ONE launch (a component is one
+      // workgroup: its x-steps read only its own pairs' hat / lam), then Z(M-1) -- M + 1 launches
+      // and M all-reduces per step instead of 2M launches
+      const size_t nx = (size_t)h->n_slots * 3 * (c.H + 1);
+      LAUNCH(h, launch_step(h->a, tk, 1, 0, 1, pd::F_FIRST | pd::F_GLOBAL | pd::F_XONLY, s));
+      if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
+      for (int it = 0; it + 1 < M; ++it) {
+        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 2, pd::F_GLOBAL | pd::F_ZONLY | pd::F_XONLY, s));
+        if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
+      }
+      LAUNCH(h, launch_step(h->a, tk, 1, M - 1, M, pd::F_GLOBAL | pd::F_ZONLY, s));
+      nit = M;
+    } else
     for (int it = 0; it < M; ++it) {
       int stop = 0;
       if (int rc = global_iteration(h, tk, it, flag, nanlast, &stop)) return rc;

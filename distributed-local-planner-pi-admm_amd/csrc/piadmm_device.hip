@@ -21,6 +21,10 @@
 // tools/qp_sim.py and tools/gi_sim.py are the NumPy prototypes of this math.
 // Shared device code: pd_common.h (wave primitives, rollouts), pd_qp.h (QP solver), pd_setup.h.
 #include <hip/hip_cooperative_groups.h>
+#include <mutex>
+#include <tuple>
+#include <vector>
+#include <algorithm>
 
 #include "pd_setup.h"
 
@@ -557,6 +561,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     qe.y_in_k = true;
     qe.gws = A.gi_ws + (size_t)e * GI_WS;
     qe.gws_warm = A.pair_warm != 0;
+    qe.wide = A.gi_wide ? A.gi_wide + (size_t)blockIdx.x * A.gi_wide_stride : nullptr;
     qe.tstep = t;
     // Ke doubles as the H x 2H staging of the per-scenario pair tables; with fp32 images in
     // LDS mode the fp32 region (2H^2 doubles of space) takes that role
@@ -1178,9 +1183,7 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
   }
 #endif
   const void* fn = mpc_fn(big, a.tie_on != 0);
-  // the dynamic-LDS limit is a per-device function attribute: set it on every launch (cheap),
-  // so handles on several devices of one process each get it
-  if (launch_rc(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)) != 0) return -1;
+  if (set_dyn_lds(fn, sh) != 0) return -1;
   if (flags & F_COOP) {
     // every workgroup must be resident for the grid barrier: the cooperative launch fails
     // (and the caller falls back to host-decided termination) rather than deadlock
@@ -1214,6 +1217,34 @@ bool coop_fits(const DevArgs& a, int device) {
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return false;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NWT * WAVE, sh) != hipSuccess) return false;
   return (long long)per * ncu >= (long long)a.C;
+}
+
+// The dynamic-LDS limit is a per-device function attribute: set once per (kernel, device), and
+// again only for a larger size, so handles on several devices of one process each get it.
+int set_dyn_lds(const void* fn, size_t bytes) {
+  static std::mutex mu;
+  static std::vector<std::tuple<const void*, int, size_t>> done;
+  int dev = 0;
+  if (launch_rc(hipGetDevice(&dev)) != 0) return -1;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& d : done)
+    if (std::get<0>(d) == fn && std::get<1>(d) == dev && std::get<2>(d) >= bytes) return 0;
+  if (launch_rc(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes)) != 0) return -1;
+  done.emplace_back(fn, dev, bytes);
+  return 0;
+}
+
+__global__ void k_copy(double* __restrict__ dst, const double* __restrict__ src, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+int launch_copy(double* dst, const double* src, size_t n, hipStream_t s) {
+  if (n == 0 || dst == src) return 0;
+  const unsigned nb = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(k_copy, dim3(nb), dim3(256), 0, s, dst, src, n);
+  return launch_rc(hipGetLastError());
 }
 
 int launch_term_partials(const DevArgs& a, int it, double* out, hipStream_t s, int devstop) {

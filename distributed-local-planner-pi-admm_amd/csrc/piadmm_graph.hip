@@ -265,6 +265,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
   qe.y_in_k = W.ylds == nullptr;
   qe.gws = A.gi_ws + (size_t)e * GI_WS;
   qe.gws_warm = A.pair_warm != 0;
+  qe.wide = A.gi_wide ? A.gi_wide + ((size_t)blockIdx.x * GW + (threadIdx.x >> 6)) * A.gi_wide_stride : nullptr;
   qe.tstep = t;
   qe.csig = -1;
   if (l == 0) W.zfs[0] = -1;
@@ -582,6 +583,9 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   const bool coop = (flags & F_COOP) != 0;
   const bool xonly = (flags & F_XONLY) != 0;
   const bool zonly = (flags & F_ZONLY) != 0;
+  // both: iteration it0's Z phase, then iteration it0+1's X phase -- one launch between two
+  // exchanges (a sharded job's fixed iterations, piadmm_capi.cpp run_steps_phases)
+  const bool zx = xonly && zonly;
   bool nanlast = (flags & F_NANLAST) != 0;
   // a component whose step already ended in an earlier launch of this step (per-component stop,
   // host-stepped by piadmm_outer_iter) runs no further iteration
@@ -622,7 +626,6 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   GCnt n;
   int iters = skip ? A.iters[ci] : it0, gflag = 0;
   for (int it = it0; it < it_end; ++it) {
-    iters = it + 1;
     // -------- X: x-steps of the component's agents (casadi/main.py:81-106)
     if (!(zonly && it == it0)) {
       unsigned long long t_xp = STAMP_T();
@@ -635,7 +638,8 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       __syncthreads();
       STAMP_ADD(ST_SYNC_A, t_sa);
     }
-    if (xonly) break;
+    if (xonly && !(zx && it == it0)) break;
+    iters = it + 1;
     // -------- ghosts (sharded job): the positions and controls their owner rank computed in this
     // iteration's X phase, from the all-reduced exchange buffer (piadmm_capi.cpp run_steps)
     if (A.xrecv) {
@@ -824,16 +828,16 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long* cn = A.counters + (size_t)ci * 8;
-    if (!xonly && !skip) cn[0] += (unsigned long long)(iters - it0);
+    if ((!xonly || zx) && !skip) cn[0] += (unsigned long long)(iters - it0);
     for (int k = 0; k < 7; ++k) {
       unsigned long long sum = 0;
       for (int ww = 0; ww < GW; ++ww) sum += (unsigned long long)s_cnt[ww][k];
       cn[k + 1] += sum;
     }
-    if (!xonly) A.iters[ci] = iters;
+    if (!xonly || zx) A.iters[ci] = iters;
     A.cst[(size_t)ci * 4 + 0] = flag;
     A.cst[(size_t)ci * 4 + 1] = aliased;
-    if (!xonly) A.cst[(size_t)ci * 4 + 3] = stopped ? 1 : 0;
+    if (!xonly || zx) A.cst[(size_t)ci * 4 + 3] = stopped ? 1 : 0;
     if (coop && ci == 0) A.giters[slot] = iters;
     if (nanlast && iters > 0 && !skip) {
       resid[2 * (iters - 1) + 0] = NAN;
@@ -951,7 +955,7 @@ int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int
 #endif
   const bool big = a.cfg.H > HMAX;
   const void* fn = graph_fn(big, a.tie_on != 0);
-  if (launch_rc(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)) != 0) return -1;
+  if (set_dyn_lds(fn, sh) != 0) return -1;
   if (flags & F_COOP) {
     DevArgs aa = a;
     void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};

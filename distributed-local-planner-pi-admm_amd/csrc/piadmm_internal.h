@@ -12,6 +12,14 @@ inline int launch_rc(hipError_t e) {
   return e == hipSuccess ? 0 : -1;
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, size, device) rather than on
+// every launch: the split / exchange paths launch several kernels per outer iteration.
+int set_dyn_lds(const void* fn, size_t bytes);
+
+// dst[0:n) = src[0:n) on stream s, as a kernel on the compute queue (the single-rank stand-in of
+// an all-reduce: no DMA-engine hand-off between two compute launches).
+int launch_copy(double* dst, const double* src, size_t n, hipStream_t s);
+
 
 constexpr int WAVE = 64;
 constexpr int NW = 2;        // agent waves per workgroup of k_mpc_step = agents per component (max)
@@ -92,6 +100,8 @@ struct DevArgs {
   double* xcache_rho;       // N   penalty of the cached agent setup (NaN: none)
   int* ecache;              // E   1 when the pair's speed-only tables are built
   int* gi_ws;               // E*(2+64) the pair's last dual active set: m, step t, codes
+  double* gi_wide;          // H >= 32: C * (GW | 1) * giw_stride(H) wide dual active-set scratch
+  size_t gi_wide_stride;    // giw_stride(H)
   double* gpart;            // 2*C*5 coop: per-component termination partials (iteration parity)
   double* ghist;            // step_cap*max_outer*2 coop: global (rk, sk) history per step
   int* giters;              // step_cap coop: global outer iterations per step
@@ -197,6 +207,15 @@ constexpr int F_COOP = 16;    // global termination decided in-kernel (cooperati
 
 // Graph mode: LDS per workgroup of k_graph_step (GW waves, one component per workgroup).
 constexpr int GW = 2;
+// The wide dual active set of pair QPs (pd_qp.h gi_solve_wide): working sets up to 126 rows
+// (two per lane), S^-1 (stride GIW_LD) and the Y columns (2H doubles each) in HBM scratch, one
+// region per solving wave (graph kernel: GW per workgroup; fused kernel: its pair wave).  Only
+// H >= 32 can outgrow the 63-row capacity (a pair QP has 2H variables).
+constexpr int GIW_LD = 2 * WAVE;
+constexpr int GIW_CAP = 2 * WAVE - 2;
+inline __host__ __device__ constexpr size_t giw_stride(int H) {
+  return (size_t)GIW_LD * GIW_LD + (size_t)GIW_LD * 2 * H;
+}
 constexpr int GZMAX = 1024;   // pairs per component whose colliding pairs are balanced over the waves
 // Dual active-set columns P^-1 n_a in LDS per wave (H <= HMAX; beyond, in HBM): the pair's
 // 2H-long columns (63 of them) or the x-step's H-long ones, in turn.
