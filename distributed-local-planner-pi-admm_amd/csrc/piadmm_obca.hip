@@ -18,7 +18,7 @@
 // oracle/obca_oracle.py (solve_local, gi_qp) is the same algorithm statement by statement;
 // tests/test_gpu_obca.py holds the two to each other and certifies the answers as KKT points.
 //
-// Layout: one workgroup = one wavefront (64 lanes) = one problem; the whole SQP state (~62 KB)
+// Layout: one workgroup = one wavefront (64 lanes) = one problem; the SQP state (~39 KB)
 // lives in LDS; lanes split stage-wise work (7 stages) and matrix work (28 x 28) among them.
 // HBM traffic per problem: 296 doubles in, 224 doubles + 3 ints out -- the kernel is latency
 // bound (barrier chains of the factorisations and the active-set updates), not HBM bound.
@@ -64,12 +64,9 @@ struct Ws {
   double Xn[NH][NX], Un[NT][NU], Ln[NT][NL];
   double ya[NT], yb[NT][2], yn[NT], yx[NT][NX], pi[NT][NX], yu[NUV], yl[NT][NL];
   double nya[NT], nyb[NT][2], nyn[NT], nyx[NT][NX], npi[NT][NX], nyu[NUV], nyl[NT][NL];
-  // linearisation
-  double A[NT][NX][NX], F[NT][NX], Wd[NT][NX][NX];
-  double Wxx[NH][NX][NX], Wxl[NH][NX][NL], Wll[NH][NL][NL];
-  double gX[NH][NX], gL[NT][NL];
-  double ga_v[NT], ga_g[NT][9], gb_v[NT][2], gb_J[NT][2][9], gn_v[NT], gn_g[NT][NL];
-  double sv[NH][NX];
+  // linearisation (the blocks read in the condensing / assembly and the multiplier recovery
+  // only live in HBM: WsG)
+  double ga_v[NT], gb_v[NT][2], gn_v[NT], gn_g[NT][NL];
   // [dX_t; dLam_t] = K_t z + k0_t with z = (dU, zeta) and K_t = [[T_t, 0], [-pmv_t (x) T_t[3], N_t]]
   // (N_t = the null space of dm/dLam at zeta block t): K is never stored
   double T[NT][NX][NUV];      // dX_t = T_t dU + s_t  (stage t = index + 1)
@@ -89,7 +86,19 @@ struct Ws {
   int flag;
 };
 
-static_assert(sizeof(Ws) <= 160 * 1024, "OBCA workspace exceeds the LDS of one CU");
+// The linearisation blocks of one problem, in HBM (L2 / L1-resident): read by the condensing, the
+// Hessian assembly and the multiplier recovery of each SQP iteration, never inside the QP's
+// active-set loop.  Off the LDS workspace they take it from ~48 KB to ~39 KB per problem, so four
+// problems (one wave each) share a CU's 160 KB -- one per SIMD -- instead of three.
+struct WsG {
+  double A[NT][NX][NX], F[NT][NX], Wd[NT][NX][NX];
+  double Wxx[NH][NX][NX], Wxl[NH][NX][NL], Wll[NH][NL][NL];
+  double gX[NH][NX], gL[NT][NL];
+  double ga_g[NT][9], gb_J[NT][2][9];
+  double sv[NH][NX];
+};
+
+static_assert(sizeof(Ws) <= 160 * 1024 / 4, "OBCA workspace: four problems per CU");
 
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
@@ -343,8 +352,8 @@ __device__ double row_elem(const Ws& S, int c, int k) {
 __device__ __forceinline__ double gval(const Ws& S, int ti, int i, int a) {
   return (i < 5) ? S.T[ti][i][a] : -S.pmv[ti][i - 5] * S.T[ti][3][a];
 }
-__device__ __forceinline__ double wval(const Ws& S, int t, int i, int j) {
-  return (i < 5) ? (j < 5 ? S.Wxx[t][i][j] : S.Wxl[t][i][j - 5]) : (j < 5 ? S.Wxl[t][j][i - 5] : S.Wll[t][i - 5][j - 5]);
+__device__ __forceinline__ double wval(const WsG& Q, int t, int i, int j) {
+  return (i < 5) ? (j < 5 ? Q.Wxx[t][i][j] : Q.Wxl[t][i][j - 5]) : (j < 5 ? Q.Wxl[t][j][i - 5] : Q.Wll[t][i - 5][j - 5]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -636,12 +645,13 @@ __device__ int gi_solve(Ws& S, int& steps) {
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs, int n,
                                                  double* __restrict__ out, int* __restrict__ ist,
-                                                 unsigned long long* __restrict__ stamps) {
+                                                 unsigned long long* __restrict__ stamps, WsG* __restrict__ qg) {
   __shared__ Ws S;
   OST_DECL
   const int lane = threadIdx.x;
   const int pb = blockIdx.x;
   if (pb >= n) return;
+  WsG& Q = qg[pb];
   const double* rec = recs + (size_t)pb * REC;
 
   // ---- load the record, derive w_t = A_o' lamb_ij, c_t = b_o' lamb_ij ----
@@ -701,15 +711,15 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       Dyn D;
       dyn_eval(S.X[k], S.U[k], D);
       for (int i = 0; i < 5; ++i) {
-        S.F[k][i] = D.F[i];
-        for (int j = 0; j < 5; ++j) { S.A[k][i][j] = D.A[i][j]; S.Wd[k][i][j] = 0.0; }
+        Q.F[k][i] = D.F[i];
+        for (int j = 0; j < 5; ++j) { Q.A[k][i][j] = D.A[i][j]; Q.Wd[k][i][j] = 0.0; }
       }
       const int fi[3] = {0, 1, 3};
       for (int a = 0; a < 3; ++a)
         for (int b = 0; b < 3; ++b) {
           double s = 0.0;
           for (int f = 0; f < 3; ++f) s += S.pi[k][fi[f]] * D.Hf[f][a][b];
-          S.Wd[k][2 + a][2 + b] = DT * s;
+          Q.Wd[k][2 + a][2 + b] = DT * s;
         }
     }
     SYNC();
@@ -719,18 +729,18 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       const double* Xt = S.X[t];
       const double* Lt = S.L[t - 1];
       for (int i = 0; i < 5; ++i)
-        S.gX[t][i] = 2 * S.qq * (Xt[i] - S.ref[t][i]) + S.lb[t - 1][i] + S.rho * (Xt[i] - S.zb[t - 1][i]);
-      for (int i = 0; i < 4; ++i) S.gL[t - 1][i] = S.lb[t - 1][5 + i] + S.rho * (Lt[i] - S.zb[t - 1][5 + i]);
+        Q.gX[t][i] = 2 * S.qq * (Xt[i] - S.ref[t][i]) + S.lb[t - 1][i] + S.rho * (Xt[i] - S.zb[t - 1][i]);
+      for (int i = 0; i < 4; ++i) Q.gL[t - 1][i] = S.lb[t - 1][5 + i] + S.rho * (Lt[i] - S.zb[t - 1][5 + i]);
       Geo G;
       geo(Xt, Lt, S.prob, S.sig_delay, G);
       double ga[9];
       S.ga_v[t - 1] = ga_val_grad(G, Lt, S.c[t - 1], ga);
-      for (int i = 0; i < 9; ++i) S.ga_g[t - 1][i] = ga[i];
+      for (int i = 0; i < 9; ++i) Q.ga_g[t - 1][i] = ga[i];
       for (int r = 0; r < 2; ++r) {
         S.gb_v[t - 1][r] = G.m[r] + S.w[t - 1][r];
-        for (int i = 0; i < 9; ++i) S.gb_J[t - 1][r][i] = 0.0;
-        S.gb_J[t - 1][r][3] = G.mt[r];
-        for (int j = 0; j < 4; ++j) S.gb_J[t - 1][r][5 + j] = G.mL[r][j];
+        for (int i = 0; i < 9; ++i) Q.gb_J[t - 1][r][i] = 0.0;
+        Q.gb_J[t - 1][r][3] = G.mt[r];
+        for (int j = 0; j < 4; ++j) Q.gb_J[t - 1][r][5 + j] = G.mL[r][j];
       }
       double a1 = Lt[0] - Lt[2], a2 = Lt[1] - Lt[3];
       S.gn_v[t - 1] = a1 * a1 + a2 * a2;
@@ -750,15 +760,15 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       const double Hn[4][4] = {{2, 0, -2, 0}, {0, 2, 0, -2}, {-2, 0, 2, 0}, {0, -2, 0, 2}};
       for (int i = 0; i < 5; ++i)
         for (int j = 0; j < 5; ++j)
-          S.Wxx[t][i][j] = (t < NH - 1 ? S.Wd[t][i][j] : 0.0) + (i == j ? 2 * S.qq + S.rho : 0.0) + H[i][j];
+          Q.Wxx[t][i][j] = (t < NH - 1 ? Q.Wd[t][i][j] : 0.0) + (i == j ? 2 * S.qq + S.rho : 0.0) + H[i][j];
       for (int i = 0; i < 5; ++i)
-        for (int j = 0; j < 4; ++j) S.Wxl[t][i][j] = H[i][5 + j];
+        for (int j = 0; j < 4; ++j) Q.Wxl[t][i][j] = H[i][5 + j];
       for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) S.Wll[t][i][j] = (i == j ? S.rho : 0.0) + H[5 + i][5 + j] - yn * Hn[i][j];
+        for (int j = 0; j < 4; ++j) Q.Wll[t][i][j] = (i == j ? S.rho : 0.0) + H[5 + i][5 + j] - yn * Hn[i][j];
     }
     OST(ST_LIN);
     // ---- condense: T_t, s_t ----
-    if (lane < NX) S.sv[0][lane] = S.init[lane] - S.X[0][lane];
+    if (lane < NX) Q.sv[0][lane] = S.init[lane] - S.X[0][lane];
     SYNC();
     for (int k = 0; k < NT; ++k) {
       // T_{k+1} = A_k T_k + B_k E_k  (T_0 = 0); index k holds T_{k+1}
@@ -766,15 +776,15 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
         int i = e / NUV, j = e % NUV;
         double s = 0.0;
         if (k > 0)
-          for (int m = 0; m < NX; ++m) s += S.A[k][i][m] * S.T[k - 1][m][j];
+          for (int m = 0; m < NX; ++m) s += Q.A[k][i][m] * S.T[k - 1][m][j];
         if (j == 2 * k && i == 2) s += DT;
         if (j == 2 * k + 1 && i == 4) s += DT;
         S.T[k][i][j] = s;
       }
       if (lane < NX) {
         double s = 0.0;
-        for (int m = 0; m < NX; ++m) s += S.A[k][lane][m] * S.sv[k][m];
-        S.sv[k + 1][lane] = s + S.F[k][lane] - S.X[k + 1][lane];
+        for (int m = 0; m < NX; ++m) s += Q.A[k][lane][m] * Q.sv[k][m];
+        Q.sv[k + 1][lane] = s + Q.F[k][lane] - S.X[k + 1][lane];
       }
       SYNC();
     }
@@ -782,18 +792,18 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
     if (lane < NT) {
       int ti = lane;
       double P[4][2], pm[4], pr[4];
-      double mth0 = S.gb_J[ti][0][3], mth1 = S.gb_J[ti][1][3];
+      double mth0 = Q.gb_J[ti][0][3], mth1 = Q.gb_J[ti][1][3];
       double r0 = -S.gb_v[ti][0], r1 = -S.gb_v[ti][1];
-      double s3 = S.sv[ti + 1][3];
+      double s3 = Q.sv[ti + 1][3];
       for (int i = 0; i < 4; ++i) {
-        P[i][0] = 0.5 * S.gb_J[ti][0][5 + i];
-        P[i][1] = 0.5 * S.gb_J[ti][1][5 + i];
+        P[i][0] = 0.5 * Q.gb_J[ti][0][5 + i];
+        P[i][1] = 0.5 * Q.gb_J[ti][1][5 + i];
         S.Pm[ti][i][0] = P[i][0];
         S.Pm[ti][i][1] = P[i][1];
         pm[i] = P[i][0] * mth0 + P[i][1] * mth1;
         pr[i] = P[i][0] * (r0 - mth0 * s3) + P[i][1] * (r1 - mth1 * s3);
       }
-      for (int i = 0; i < 5; ++i) S.k0[ti][i] = S.sv[ti + 1][i];
+      for (int i = 0; i < 5; ++i) S.k0[ti][i] = Q.sv[ti + 1][i];
       for (int i = 0; i < 4; ++i) S.k0[ti][5 + i] = pr[i];
       for (int i = 0; i < 4; ++i) S.pmv[ti][i] = pm[i];
     }
@@ -814,17 +824,17 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
         int i = e >> 4, a = e & 15;
         double v = 0.0;
         if (a < NUV) {
-          for (int j = 0; j < 9; ++j) v += wval(S, t, i, j) * gval(S, ti, j, a);
+          for (int j = 0; j < 9; ++j) v += wval(Q, t, i, j) * gval(S, ti, j, a);
         } else {
           int c = a - NUV;
-          v = wval(S, t, i, 5 + c) + wval(S, t, i, 7 + c);
+          v = wval(Q, t, i, 5 + c) + wval(Q, t, i, 7 + c);
         }
         S.R[i][a] = v;
       }
       if (lane >= 48 && lane < 57) {
         int i = lane - 48;
-        double v = (i < 5) ? S.gX[t][i] : S.gL[ti][i - 5];
-        for (int j = 0; j < 9; ++j) v += wval(S, t, i, j) * S.k0[ti][j];
+        double v = (i < 5) ? Q.gX[t][i] : Q.gL[ti][i - 5];
+        for (int j = 0; j < 9; ++j) v += wval(Q, t, i, j) * S.k0[ti][j];
         S.dd[i] = v;
       }
       SYNC();
@@ -870,11 +880,11 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       int ti = e / NZ, a = e % NZ;
       double sa = 0.0, sn = 0.0;
       if (a < NUV) {
-        for (int i = 0; i < 9; ++i) sa += S.ga_g[ti][i] * gval(S, ti, i, a);
+        for (int i = 0; i < 9; ++i) sa += Q.ga_g[ti][i] * gval(S, ti, i, a);
         for (int j = 0; j < 4; ++j) sn += S.gn_g[ti][j] * gval(S, ti, 5 + j, a);
       } else if (((a - NUV) >> 1) == ti) {
         int c = (a - NUV) & 1;
-        sa = S.ga_g[ti][5 + c] + S.ga_g[ti][7 + c];
+        sa = Q.ga_g[ti][5 + c] + Q.ga_g[ti][7 + c];
         sn = S.gn_g[ti][c] + S.gn_g[ti][2 + c];
       }
       S.garow[ti][a] = sa;
@@ -897,7 +907,7 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
           dv = (r & 1) ? base - hi[j] : lo[j] - base;
         } else if (r <= 11) {
           double base = S.ga_v[ti];
-          for (int i = 0; i < 9; ++i) base += S.ga_g[ti][i] * S.k0[ti][i];
+          for (int i = 0; i < 9; ++i) base += Q.ga_g[ti][i] * S.k0[ti][i];
           dv = (r == 10) ? S.min_dis - base : base - GA_MAX;
         } else if (r == 12) {
           double base = S.gn_v[ti];
@@ -990,7 +1000,7 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
     }
     // ---- step in the full space ----
     if (lane < NUV) (&S.dU[0][0])[lane] = S.x[lane];
-    if (lane < NX) S.dX[0][lane] = S.sv[0][lane];
+    if (lane < NX) S.dX[0][lane] = Q.sv[0][lane];
     for (int e = lane; e < NT * 9; e += 64) {
       int ti = e / 9, i = e % 9;
       int ir = (i < 5) ? i : 3;
@@ -1014,10 +1024,10 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
       int ti = lane, t = ti + 1;
       double resL[4];
       for (int i = 0; i < 4; ++i) {
-        double s = S.gL[ti][i];
-        for (int j = 0; j < 5; ++j) s += S.Wxl[t][j][i] * S.dX[t][j];
-        for (int j = 0; j < 4; ++j) s += S.Wll[t][i][j] * S.dL[ti][j];
-        s -= S.nya[ti] * S.ga_g[ti][5 + i] + S.nyn[ti] * S.gn_g[ti][i] + S.nyl[ti][i];
+        double s = Q.gL[ti][i];
+        for (int j = 0; j < 5; ++j) s += Q.Wxl[t][j][i] * S.dX[t][j];
+        for (int j = 0; j < 4; ++j) s += Q.Wll[t][i][j] * S.dL[ti][j];
+        s -= S.nya[ti] * Q.ga_g[ti][5 + i] + S.nyn[ti] * S.gn_g[ti][i] + S.nyl[ti][i];
         resL[i] = s;
       }
       for (int r = 0; r < 2; ++r) {
@@ -1031,13 +1041,13 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
     for (int t = NH - 1; t >= 1; --t) {
       if (lane < NX) {
         int i = lane, ti = t - 1;
-        double s = S.gX[t][i];
-        for (int j = 0; j < 5; ++j) s += S.Wxx[t][i][j] * S.dX[t][j];
-        for (int j = 0; j < 4; ++j) s += S.Wxl[t][i][j] * S.dL[ti][j];
-        s -= S.nya[ti] * S.ga_g[ti][i] + S.nyb[ti][0] * S.gb_J[ti][0][i] + S.nyb[ti][1] * S.gb_J[ti][1][i];
+        double s = Q.gX[t][i];
+        for (int j = 0; j < 5; ++j) s += Q.Wxx[t][i][j] * S.dX[t][j];
+        for (int j = 0; j < 4; ++j) s += Q.Wxl[t][i][j] * S.dL[ti][j];
+        s -= S.nya[ti] * Q.ga_g[ti][i] + S.nyb[ti][0] * Q.gb_J[ti][0][i] + S.nyb[ti][1] * Q.gb_J[ti][1][i];
         s -= S.nyx[ti][i];
         if (t < NH - 1)
-          for (int j = 0; j < 5; ++j) s += S.A[t][j][i] * S.npi[t][j];
+          for (int j = 0; j < 5; ++j) s += Q.A[t][j][i] * S.npi[t][j];
         S.npi[ti][i] = s;
       }
       SYNC();
@@ -1074,9 +1084,9 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
     mu = fmax(mu, 1.01 * mm + 1e-6);
     double phi0 = f0 + mu * viol;
     double gd = 0.0;
-    for (int e = lane; e < NT * NX; e += 64) gd += (&S.gX[1][0])[e] * (&S.dX[1][0])[e];
+    for (int e = lane; e < NT * NX; e += 64) gd += (&Q.gX[1][0])[e] * (&S.dX[1][0])[e];
     if (lane < NUV) gd += 2 * S.rr * (&S.U[0][0])[lane] * (&S.dU[0][0])[lane];
-    if (lane < NT * NL) gd += (&S.gL[0][0])[lane] * (&S.dL[0][0])[lane];
+    if (lane < NT * NL) gd += (&Q.gL[0][0])[lane] * (&S.dL[0][0])[lane];
     gd = wsum(gd);
     double D = gd - mu * viol;
     double alpha = 1.0;
@@ -1154,6 +1164,7 @@ struct piadmm_obca_s {
   double* d_rec = nullptr;
   double* d_out = nullptr;
   int* d_ist = nullptr;
+  obca::WsG* d_qg = nullptr;   // per-problem linearisation blocks (HBM)
   unsigned long long* d_stamps = nullptr;
   int cap = 0, n = 0;
   std::string err;
@@ -1172,9 +1183,9 @@ int fail(piadmm_obca_t h, int code, const std::string& msg) {
 
 int ensure(piadmm_obca_t h, int n) {
   if (n <= h->cap) return 0;
-  if (h->d_rec) { (void)hipFree(h->d_rec); (void)hipFree(h->d_out); (void)hipFree(h->d_ist); }
+  if (h->d_rec) { (void)hipFree(h->d_rec); (void)hipFree(h->d_out); (void)hipFree(h->d_ist); (void)hipFree(h->d_qg); }
   if (h->d_stamps) (void)hipFree(h->d_stamps);
-  h->d_rec = nullptr; h->d_out = nullptr; h->d_ist = nullptr; h->d_stamps = nullptr; h->cap = 0;
+  h->d_rec = nullptr; h->d_out = nullptr; h->d_ist = nullptr; h->d_qg = nullptr; h->d_stamps = nullptr; h->cap = 0;
 #ifdef PIADMM_STAMPS
   OHIP(h, hipMalloc(&h->d_stamps, (size_t)n * obca::NSTAMP * sizeof(unsigned long long)));
   OHIP(h, hipMemset(h->d_stamps, 0, (size_t)n * obca::NSTAMP * sizeof(unsigned long long)));
@@ -1182,6 +1193,7 @@ int ensure(piadmm_obca_t h, int n) {
   OHIP(h, hipMalloc(&h->d_rec, (size_t)n * obca::REC * sizeof(double)));
   OHIP(h, hipMalloc(&h->d_out, (size_t)n * obca::OUT * sizeof(double)));
   OHIP(h, hipMalloc(&h->d_ist, (size_t)n * 3 * sizeof(int)));
+  OHIP(h, hipMalloc(&h->d_qg, (size_t)n * sizeof(obca::WsG)));
   h->cap = n;
   return 0;
 }
@@ -1199,7 +1211,7 @@ int check_recs(piadmm_obca_t h, const double* recs, int n) {
 
 int launch(piadmm_obca_t h) {
   hipLaunchKernelGGL(obca::k_obca_sqp, dim3(h->n), dim3(64), 0, h->stream, h->d_rec, h->n, h->d_out, h->d_ist,
-                     h->d_stamps);
+                     h->d_stamps, h->d_qg);
   OHIP(h, hipGetLastError());
   return 0;
 }
@@ -1227,7 +1239,7 @@ int32_t piadmm_obca_destroy(piadmm_obca_t h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->d_rec) { (void)hipFree(h->d_rec); (void)hipFree(h->d_out); (void)hipFree(h->d_ist); }
+  if (h->d_rec) { (void)hipFree(h->d_rec); (void)hipFree(h->d_out); (void)hipFree(h->d_ist); (void)hipFree(h->d_qg); }
   if (h->d_stamps) (void)hipFree(h->d_stamps);
   if (h->e0) (void)hipEventDestroy(h->e0);
   if (h->e1) (void)hipEventDestroy(h->e1);
