@@ -59,6 +59,8 @@ struct QP {
   int pre_m = -1;         // pair: rows of the stored active set already appended (gi_solve prebuild), -1: none
   int pre_wbits = 0;
   double* wide = nullptr; // pair: HBM scratch of the wide dual active set (gi_solve_wide), nullptr: none
+  double* snap = nullptr; // pair (graph kernel): HBM snapshot of the last dual active set's S^-1 and Y
+                          // columns, written with gws (gi_snap_restore), nullptr: none
   bool gi_full = false;   // pair: the last gi_solve stopped at its working-set capacity
   float* t32 = nullptr;   // x-step, precision 2 (tables in HBM): fp32 copies of the UNFOLDED G (H x H) and
                           // X' (H rows, stride XLDG) -- the hit path's tables, refined once in fp64
@@ -1781,10 +1783,76 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
         P.gws[0] = m;
         P.gws[1] = P.tstep;
       }
+      // and its S^-1 and Y columns (they depend on the step's geometry only, not on q): the pair's
+      // next solve in this step restores them instead of appending the rows again
+      if (P.snap) {
+        double* sS = P.snap;
+        double* sY = P.snap + WAVE * WAVE;
+        for (int j = 0; j < m; ++j)
+          if (l < m) sS[j * WAVE + l] = Sil[j * ld + l];
+        if (l < H)
+          for (int a = 0; a < m; ++a)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) sY[a * H2 + v * H + l] = Y[a * H2 + v * H + l];
+      }
     }
     wsync();
   }
   return true;
+}
+
+// ---- Restore of a pair's dual active set within an MPC step (graph kernel).  The active set a
+// pair's last solve ended with (P.gws: m, step, codes) comes with its S^-1 and Y columns
+// (P.snap, written by gi_solve): in the same MPC step the pair's QP has the same P and rows --
+// only q changed -- so the next solve starts from them (gi_solve's pre_m path: x0 from the new q,
+// then the dual-feasibility drops) instead of appending the m rows again (one P^-1 column, one
+// bordering pass each).  Not with a hinge row held from its upper side (gi_solve restarts those
+// from the lower side) nor under the global-PI law (the pair's penalty changes every iteration).
+__device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
+  constexpr int NV = 2;
+  const int l = lid(), H = P.H, H2 = NV * H, ld = P.fld;
+  if (!P.snap || !P.gws || !P.gws_warm) return;
+  const int gm = P.gws[0], gt = P.gws[1];
+  if (gt != P.tstep || gm <= 0 || gm > min(P.mmax - 1, P.ycap)) return;
+  const int code = (l < gm) ? P.gws[2 + l] : 0;
+  const bool hup = (l < gm) && ((code & 1) != 0) && P.hinge((code >> 1) / H);
+  const bool kill = (l < gm) && (code < 0 || (P.g1 == 0.0 && P.g2 == 0.0 && P.hinge((code >> 1) / H)));
+  if (wany(hup || kill)) return;
+  ldsd* Sil = lds_ptr(P.fac);
+  const double* sS = P.snap;
+  const double* sY = P.snap + WAVE * WAVE;
+  for (int j0 = 0; j0 < gm; j0 += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (l < gm && j0 + u < gm) ? sS[(j0 + u) * WAVE + l] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (l < gm && j0 + u < gm) Sil[(j0 + u) * ld + l] = v[u];
+  }
+  if (l < H) {
+    for (int a0 = 0; a0 < gm; a0 += 4) {
+      double v[4][NV];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < NV; ++w) v[u][w] = (a0 + u < gm) ? sY[(a0 + u) * H2 + w * H + l] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < NV; ++w)
+          if (a0 + u < gm) P.Y[(a0 + u) * H2 + w * H + l] = v[u][w];
+    }
+  }
+  if (l < gm) P.ib[l] = code;
+  int wb = 0;
+  for (int a = 0; a < gm; ++a) {
+    const int c = rdli(code, a), row = c >> 1, sl = row / H, k = row - sl * H;
+    if (k == l) wb |= 1 << (2 * sl + (c & 1));
+  }
+  P.pre_m = gm;
+  P.pre_wbits = wb;
+  if (P.gmem) gsync();
+  else wsync();
 }
 
 // ---- Wide dual active set: pair QPs whose working set outgrows one row per lane (saturated
@@ -2313,6 +2381,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       int ngi = 0;
       signed char glab[NR];
       signed char clab[NR];
+      if constexpr (NV == 2) gi_snap_restore(P);
       if (gi_solve(P, nullptr, glab, x, y, ngi, clab)) {
         signed char nl[NR];
         ok = kkt_check(P, glab, x, y, nl);

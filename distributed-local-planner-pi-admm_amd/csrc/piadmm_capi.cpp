@@ -558,6 +558,14 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   A.gi_wide_stride = pd::giw_stride(H);
   if (E > 0 && A.pair_gi && 2 * H > pd::WAVE - 1)
     rc |= dalloc(h, &A.gi_wide, C * (A.graph ? pd::GW : 1) * A.gi_wide_stride);
+  // graph mode: each pair's last dual active set (S^-1 and Y columns) for its next solve in the
+  // same MPC step (pd_qp.h gi_snap_restore); PIADMM_PAIR_SNAP=0 appends the rows again instead
+  {
+    const char* sn = std::getenv("PIADMM_PAIR_SNAP");
+    const size_t snap_n = E * ((size_t)pd::WAVE * pd::WAVE + (size_t)pd::WAVE * 2 * H);
+    if (A.graph && E > 0 && A.pair_gi && !(sn && sn[0] == '0') && snap_n * sizeof(double) <= ((size_t)8 << 30))
+      rc |= dalloc(h, &A.gi_snap, snap_n);
+  }
   rc |= dalloc(h, &A.gpart, (size_t)2 * C * 5);
   rc |= dalloc(h, &A.ghist, (size_t)h->step_cap * std::max(h->cfg.max_outer, 1) * 2);
   rc |= dalloc(h, &A.giters, (size_t)h->step_cap);

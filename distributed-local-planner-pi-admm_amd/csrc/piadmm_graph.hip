@@ -266,6 +266,10 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
   qe.gws = A.gi_ws + (size_t)e * GI_WS;
   qe.gws_warm = A.pair_warm != 0;
   qe.wide = A.gi_wide ? A.gi_wide + ((size_t)blockIdx.x * GW + (threadIdx.x >> 6)) * A.gi_wide_stride : nullptr;
+  // the pair's dual active set of its last solve in this step (not under the global-PI law: the
+  // pair's penalty, hence P, changes every iteration)
+  qe.snap = (A.gi_snap && c.dual_mode != PIADMM_DUAL_PI_GLOBAL)
+                ? A.gi_snap + (size_t)e * ((size_t)WAVE * WAVE + (size_t)WAVE * 2 * H) : nullptr;
   qe.tstep = t;
   qe.csig = -1;
   if (l == 0) W.zfs[0] = -1;
