@@ -978,21 +978,6 @@ static int32_t run_steps(piadmm_handle_t h, int32_t t, int32_t n, bool sync_outp
     LAUNCH(h, pd::launch_pair_deff(h->a, s));
     h->ghist.assign((size_t)2 * M, NAN);
     int flag = 0, nit = 0, nanlast = 0;
-    if (c.fixed_iters && h->xchg && !h->split && M > 1 && !no_zx()) {
-      // a sharded job's fixed iterations, one launch between two exchanges: X(0), then per
-      // iteration it the Z phase of it and the X phase of it+1 in ONE launch (a component is one
-      // workgroup: its x-steps read only its own pairs' hat / lam), then Z(M-1) -- M + 1 launches
-      // and M all-reduces per step instead of 2M launches
-      const size_t nx = (size_t)h->n_slots * 3 * (c.H + 1);
-      LAUNCH(h, launch_step(h->a, tk, 1, 0, 1, pd::F_FIRST | pd::F_GLOBAL | pd::F_XONLY, s));
-      if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
-      for (int it = 0; it + 1 < M; ++it) {
-        LAUNCH(h, launch_step(h->a, tk, 1, it, it + 2, pd::F_GLOBAL | pd::F_ZONLY | pd::F_XONLY, s));
-        if (int rc = allreduce(h, h->a.xbuf, h->d_xrecv, nx)) return rc;
-      }
-      LAUNCH(h, launch_step(h->a, tk, 1, M - 1, M, pd::F_GLOBAL | pd::F_ZONLY, s));
-      nit = M;
-    } else
     for (int it = 0; it < M; ++it) {
       int stop = 0;
       if (int rc = global_iteration(h, tk, it, flag, nanlast, &stop)) return rc;
