@@ -58,6 +58,7 @@ struct QP {
   int tstep;              // MPC step index (warm-set bookkeeping)
   int pre_m = -1;         // pair: rows of the stored active set already appended (gi_solve prebuild), -1: none
   int pre_wbits = 0;
+  bool pre_lin = false;   // pair, restored active set (gi_snap_restore): this lane's hinge regime (linear)
   double* wide = nullptr; // pair: HBM scratch of the wide dual active set (gi_solve_wide), nullptr: none
   double* snap = nullptr; // pair (graph kernel): HBM snapshot of the last dual active set's S^-1 and Y
                           // columns, written with gws (gi_snap_restore), nullptr: none
@@ -1352,7 +1353,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   // turns the row back to its zero regime (x0 += beta P^-1 n again).  Both events keep the
   // iterate stationary and dual feasible, so the dual active set continues in place (a bounded
   // dual method): no restart, no cycling between the regimes.
-  bool lin = false;
+  // (a restored active set of this step comes with its hinge regimes: gi_snap_restore)
+  bool lin = (!prebuild && P.pre_m >= 0) ? P.pre_lin : false;
   auto start = [&]() {
     double qt[NV];
 #pragma unroll
@@ -1794,6 +1796,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
           for (int a = 0; a < m; ++a)
 #pragma unroll
             for (int v = 0; v < NV; ++v) sY[a * H2 + v * H + l] = Y[a * H2 + v * H + l];
+        sY[WAVE * H2 + l] = lin ? 1.0 : 0.0;   // the hinge regimes of the final state
       }
     }
     wsync();
@@ -1806,8 +1809,9 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
 // (P.snap, written by gi_solve): in the same MPC step the pair's QP has the same P and rows --
 // only q changed -- so the next solve starts from them (gi_solve's pre_m path: x0 from the new q,
 // then the dual-feasibility drops) instead of appending the m rows again (one P^-1 column, one
-// bordering pass each).  Not with a hinge row held from its upper side (gi_solve restarts those
-// from the lower side) nor under the global-PI law (the pair's penalty changes every iteration).
+// bordering pass each).  The hinge rows' regimes (linear or zero) of that final state come with
+// it, so the solve resumes from exactly the state it ended in.  Not under the global-PI law (the
+// pair's penalty changes every iteration).
 __device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
   constexpr int NV = 2;
   const int l = lid(), H = P.H, H2 = NV * H, ld = P.fld;
@@ -1815,9 +1819,8 @@ __device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
   const int gm = P.gws[0], gt = P.gws[1];
   if (gt != P.tstep || gm <= 0 || gm > min(P.mmax - 1, P.ycap)) return;
   const int code = (l < gm) ? P.gws[2 + l] : 0;
-  const bool hup = (l < gm) && ((code & 1) != 0) && P.hinge((code >> 1) / H);
   const bool kill = (l < gm) && (code < 0 || (P.g1 == 0.0 && P.g2 == 0.0 && P.hinge((code >> 1) / H)));
-  if (wany(hup || kill)) return;
+  if (wany(kill)) return;
   ldsd* Sil = lds_ptr(P.fac);
   const double* sS = P.snap;
   const double* sY = P.snap + WAVE * WAVE;
@@ -1844,6 +1847,7 @@ __device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
     }
   }
   if (l < gm) P.ib[l] = code;
+  P.pre_lin = sY[WAVE * H2 + l] != 0.0;
   int wb = 0;
   for (int a = 0; a < gm; ++a) {
     const int c = rdli(code, a), row = c >> 1, sl = row / H, k = row - sl * H;

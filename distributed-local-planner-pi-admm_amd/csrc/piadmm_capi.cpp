@@ -562,7 +562,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   // same MPC step (pd_qp.h gi_snap_restore); PIADMM_PAIR_SNAP=0 appends the rows again instead
   {
     const char* sn = std::getenv("PIADMM_PAIR_SNAP");
-    const size_t snap_n = E * ((size_t)pd::WAVE * pd::WAVE + (size_t)pd::WAVE * 2 * H);
+    const size_t snap_n = E * ((size_t)pd::WAVE * pd::WAVE + (size_t)pd::WAVE * 2 * H + pd::WAVE);
     if (A.graph && E > 0 && A.pair_gi && !(sn && sn[0] == '0') && snap_n * sizeof(double) <= ((size_t)8 << 30))
       rc |= dalloc(h, &A.gi_snap, snap_n);
   }

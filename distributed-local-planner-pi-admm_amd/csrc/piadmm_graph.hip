@@ -269,7 +269,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
   // the pair's dual active set of its last solve in this step (not under the global-PI law: the
   // pair's penalty, hence P, changes every iteration)
   qe.snap = (A.gi_snap && c.dual_mode != PIADMM_DUAL_PI_GLOBAL)
-                ? A.gi_snap + (size_t)e * ((size_t)WAVE * WAVE + (size_t)WAVE * 2 * H) : nullptr;
+                ? A.gi_snap + (size_t)e * ((size_t)WAVE * WAVE + (size_t)WAVE * 2 * H + WAVE) : nullptr;
   qe.tstep = t;
   qe.csig = -1;
   if (l == 0) W.zfs[0] = -1;

@@ -102,7 +102,7 @@ struct DevArgs {
   int* gi_ws;               // E*(2+64) the pair's last dual active set: m, step t, codes
   double* gi_wide;          // H >= 32: C * (GW | 1) * giw_stride(H) wide dual active-set scratch
   size_t gi_wide_stride;    // giw_stride(H)
-  double* gi_snap;          // graph mode: E * (64*64 + 64*2H) the pair's last dual active set's S^-1 | Y
+  double* gi_snap;          // graph mode: E * (64*64 + 64*2H + 64) the pair's last dual active set: S^-1 | Y | hinge regimes
   double* gpart;            // 2*C*5 coop: per-component termination partials (iteration parity)
   double* ghist;            // step_cap*max_outer*2 coop: global (rk, sk) history per step
   int* giters;              // step_cap coop: global outer iterations per step
