@@ -11,19 +11,22 @@ namespace pd {
 
 // Diagnostic phase stamps (separate build, never in the measured library).
 #ifdef PIADMM_STAMPS
-// cycles accumulate in LDS (one ds_add_u64 per stamp, lane 0) and are flushed to g_stamps
-// once per launch, so that a stamp costs an LDS atomic, not a global one
+// cycles accumulate in LDS per wave (one ds_add_u64 per stamp, lane 0; slot + 64 x wave, waves
+// 0..3) and are flushed to g_stamps (C x 4 x 64) once per launch, so that a stamp costs an LDS
+// atomic, not a global one
+constexpr int STAMP_WAVES = 4;
 __device__ unsigned long long* g_stamps;
-__shared__ unsigned long long s_stamps[64];
+__shared__ unsigned long long s_stamps[64 * STAMP_WAVES];
 #define STAMP_T() __builtin_amdgcn_s_memtime()
+#define STAMP_W() (((int)threadIdx.x >> 6) & (STAMP_WAVES - 1))
 #define STAMP_ADD(slot, t0)                                                                   \
   do {                                                                                        \
     const unsigned long long _d = __builtin_amdgcn_s_memtime() - (t0);                       \
-    if (__lane_id() == 0) atomicAdd(&s_stamps[(slot)], _d);                                  \
+    if (__lane_id() == 0) atomicAdd(&s_stamps[(slot) + 64 * STAMP_W()], _d);                 \
   } while (0)
 #define STAMP_CNT(slot, n)                                                                    \
   do {                                                                                        \
-    if (__lane_id() == 0) atomicAdd(&s_stamps[(slot)], (unsigned long long)(n));             \
+    if (__lane_id() == 0) atomicAdd(&s_stamps[(slot) + 64 * STAMP_W()], (unsigned long long)(n)); \
   } while (0)
 #else
 #define STAMP_CNT(slot, n) ((void)(n))
@@ -208,8 +211,10 @@ __device__ __forceinline__ double around(double x, int d) {
 // in a cold branch (ties are rare: the hot path pays a compare and a ballot).
 __device__ __forceinline__ void tie_record(const DevArgs& A, int t, int it, int kind, int id, int idx, double margin) {
   atomicAdd(A.tie_cnt + kind, 1ull);
-  const int k = atomicAdd(A.tie_n, 1);
-  if (k < A.tie_cap) {
+  // 64-bit event counter: it cannot wrap to a negative slot however many decisions a wide
+  // tolerance logs; only the first tie_cap events are stored
+  const unsigned long long k = atomicAdd(A.tie_n, 1ull);
+  if (k < (unsigned long long)A.tie_cap) {
     int* ev = A.tie_ev + 6 * k;
     ev[0] = t;
     ev[1] = it;

@@ -61,6 +61,10 @@ struct piadmm_ctx {
   // host-stepped MPC step (piadmm_outer_iter / piadmm_step_finish): the open step, the next
   // outer iteration, and the host-decided stop state of the global scope
   bool step_open = false;
+  // the MPC step the receding-horizon sequence continues with (-1: a fresh sequence, any t).  A
+  // step run at any other t (the same t again, a jump) must not resume a pair's stored dual active
+  // set: its S^-1 and Y columns were built for another step's geometry (pd_qp.h gi_snap_restore)
+  int t_next = -1;
   int step_t = -1, step_it = 0, step_flag = 0, step_nanlast = 0, step_stop = 0;
   // device-decided global termination (F_DEVSTOP): pinned copy of the stop state, iterations
   // enqueued per chunk (the last step's count), PIADMM_HOST_DECIDE=1 keeps one host decision
@@ -137,6 +141,12 @@ int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
     return fail(h, PIADMM_E_ARG, "dual_mode must be 0 (plain), 1 (PI) or 2 (global PI)");
   if (c.dual_mode == PIADMM_DUAL_PI_GLOBAL && !(c.rho_min > 0 && c.rho_max >= c.rho_min && c.rho_num > 0))
     return fail(h, PIADMM_E_ARG, "global PI needs 0 < rho_min <= rho_max and rho_num > 0");
+  if ((c.pi_trad != 0 && c.pi_trad != 1) || (c.ki_adapt != 0 && c.ki_adapt != 1))
+    return fail(h, PIADMM_E_ARG, "pi_trad and ki_adapt must be 0 or 1");
+  if ((c.pi_trad || c.ki_adapt) && c.dual_mode != PIADMM_DUAL_PI_GLOBAL)
+    return fail(h, PIADMM_E_ARG, "pi_trad / ki_adapt select variants of the global PI law (dual_mode 2)");
+  if (!std::isfinite(c.d_gain) || !std::isfinite(c.dual_init))
+    return fail(h, PIADMM_E_ARG, "d_gain and dual_init must be finite");
   if (!(c.dt > 0) || !(c.L > 0) || !(c.rho > 0) || !(c.Pcost > 0) || c.Pnorm < 0 || c.beta < 0)
     return fail(h, PIADMM_E_ARG, "dt, L, rho, Pcost must be > 0; Pnorm, beta >= 0");
   if (c.max_inner <= 0 || c.polish_every <= 0) return fail(h, PIADMM_E_ARG, "max_inner, polish_every must be > 0");
@@ -305,7 +315,8 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     if (g && g[0] == '1') simple = false;
   }
   // the global PI law (adaptive per-pair penalties) runs on the graph kernel
-  if (h->cfg.dual_mode == PIADMM_DUAL_PI_GLOBAL || h->cfg.no_collision_gate) simple = false;
+  // (and a nonzero initial pair state, dual_init: the adaptive-gain script's 1e-4)
+  if (h->cfg.dual_mode == PIADMM_DUAL_PI_GLOBAL || h->cfg.no_collision_gate || h->cfg.dual_init != 0.0) simple = false;
   // a sharded job with a boundary exchange runs on the graph kernel (its X / Z phases are
   // split launches around the all-reduce)
   const bool sharded = owned != nullptr;
@@ -556,8 +567,12 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
   // the wide dual active set's scratch (pair working sets beyond 63 rows, H >= 32): one region
   // per wave that solves pair QPs -- the graph kernel's GW waves, the fused kernel's pair wave
   A.gi_wide_stride = pd::giw_stride(H);
-  if (E > 0 && A.pair_gi && 2 * H > pd::WAVE - 1)
-    rc |= dalloc(h, &A.gi_wide, C * (A.graph ? pd::GW : 1) * A.gi_wide_stride);
+  // (over 8 GB -- hundreds of thousands of components at H >= 32 -- the wide path is off: such
+  // saturated pair QPs are then reported PIADMM_QP_INEXACT, as before it existed)
+  if (E > 0 && A.pair_gi && 2 * H > pd::WAVE - 1) {
+    const size_t wide_n = C * (A.graph ? pd::GW : 1) * A.gi_wide_stride;
+    if (wide_n * sizeof(double) <= ((size_t)8 << 30)) rc |= dalloc(h, &A.gi_wide, wide_n);
+  }
   // graph mode: each pair's last dual active set (S^-1 and Y columns) for its next solve in the
   // same MPC step (pd_qp.h gi_snap_restore); PIADMM_PAIR_SNAP=0 appends the rows again instead
   {
@@ -620,7 +635,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     rc |= dalloc(h, &h->d_xrecv, (size_t)n_slots * 3 * H1);
   }
 #ifdef PIADMM_STAMPS
-  rc |= dalloc(h, &A.stamps, C * 64);
+  rc |= dalloc(h, &A.stamps, C * 64 * 4);     // per component and wave (pd_common.h STAMP_WAVES)
 #endif
   if (rc) return PIADMM_E_HIP;
   HIPCHK(h, hipMemcpyAsync(d_spd, spd, N * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -692,6 +707,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     (void)hipGetLastError();   // a refused query must not surface as the next launch's error
   }
   h->have_scn = true;
+  h->t_next = -1;
   return PIADMM_OK;
 }
 
@@ -725,6 +741,7 @@ int32_t piadmm_set_xt(piadmm_handle_t h, const double* xt) {
   // a new state breaks the receding-horizon sequence: no label warm start for the next step
   HIPCHK(h, hipMemsetAsync(h->a.warm_ok, 0, (size_t)h->N * sizeof(int), h->stream));
   if (h->E) HIPCHK(h, hipMemsetAsync(h->a.gi_ws, 0, (size_t)h->E * (2 + pd::WAVE) * sizeof(int), h->stream));
+  h->t_next = -1;
   // and no carried ADMM penalties: a run from a new state starts from the configured penalty
   // (the per-scenario caches stay: they are keyed by the penalty they were built for)
   if (int rc = reset_penalties(h)) return rc;
@@ -1013,6 +1030,14 @@ static int32_t sync_step_cap(piadmm_handle_t h) {
   return PIADMM_OK;
 }
 
+// A step at t0 that does not continue the receding-horizon sequence forgets the pairs' stored
+// active sets (codes, step index, the snapshot's validity: pd_qp.h gi_solve / gi_snap_restore).
+static int32_t continue_sequence(piadmm_handle_t h, int32_t t0) {
+  if (h->t_next >= 0 && t0 != h->t_next && h->E)
+    HIPCHK(h, hipMemsetAsync(h->a.gi_ws, 0, (size_t)h->E * (2 + pd::WAVE) * sizeof(int), h->stream));
+  return PIADMM_OK;
+}
+
 static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
   if (!h) return fail(nullptr, PIADMM_E_ARG, "null handle");
   if (!h->have_scn) return fail(h, PIADMM_E_STATE, "set_scenario first");
@@ -1020,6 +1045,8 @@ static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
   if (n < 0 || t0 < 0 || t0 + (n > 0 ? n - 1 : 0) + h->cfg.H + 1 > h->T)
     return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
   HIPCHK(h, hipSetDevice(h->cfg.device));
+  if (int rc = continue_sequence(h, t0)) return rc;
+  h->t_next = t0 + n;
   if ((h->comm || h->xfn) && !h->cap_synced)
     if (int rc = sync_step_cap(h)) return rc;
   for (int i = 0; i < n;) {
@@ -1070,6 +1097,9 @@ int32_t piadmm_outer_iter(piadmm_handle_t h, int32_t t, int32_t it, int32_t* sto
   if (it < 0 || it >= c.max_outer) return fail(h, PIADMM_E_ARG, "it must be in [0, max_outer)");
   if (t < 0 || t + c.H + 1 > h->T) return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
   if (it == 0) {
+    HIPCHK(h, hipSetDevice(c.device));
+    if (int rc = continue_sequence(h, t)) return rc;
+    h->t_next = t + 1;
     h->step_open = true;
     h->step_t = t;
     h->step_flag = h->step_nanlast = h->step_stop = 0;
@@ -1311,14 +1341,26 @@ int32_t piadmm_candidate_pairs(piadmm_handle_t h, const double* xy, const double
   return PIADMM_OK;
 }
 
-// Diagnostic builds only: per-component phase cycle sums (C x 32), reset with the counters.
+// Diagnostic builds only: per-component phase cycle sums, reset with the counters: C x 64 summed
+// over the workgroup's waves, or (n >= C x 256) C x 4 x 64 per wave.
 int32_t piadmm_debug_stamps(piadmm_handle_t h, uint64_t* out, int32_t n) {
   if (!h || !out) return fail(h, PIADMM_E_ARG, "null argument");
   if (!h->a.stamps) return fail(h, PIADMM_E_STATE, "library built without PIADMM_STAMPS");
   if (n < h->C * 64) return fail(h, PIADMM_E_ARG, "buffer too small");
   HIPCHK(h, hipSetDevice(h->cfg.device));
-  HIPCHK(h, hipMemcpyAsync(out, h->a.stamps, (size_t)h->C * 64 * 8, hipMemcpyDeviceToHost, h->stream));
+  std::vector<uint64_t> raw((size_t)h->C * 64 * 4);
+  HIPCHK(h, hipMemcpyAsync(raw.data(), h->a.stamps, raw.size() * 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (n >= h->C * 64 * 4) {
+    std::copy(raw.begin(), raw.end(), out);
+  } else {
+    for (int ci = 0; ci < h->C; ++ci)
+      for (int k = 0; k < 64; ++k) {
+        uint64_t v = 0;
+        for (int w = 0; w < 4; ++w) v += raw[((size_t)ci * 4 + w) * 64 + k];
+        out[(size_t)ci * 64 + k] = v;
+      }
+  }
   return PIADMM_OK;
 }
 
@@ -1339,11 +1381,11 @@ int32_t piadmm_get_near_ties(piadmm_handle_t h, uint64_t* counts, piadmm_near_ti
   HIPCHK(h, hipSetDevice(h->cfg.device));
   hipStream_t s = h->stream;
   unsigned long long cnt[PIADMM_TIE_KINDS];
-  int nd = 0;
+  unsigned long long nd = 0;
   HIPCHK(h, hipMemcpyAsync(cnt, h->a.tie_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
-  HIPCHK(h, hipMemcpyAsync(&nd, h->a.tie_n, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipMemcpyAsync(&nd, h->a.tie_n, sizeof(nd), hipMemcpyDeviceToHost, s));
   HIPCHK(h, hipStreamSynchronize(s));
-  const int kept = std::min(nd, PIADMM_TIE_CAP);
+  const int kept = (int)std::min<unsigned long long>(nd, (unsigned long long)PIADMM_TIE_CAP);
   std::vector<int> ev((size_t)kept * 6);
   std::vector<double> mg((size_t)kept);
   if (kept > 0) {
@@ -1365,7 +1407,7 @@ int32_t piadmm_get_near_ties(piadmm_handle_t h, uint64_t* counts, piadmm_near_ti
     o.margin = mg[i];
   }
   for (size_t i = 0; i < h->host_ties.size() && w < max_events; ++i, ++w) events[w] = h->host_ties[i];
-  if (n_events) *n_events = nd + (int)h->host_ties.size();
+  if (n_events) *n_events = w;   // events written; the totals are the per-kind counts
   return PIADMM_OK;
 }
 
@@ -1400,7 +1442,14 @@ int32_t piadmm_set_state(piadmm_handle_t h, const double* xt, const double* hat,
     if (!std::isfinite(xt[i])) return fail(h, PIADMM_E_ARG, "non-finite state");
   if (rho_pi)
     for (size_t e = 0; e < E; ++e)
-      if (!(rho_pi[e] > 0.0)) return fail(h, PIADMM_E_ARG, "rho_pi must be > 0");
+      if (!(rho_pi[e] > 0.0) || !std::isfinite(rho_pi[e])) return fail(h, PIADMM_E_ARG, "rho_pi must be finite and > 0");
+  {
+    const double* pst[5] = {hat, lam, S, D, last_hat};
+    for (int k = 0; k < 5; ++k)
+      if (pst[k])
+        for (size_t i = 0; i < E * 4 * H1; ++i)
+          if (!std::isfinite(pst[k][i])) return fail(h, PIADMM_E_ARG, "non-finite pair state");
+  }
   // xt, and a fresh receding-horizon sequence (labels, warm active sets, ADMM penalties)
   if (int rc = piadmm_set_xt(h, xt)) return rc;
   HIPCHK(h, hipSetDevice(h->cfg.device));
@@ -1426,10 +1475,10 @@ int32_t piadmm_reset_counters(piadmm_handle_t h) {
   HIPCHK(h, hipSetDevice(h->cfg.device));
   HIPCHK(h, hipMemsetAsync(h->a.counters, 0, (size_t)h->C * 8 * 8, h->stream));
   HIPCHK(h, hipMemsetAsync(h->a.tie_cnt, 0, PIADMM_TIE_KINDS * sizeof(unsigned long long), h->stream));
-  HIPCHK(h, hipMemsetAsync(h->a.tie_n, 0, sizeof(int), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->a.tie_n, 0, sizeof(unsigned long long), h->stream));
   h->host_ties.clear();
   for (auto& v : h->host_tie_cnt) v = 0;
-  if (h->a.stamps) HIPCHK(h, hipMemsetAsync(h->a.stamps, 0, (size_t)h->C * 64 * 8, h->stream));
+  if (h->a.stamps) HIPCHK(h, hipMemsetAsync(h->a.stamps, 0, (size_t)h->C * 64 * 4 * 8, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PIADMM_OK;
 }

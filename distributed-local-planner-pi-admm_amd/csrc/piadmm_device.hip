@@ -617,12 +617,14 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       // agent 1's on the roller wave at the same time (roll_part); then wait for the roller's flag
       const bool nonlin_pos = c.pos_model != 0;
       double px, py, pth;
+      unsigned long long t_ro = STAMP_T();
       const double u = (l < H) ? S.u[(it & 1) * 2 * H + l] : 0.0;
       rollout_r(S.xt[0], S.xt[1], S.xt[2], ra_s[0], ra_s[0] / c.L, u, c, H, nonlin_pos, px, py, pth);
       if (l <= H) {
         pos[0 * H1 + l] = px;
         pos[1 * H1 + l] = py;
       }
+      STAMP_ADD(ST_XQ, t_ro);          // (pair wave: its rollout of agent 0)
       unsigned long long t_rw = STAMP_T();
       while (__hip_atomic_load(X.rflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != it + 1)
         __builtin_amdgcn_s_sleep(1);
@@ -844,7 +846,10 @@ __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
   __syncthreads();                                       // the parts' setup barrier
   for (int it = X.it0; it < X.it_end; ++it) {
     double* const pos = S.pos + (it & 1) * 4 * H1;
+    unsigned long long t_sa = STAMP_T();
     __syncthreads();                                     // A: the agents' controls of iteration it
+    STAMP_ADD(ST_SYNC_A, t_sa);
+    unsigned long long t_ro = STAMP_T();
     if (has) {
       double px, py, pth;
       const double u = (l < H) ? S.u[(it & 1) * 2 * H + H + l] : 0.0;
@@ -856,7 +861,10 @@ __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
     }
     // (release: the wave's position stores complete before the flag)
     if (l == 0) __hip_atomic_store(X.rflag, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    STAMP_ADD(ST_XQ, t_ro);
+    unsigned long long t_sb = STAMP_T();
     __syncthreads();                                     // B: the pair wave's verdict
+    STAMP_ADD(ST_SYNC_B, t_sb);
     if (X.vd[1]) break;
   }
 }
@@ -1070,7 +1078,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 template <bool BIG, bool TIES>
 __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
 #ifdef PIADMM_STAMPS
-  if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
+  for (int i = threadIdx.x; i < 64 * STAMP_WAVES; i += blockDim.x) s_stamps[i] = 0ull;
   __syncthreads();
 #endif
   if (flags & F_DEVSTOP) {      // device-decided global stop (uniform: every thread reads it)
@@ -1087,7 +1095,9 @@ __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int 
     __syncthreads();
   }
 #ifdef PIADMM_STAMPS
-  if (threadIdx.x < 64 && g_stamps) atomicAdd(&g_stamps[blockIdx.x * 64 + threadIdx.x], s_stamps[threadIdx.x]);
+  if (g_stamps)
+    for (int i = threadIdx.x; i < 64 * STAMP_WAVES; i += blockDim.x)
+      atomicAdd(&g_stamps[(size_t)blockIdx.x * 64 * STAMP_WAVES + i], s_stamps[i]);
 #endif
 }
 

@@ -342,6 +342,8 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
     }
     const double dmin = wmin(tl ? dn : INFINITY);
     const double kP = fmin(c.theta1 / dmin, c.theta2);
+    // K_I: constant (casadi_old :135) or K_I_coeff / d_min (adaptive gains, ADMM_CVX_..._adp_PI_antiwindup1.m:127)
+    const double kI = c.ki_adapt ? c.kI / dmin : c.kI;
     const double rnew = fmax(c.rho_min, fmin(c.rho_max, c.rho_num / dmin));
     double lraw[2][2], lsat[2][2];
     bool changed = false;
@@ -353,9 +355,17 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
         const double p = xy == 0 ? px[v] : py[v];
         const double h = xy == 0 ? hx[v] : hy[v];
         const double err = p - h;
-        const double so = tl ? Sv[xy * H1 + l] : 0.0;
-        lraw[v][xy] = so + kP * err;                          // lam = S + K_P e (:143)
-        if (tl) Sv[xy * H1 + l] = (so + c.kI * err) + 2.0 * Dv[xy * H1 + l];   // S += K_I e + 2 D (:144)
+        if (c.pi_trad) {
+          // the scripts' trad branch: lam += rho e + D, the updated rho (casadi_old :138-139, adp :131-132)
+          const double lo = tl ? lam[v * 2 * H1 + xy * H1 + l] : 0.0;
+          const double dv = tl ? Dv[xy * H1 + l] : 0.0;
+          lraw[v][xy] = (lo + rnew * err) + dv;
+        } else {
+          const double so = tl ? Sv[xy * H1 + l] : 0.0;
+          lraw[v][xy] = so + kP * err;                        // lam = S + K_P e (casadi_old :141)
+          // S += K_I e + d_gain D: d_gain 2 (casadi_old :142), 1 (adp :135)
+          if (tl) Sv[xy * H1 + l] = (so + kI * err) + c.d_gain * Dv[xy * H1 + l];
+        }
         lsat[v][xy] = c.windup ? fmin(c.windup_sat, fmax(lraw[v][xy], -c.windup_sat)) : lraw[v][xy];
         changed |= tl && (lsat[v][xy] != lraw[v][xy]);
         if (tl) hv[xy * H1 + l] = h;
@@ -502,7 +512,9 @@ __device__ __forceinline__ void g_step_init(const DevArgs& A, int ci, int w, int
     for (int k = 0; k < 5; ++k) {
       double* p = eh[k] + (size_t)e * 4 * H1;
       double v[4];
-      for (int r = 0; r < 4; ++r) v[r] = (c.warm_duals && l <= H) ? p[r * H1 + min(l + 1, H)] : 0.0;
+      // (the adaptive-gain script starts hat, lam and last_hat at 1e-4: dual_init, adp :59-61)
+      const double v0 = (k == 0 || k == 1 || k == 4) ? c.dual_init : 0.0;
+      for (int r = 0; r < 4; ++r) v[r] = (c.warm_duals && l <= H) ? p[r * H1 + min(l + 1, H)] : v0;
       gsync();
       if (l <= H)
         for (int r = 0; r < 4; ++r) p[r * H1 + l] = v[r];
@@ -863,7 +875,7 @@ __global__ void __launch_bounds__(GW * WAVE) k_graph_step(DevArgs A, int t0, int
     }
   }
 #ifdef PIADMM_STAMPS
-  if (threadIdx.x < 64) s_stamps[threadIdx.x] = 0ull;
+  for (int i = threadIdx.x; i < 64 * STAMP_WAVES; i += blockDim.x) s_stamps[i] = 0ull;
   __syncthreads();
 #endif
   int nbar = 0;
@@ -872,7 +884,9 @@ __global__ void __launch_bounds__(GW * WAVE) k_graph_step(DevArgs A, int t0, int
     __syncthreads();
   }
 #ifdef PIADMM_STAMPS
-  if (threadIdx.x < 64 && g_stamps) atomicAdd(&g_stamps[blockIdx.x * 64 + threadIdx.x], s_stamps[threadIdx.x]);
+  if (g_stamps)
+    for (int i = threadIdx.x; i < 64 * STAMP_WAVES; i += blockDim.x)
+      atomicAdd(&g_stamps[(size_t)blockIdx.x * 64 * STAMP_WAVES + i], s_stamps[i]);
 #endif
 }
 

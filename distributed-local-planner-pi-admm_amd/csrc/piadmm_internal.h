@@ -93,7 +93,7 @@ struct DevArgs {
   signed char* ql_e;        // E*5*WAVE  labels of the pair QP
   int* cst;                 // C*4       flag, aliased, warm bits (x0, x1, pair), spare
   unsigned long long* counters;  // C*8  accumulated work counters (see piadmm_get_counters)
-  unsigned long long* stamps;    // C*32 phase cycle sums (diagnostic build -DPIADMM_STAMPS only)
+  unsigned long long* stamps;    // C x 4 waves x 64 phase cycle sums (diagnostic build -DPIADMM_STAMPS only)
   double* rho_x;            // N   ADMM penalty per agent QP (adapted, persists across steps)
   double* rho_e;            // E   ADMM penalty per pair QP
   double* Kx_cache;         // N*H*H agent K_s^-1 for the penalty xcache_rho[a] (per scenario)
@@ -150,7 +150,7 @@ struct DevArgs {
   // (:112-113), the stop test (:174) and MATLAB's distance check -- where two exact
   // implementations may resolve them differently
   unsigned long long* tie_cnt;   // PIADMM_TIE_KINDS counts
-  int* tie_n;                    // events so far (may exceed tie_cap)
+  unsigned long long* tie_n;     // events so far (may exceed tie_cap)
   int* tie_ev;                   // tie_cap x 6 ints: step, iter, kind, id, index, 0
   double* tie_mg;                // tie_cap margins
   int tie_cap;

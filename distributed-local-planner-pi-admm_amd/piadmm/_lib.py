@@ -34,7 +34,7 @@ class PiadmmConfigC(ctypes.Structure):
         ("term_global", c_i32), ("warm_duals", c_i32), ("tighten", c_i32), ("precision", c_i32),
         ("tight_p", c_dbl), ("avg_delay", c_dbl), ("var_delay", c_dbl),
         ("rho_num", c_dbl), ("rho_min", c_dbl), ("rho_max", c_dbl), ("no_collision_gate", c_i32),
-        ("reserved0", c_i32),
+        ("pi_trad", c_i32), ("ki_adapt", c_i32), ("reserved1", c_i32), ("d_gain", c_dbl), ("dual_init", c_dbl),
     ]
 
 

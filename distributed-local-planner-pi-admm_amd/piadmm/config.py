@@ -74,7 +74,12 @@ class PIADMMConfig:
     rho_max: float = 5.0
     no_collision_gate: int = 0  # 1: every candidate pair's QP every iteration (the script has no
                                 #    collision test: its edge problem is solved unconditionally, :96-115)
-    reserved0: int = 0
+    pi_trad: int = 0            # 1: the scripts' `trad == 1` branch: lam += rho e + D (casadi_old_PI_ADMM/main.py:138-139)
+    # --- the adaptive-gain global PI (ADMM_CVX_two_veh_intesection_adp_PI_antiwindup1.m:121-146) ---
+    ki_adapt: int = 0           # 1: K_I = kI / dis_min (K_I_coeff / dis_min, :127); 0: K_I = kI (casadi_old :135)
+    reserved1: int = 0
+    d_gain: float = 2.0         # S += K_I e + d_gain D: 2 (casadi_old_PI_ADMM/main.py:142), 1 (adp :135)
+    dual_init: float = 0.0      # hat, lam, last_hat at each step's start: 0 (casadi/main.py:56-63) or 1e-4 (adp :59-61)
     # --- inner QP solver (build's own; not in the reference) ---
     admm_rho: float = 0.05      # ADMM penalty in the Ruiz-scaled space (tools/qp_sim.py sweep)
     admm_sigma: float = 1e-6
@@ -129,4 +134,28 @@ def casadi_old_pi(**kw) -> PIADMMConfig:
     return base.replace(**kw)
 
 
-PRESETS = {"casadi_default": casadi_default, "matlab_pi": matlab_pi, "casadi_old_pi": casadi_old_pi}
+def matlab_adp_pi(**kw) -> PIADMMConfig:
+    """``matlab_old_files/ADMM_CVX_two_veh_intesection_adp_PI_antiwindup1.m``: the global PI law
+    with adaptive gains (:121-147) -- from the minimum distance d of the x-step plans (nonlinear
+    rollouts, :121-125), K_I = K_I_coeff / d (:127, K_I_coeff = 3, :51), K_P = min(5 / d, 3)
+    (:128), rho = max(1, min(5, 4 / d)) (:129, kept across MPC steps: param.rho is never reset);
+    lam = S + K_P e, S += K_I e + D (the back-calculation added once, :134-135), or with ``trad``
+    lam += rho e + D (:131-132); saturation +-50 (:40) with back-calculation over the whole dual
+    array (:138-147); hat = lam = 1e-4 at each step's start (:59-61); residuals over both sides
+    without the factor 2 (:151-152) and the stop test without the distance check (:154, commented
+    out); the edge problem solved every iteration (:94-110, no collision test); parameters :3-16
+    (H = 5, dis_thres 1.5, beta 1000, Pnorm 5, Pcost 1, rho 1, eps 1 / 1).  CVX solves exactly
+    (no rounding); pos_old is the numeric dynamic_update_local (its nargin == 4 branch: the
+    nonlinear rollout); the steering box is two-sided as in nonlcon_function (the script's
+    one-sided ``veh_u <= pi/6``, :80, is the same typo as in the per-edge PI script)."""
+    base = PIADMMConfig(
+        H=5, max_outer=100, dt=0.1, L=1.0, dis_thres=1.5, beta=1000.0, Pnorm=5.0, Pcost=1.0,
+        rho=1.0, eps_pri=1.0, eps_dual=1.0, dual_mode=DUAL_PI_GLOBAL, windup=1, kP=0.0, kI=3.0,
+        theta1=5.0, theta2=3.0, windup_sat=50.0, round_decimals=-1, collide_sq_thres=1,
+        alias_dual_residual=0, pos_model=POS_NONLINEAR, term_dist_check=0, rho_num=4.0, rho_min=1.0,
+        rho_max=5.0, no_collision_gate=1, pi_trad=0, ki_adapt=1, d_gain=1.0, dual_init=1e-4)
+    return base.replace(**kw)
+
+
+PRESETS = {"casadi_default": casadi_default, "matlab_pi": matlab_pi, "casadi_old_pi": casadi_old_pi,
+           "matlab_adp_pi": matlab_adp_pi}

@@ -10,6 +10,7 @@ reference's progress line.
 from __future__ import annotations
 
 import dataclasses
+import hashlib
 import json
 import os
 
@@ -94,7 +95,14 @@ def load_run(path: str) -> RunRecord:
 CHECKPOINT_KEYS = ("xt", "hat", "lam", "S", "D", "last_hat", "rho_pi")
 
 
-def save_checkpoint(path: str, state: dict, cfg=None) -> str:
+def scenario_fingerprint(scn) -> np.ndarray:
+    """(N, E, sha256 of the candidate pair list) of a scenario: a checkpoint's pair state (hat /
+    lam / S / D, one row per pair) only means something for the same pairs in the same order."""
+    edges = np.ascontiguousarray(np.asarray(scn.edges, np.int64).reshape(-1, 2))
+    return np.array([str(int(scn.n_agents)), str(int(edges.shape[0])), hashlib.sha256(edges.tobytes()).hexdigest()])
+
+
+def save_checkpoint(path: str, state: dict, cfg=None, scn=None) -> str:
     """Checkpoint of an MPC run between two steps (the ``.npz`` dump of xt,
     duals, S, D): ``state`` from ``PI_ADMM_MI355X.step_state()`` (or the oracle's edge state) --
     xt, the pair state hat / lam / S / D / last_hat (carried by warm_duals, a12), the global-PI
@@ -105,19 +113,31 @@ def save_checkpoint(path: str, state: dict, cfg=None) -> str:
     arrs["t"] = np.array(int(state.get("t", 0)), np.int64)
     if cfg is not None:
         arrs["cfg_json"] = np.array(json.dumps(dataclasses.asdict(cfg), sort_keys=True))
+    if scn is not None:
+        arrs["scenario"] = scenario_fingerprint(scn)
     np.savez_compressed(base + ".npz", **arrs)
     return base + ".npz"
 
 
-def load_checkpoint(path: str, cfg=None) -> dict:
+def load_checkpoint(path: str, cfg=None, scn=None) -> dict:
     """The state :func:`save_checkpoint` wrote (NumPy only, no pickles), for
-    ``PI_ADMM_MI355X.set_state``.  With ``cfg``: refuses a checkpoint of another configuration."""
+    ``PI_ADMM_MI355X.set_state``.  With ``cfg``: refuses a checkpoint of another configuration;
+    with ``scn``: one of another scenario (agent count, pair count or pair list), or one that was
+    saved without the scenario's fingerprint.  Non-finite state is refused either way."""
     base = path[:-4] if path.endswith(".npz") else path
     d = np.load(base + ".npz", allow_pickle=False)
     if cfg is not None and "cfg_json" in d.files:
         if json.loads(str(d["cfg_json"])) != json.loads(json.dumps(dataclasses.asdict(cfg), sort_keys=True)):
             raise ValueError("checkpoint was written with another configuration")
+    if scn is not None:
+        if "scenario" not in d.files:
+            raise ValueError("checkpoint carries no scenario fingerprint (save_checkpoint(..., scn=...))")
+        if not np.array_equal(d["scenario"], scenario_fingerprint(scn)):
+            raise ValueError("checkpoint was written for another scenario (agents, pairs or pair order differ)")
     st = {k: d[k] for k in CHECKPOINT_KEYS if k in d.files}
+    for k, v in st.items():
+        if not np.all(np.isfinite(v)):
+            raise ValueError(f"checkpoint holds non-finite {k}")
     st["t"] = int(d["t"])
     return st
 

@@ -218,7 +218,9 @@ class PI_ADMM_MI355X:
         ev = np.zeros(_lib.TIE_CAP * 2, _lib.TIE_DTYPE)
         n = ctypes.c_int32()
         self._check(self.lib.piadmm_get_near_ties(self._h, cnt, ev.ctypes.data, ev.size, ctypes.byref(n)))
-        return dict(zip(_lib.TIE_KINDS, (int(v) for v in cnt))), ev[:min(int(n.value), ev.size)].copy()
+        # n = the events written (the C side stops at max_events and at each log's cap); the
+        # per-kind counts are the totals
+        return dict(zip(_lib.TIE_KINDS, (int(v) for v in cnt))), ev[:max(0, min(int(n.value), ev.size))].copy()
 
     def step_state(self) -> dict:
         """The state that carries into the next MPC step (piadmm_get_step_state): xt, and hat, lam,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PIADMM_ABI_VERSION 6
+#define PIADMM_ABI_VERSION 7
 
 enum {
   PIADMM_OK = 0,
@@ -50,7 +50,9 @@ enum {
 /* dual_mode */
 #define PIADMM_DUAL_PLAIN 0  /* lam += rho (p - hat)            casadi/main.py:161-162 */
 #define PIADMM_DUAL_PI 1     /* per-edge PI + back-calculation  ADMM_CVX_..._PI_antiwindup.m:156-188 */
-#define PIADMM_DUAL_PI_GLOBAL 2  /* PI with adaptive rho and K_P   casadi_old_PI_ADMM/main.py:133-151 */
+#define PIADMM_DUAL_PI_GLOBAL 2  /* PI with adaptive rho and K_P   casadi_old_PI_ADMM/main.py:133-151;
+                                    with ki_adapt / d_gain / dual_init (ABI 7) the adaptive-gain
+                                    variant ADMM_CVX_two_veh_intesection_adp_PI_antiwindup1.m:121-147 */
 
 /* status_out codes per agent / pair (bit flags accumulated over one MPC step) */
 #define PIADMM_QP_OK 0
@@ -100,7 +102,15 @@ typedef struct piadmm_config {
   double rho_num, rho_min, rho_max;
   int32_t no_collision_gate; /* 1: every candidate pair runs its pair QP every iteration (the
                                 global-PI script solves the edge problem unconditionally) */
-  int32_t reserved0;
+  int32_t pi_trad;           /* ABI 7 (was reserved0), PIADMM_DUAL_PI_GLOBAL: the scripts' `trad == 1`
+                                branch, lam += rho e + D then the same saturation / back-calculation
+                                (casadi_old_PI_ADMM/main.py:138-139, ADMM_CVX_..._adp_PI_antiwindup1.m:131-132) */
+  /* ABI 7: the adaptive-gain global PI (ADMM_CVX_two_veh_intesection_adp_PI_antiwindup1.m:121-147) */
+  int32_t ki_adapt;          /* 1: K_I = kI / d_min (K_I_coeff / dis_min, :127); 0: K_I = kI (casadi_old :135) */
+  int32_t reserved1;
+  double d_gain;             /* S += K_I e + d_gain D: 2 (casadi_old_PI_ADMM/main.py:142), 1 (adp :135) */
+  double dual_init;          /* hat, lam and last_hat at every MPC step's start: 0 (casadi/main.py:56-63,
+                                casadi_old :49-51) or 1e-4 (adp :59-61) */
 } piadmm_config_t;
 
 typedef struct piadmm_ctx* piadmm_handle_t;
@@ -232,8 +242,10 @@ int32_t piadmm_get_component_counters(piadmm_handle_t h, uint64_t* out, int32_t 
  *     index 0: rk vs eps_pri, 1: sk vs eps_dual, margin = (r - eps) / eps (relative)
  *   PIADMM_TIE_DIST        the distance check       id = pair (-1: unknown), margin = (d - d_eff) / d_eff
  * Each event carries the reference time index of the MPC step and the outer iteration (-1: the
- * step's seeds).  Counts and events accumulate until piadmm_reset_counters; at most
- * PIADMM_TIE_CAP events are kept (*n_events reports the total). */
+ * step's seeds).  Counts and events accumulate until piadmm_reset_counters; the counts are the
+ * totals, and at most PIADMM_TIE_CAP device events (the kernels' decisions) plus PIADMM_TIE_CAP host
+ * events (the host's stop decisions) are kept.  *n_events = the number of events written to
+ * `events` (<= max_events). */
 #define PIADMM_TIE_ROUND_U 0
 #define PIADMM_TIE_ROUND_UHAT 1
 #define PIADMM_TIE_ROUND_SEED 2

@@ -8,6 +8,12 @@
                                two intersection tiles, a 3-vehicle chain (a pair QP beyond 63
                                rows at step 5), the two-vehicle intersection, a lone vehicle
 
+Every QP of these runs is certified: oracle/qp_exact.py's solve() raises unless its answer passes
+the complete KKT certificate (stationarity, feasibility of every row, dual signs, complementarity
+at 1e-9 relative).  Round 4's solver did not certify, and this crossing's step-5 pair QP came out
+infeasible: the fixture was regenerated with the certifying solver (steps 5-11 changed; B-opt
+now equals it at 1e-8 on every step, tests/test_cpu_bopt.py).
+
 The oracle takes minutes for them, too long for a live GPU test; tests/test_gpu_graph.py
 compares libpiadmm's wide dual active set (csrc/pd_qp.h gi_solve_wide) against these files,
 and tests/test_oracle_golden.py re-derives the crossing's first step from the oracle.

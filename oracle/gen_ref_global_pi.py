@@ -9,7 +9,8 @@ them on seeded inputs over several chained outer iterations (sum_err, diff_val a
 PI_ADMM.param.rho carry from one iteration to the next, as in the script):
 
   x_curr_pred / dis_vec / dis_min   casadi_old_PI_ADMM/main.py:128-133
-  K_I, K_P, adaptive rho, PI law    :135-142 (trad = 0: the script's setting, :16)
+  K_I, K_P, adaptive rho, PI law    :135-142 (trad = 0: the script's setting, :16; and trad = 1,
+                                    the plain update with back-calculation, :138-139)
   saturation + back-calculation     :145-151
   residuals                         :154-155
 
@@ -68,14 +69,14 @@ def main(ref_root: str = "/root/reference"):
     _, due = load_reference_rollouts(ref_root)
     rng = np.random.default_rng(20261016)
     recs = []
-    for H in (5, 8, 15, 30):
+    for H, trad in ((5, 0), (8, 0), (15, 0), (30, 0), (5, 1), (15, 1)):
         for rep in range(3):
             param = types.SimpleNamespace(dt=0.1, L=1, num_ho=H, num_veh=2, spd=np.array([4, 8]), rho=1.0,
                                           dis_thres=1.5)
             PI = types.SimpleNamespace(param=param, dynamic_update_edge=functools.partial(
                 due, types.SimpleNamespace(param=param)))
             xt = np.array([[-10, 0, 0], [0, 20, -np.pi / 2]], dtype=np.float64) + rng.uniform(-1, 1, (2, 3)) * [6, 6, 0.3]
-            ns = {"np": np, "PI_ADMM": PI, "xt": xt, "trad": 0, "windup_sat": 20, "sum_err": 0, "diff_val": 0,
+            ns = {"np": np, "PI_ADMM": PI, "xt": xt, "trad": trad, "windup_sat": 20, "sum_err": 0, "diff_val": 0,
                   "dual_var_old": np.zeros((4, H + 1)), "last_iter_hat_pos": np.zeros((4, H + 1))}
             its = []
             for it in range(6):
@@ -86,22 +87,24 @@ def main(ref_root: str = "/root/reference"):
                 S_in = np.array(ns["sum_err"], dtype=np.float64) * np.ones((4, H + 1))
                 D_in = np.array(ns["diff_val"], dtype=np.float64) * np.ones((4, H + 1))
                 rho_in = float(param.rho)
+                lam_in = np.array(ns["dual_var_old"], np.float64)
                 last = ns["last_iter_hat_pos"]
                 ns.update(primal_u=primal_u, pos_old=pos_old, hat_pos_old=hat)
                 for b in ("dist", "law", "windup", "resid"):
                     exec(blocks[b], ns)
                 its.append(dict(primal_u=primal_u, pos_old=pos_old, hat=hat, last=np.array(last, np.float64),
-                                S_in=S_in, D_in=D_in, rho_in=rho_in,
+                                S_in=S_in, D_in=D_in, rho_in=rho_in, lam_in=lam_in,
                                 dual_out=np.array(ns["dual_var_old"], np.float64),
                                 S_out=np.array(ns["sum_err"], np.float64) * np.ones((4, H + 1)),
                                 D_out=np.array(ns["diff_val"], np.float64) * np.ones((4, H + 1)),
                                 rho_out=float(param.rho), dis_vec=np.asarray(ns["dis_vec"]),
                                 error_rk=float(ns["error_rk"]), error_sk=float(ns["error_sk"])))
                 ns["last_iter_hat_pos"] = hat.copy()
-            recs.append(dict(H=H, xt=xt, its=its))
+            recs.append(dict(H=H, xt=xt, its=its, trad=trad))
     flat = {}
     for k, r in enumerate(recs):
         flat[f"c{k}_H"] = np.array(r["H"])
+        flat[f"c{k}_trad"] = np.array(r["trad"])
         flat[f"c{k}_xt"] = r["xt"]
         flat[f"c{k}_n"] = np.array(len(r["its"]))
         for j, it in enumerate(r["its"]):
@@ -110,7 +113,7 @@ def main(ref_root: str = "/root/reference"):
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     np.savez_compressed(OUT, n_cases=np.array(len(recs)),
                         source=np.array("casadi_old_PI_ADMM/main.py:128-133,135-142,145-151,154-155 "
-                                        "(NumPy statements, executed; trad = 0, windup_sat = 20)"), **flat)
+                                        "(NumPy statements, executed; trad = 0 and 1, windup_sat = 20)"), **flat)
     print(f"wrote {OUT} ({len(recs)} cases)")
 
 

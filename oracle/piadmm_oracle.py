@@ -411,8 +411,13 @@ class Oracle:
             # a12: the previous step's duals, edge positions and PI accumulators, shifted
             hat, lam, S, D, last_hat = (shift_horizon(a) for a in self.edge_state)
         else:
-            # casadi/main.py:52-63: reset every MPC step
+            # casadi/main.py:52-63: reset every MPC step (the adaptive-gain script starts hat and
+            # lam at 1e-4, ADMM_CVX_..._adp_PI_antiwindup1.m:58-61: cfg.dual_init)
             hat, lam, S, D, last_hat = (np.zeros((E, 2, 2, H + 1)) for _ in range(5))
+            if cfg.dual_init != 0.0:
+                hat[...] = cfg.dual_init
+                lam[...] = cfg.dual_init
+                last_hat[...] = cfg.dual_init
         active = np.zeros(E, bool)
         iters = np.zeros(self.n_comp, np.int32)
         resid = [[] for _ in range(self.n_comp)]
@@ -577,25 +582,35 @@ def dual_update(cfg, p1, p2, hat_e, lam_e, S_e, D_e, dist):
 
 
 def dual_update_global_pi(cfg, xt, spd, primal_u, v1, v2, pos_old, hat_e, lam_e, S_e, D_e, rho_pi, e):
-    """Global PI with adaptive rho and K_P (``casadi_old_PI_ADMM/main.py:133-151``) for one pair,
+    """Global PI with adaptive rho and K_P (``casadi_old_PI_ADMM/main.py:128-151``) for one pair,
     in place.  d = the pair's distances along the nonlinear rollouts of the x-step controls
-    (``x_curr_pred``, :133-137); K_P = min(theta1/d_min, theta2) (:138, 5 and 2.5), the penalty
-    rho = max(rho_min, min(rho_max, rho_num/d_min)) (:139); lam = S + K_P e, S += K_I e + 2 D
-    (:143-144, S before its update); saturation with back-calculation over the pair (:147-153,
-    ``np.sum(orig != sat) > 0`` over the whole dual array).  Returns dis_vec[1] (the stop
-    check, :156)."""
+    (``x_curr_pred``, :128-133); K_I = 3 (:135), K_P = min(theta1/d_min, theta2) (:136, 5 and
+    2.5), the penalty rho = max(rho_min, min(rho_max, rho_num/d_min)) (:137); lam = S + K_P e,
+    S += K_I e + 2 D (:141-142, S before its update); saturation with back-calculation over the
+    pair (:145-151, ``np.sum(orig != sat) > 0`` over the whole dual array).  Returns dis_vec[1]
+    (the stop check, :157).
+
+    The adaptive-gain variant (``matlab_old_files/ADMM_CVX_two_veh_intesection_adp_PI_antiwindup1.m:
+    121-147``, preset matlab_adp_pi): K_I = K_I_coeff / d_min (``ki_adapt``, :127), K_P = min(5/d_min,
+    3) (:128), S += K_I e + D (``d_gain`` 1, :135).  Both scripts' ``trad == 1`` branch
+    (``pi_trad``; casadi_old :139-140, adp :131-132): lam += rho e + D with the updated rho, then
+    the same saturation."""
     x1, y1, _ = rollout_nonlinear(xt[v1], primal_u[v1], spd[v1], cfg.dt, cfg.L)
     x2, y2, _ = rollout_nonlinear(xt[v2], primal_u[v2], spd[v2], cfg.dt, cfg.L)
     dx, dy = x1 - x2, y1 - y2
     dist = np.sqrt(dx * dx + dy * dy)
     dmin = np.min(dist)
+    kI = cfg.kI / dmin if cfg.ki_adapt else cfg.kI
     kP = min(cfg.theta1 / dmin, cfg.theta2)
     rho_pi[e] = max(cfg.rho_min, min(cfg.rho_max, cfg.rho_num / dmin))
     raw = np.empty_like(lam_e)
     for d, v in enumerate((v1, v2)):
         err = pos_old[v] - hat_e[d]
+        if cfg.pi_trad:
+            raw[d] = lam_e[d] + rho_pi[e] * err + D_e[d]
+            continue
         raw[d] = S_e[d] + kP * err
-        S_e[d] = S_e[d] + cfg.kI * err + 2.0 * D_e[d]
+        S_e[d] = S_e[d] + kI * err + cfg.d_gain * D_e[d]
     if cfg.windup:
         W = cfg.windup_sat
         sat = np.minimum(W, np.maximum(raw, -W))

@@ -1,10 +1,10 @@
 """Exact dense QP solver for the oracle (TEST INFRASTRUCTURE ONLY).
 
 Solves   min 1/2 x'Px + q'x   s.t.   l <= A x <= u
-with P positive semidefinite (positive definite on the null space of the
-working set), by a textbook primal active-set method with exact dense KKT
-solves, followed by a final direct solve of the optimal working set and a KKT
-certificate.
+with P positive semidefinite, by a textbook null-space primal active-set method with exact
+dense linear algebra, followed by a direct solve of the final working set and a complete KKT
+certificate.  ``solve`` never returns an answer that fails the certificate: it raises
+:class:`QPError` instead.
 
 Why an active-set method: the reference hands every subproblem to OSQP through
 ``ca.qpsol("solver", "osqp", ...)`` (``casadi/main.py:96,146``).  OSQP stops at
@@ -13,14 +13,32 @@ eps_abs = eps_rel = 1e-3 and the reference then rounds to 4 decimals
 ~1e-3 accurate.  Parity is therefore defined against the *exact* minimiser of
 the same convex QP, which is unique (P is positive definite in the control
 variables) and certified here by KKT residuals.  This algorithm is deliberately
-different from the build's GPU solver (ADMM + active-set polish), so the two
+different from the build's GPU solver (a dual active set on the hinge form), so the two
 agreeing is evidence about both.
+
+The method (Nocedal & Wright, Algorithm 16.3, null-space form, for a positive SEMIdefinite P):
+  * the working set W is kept linearly independent: the null-space basis Z of A_W comes from a
+    complete QR of the row-normalised A_W', and a row enters W only as the blocking row of a
+    step p with A_W p = 0 and |a_i'p| above rounding, so it is never in span(A_W);
+  * the step is the minimiser of the quadratic on x + null(A_W) when Z'PZ is positive
+    definite along Z'g, and a descent ray of zero curvature otherwise (the pair QP's slack
+    variables: a slack with neither of its rows in W), of unbounded length;
+  * every row outside W enters the ratio test (round 4's solver skipped rows it judged
+    dependent on W and could leave the feasible set);
+  * at a stationary point the multipliers come from A_W'y = -g; the most negative is dropped
+    (Bland's rule -- lowest row index -- after a step of length zero, against cycling on
+    degenerate vertices);
+  * the optimal working set is re-solved directly (one refinement step), and the answer is
+    certified: stationarity, feasibility of EVERY row, dual signs and complementarity, all at
+    1e-9 relative (:func:`certify`).
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may import this.
 """
 from __future__ import annotations
 
 import numpy as np
+
+CERT_TOL = 1e-9
 
 
 class QPError(RuntimeError):
@@ -45,101 +63,172 @@ def kkt_residuals(P, q, A, l, u, x, y):
     return float(stat), float(infeas), float(comp)
 
 
-def solve(P, q, A, l, u, x0, tol=1e-12, max_iter=2000, W0=None):
-    """Primal active-set QP.  ``x0`` must be feasible.  Returns (x, y, working_set).
+def certify(P, q, A, l, u, x, y, tol=CERT_TOL):
+    """Complete KKT certificate at ``tol`` relative; returns the relative residuals
+    (stationarity, infeasibility, complementarity incl. dual signs) or raises QPError.
+
+    stationarity   |P x + q + A'y|_inf <= tol * (1 + max(|q|, |Px|, |A'y|))
+    feasibility    every row: l_i - tol (1 + |l_i|) <= a_i'x <= u_i + tol (1 + |u_i|)
+    dual signs     y_i > 0 only on a finite upper bound, y_i < 0 only on a finite lower bound
+    complementarity |y_i| * slack_i <= tol * (1 + |y|_inf) * (1 + |bound_i|)
+    """
+    Ax = A @ x
+    Px, Aty = P @ x, A.T @ y
+    ssc = 1.0 + max(np.max(np.abs(q), initial=0.0), np.max(np.abs(Px), initial=0.0),
+                    np.max(np.abs(Aty), initial=0.0))
+    stat = float(np.max(np.abs(Px + q + Aty), initial=0.0)) / ssc
+    fu = np.isfinite(u)
+    fl = np.isfinite(l)
+    vu = np.where(fu, (Ax - np.where(fu, u, 0.0)) / (1.0 + np.abs(np.where(fu, u, 0.0))), -np.inf)
+    vl = np.where(fl, (np.where(fl, l, 0.0) - Ax) / (1.0 + np.abs(np.where(fl, l, 0.0))), -np.inf)
+    infeas = float(max(np.max(vu, initial=0.0), np.max(vl, initial=0.0)))
+    ysc = 1.0 + float(np.max(np.abs(y), initial=0.0))
+    comp = 0.0
+    for i in np.nonzero(y)[0]:
+        if y[i] > 0:
+            if not fu[i]:
+                comp = max(comp, y[i] / ysc)
+            else:
+                comp = max(comp, y[i] * abs(u[i] - Ax[i]) / (ysc * (1.0 + abs(u[i]))))
+        else:
+            if not fl[i]:
+                comp = max(comp, -y[i] / ysc)
+            else:
+                comp = max(comp, -y[i] * abs(Ax[i] - l[i]) / (ysc * (1.0 + abs(l[i]))))
+    if not (stat <= tol and infeas <= tol and comp <= tol):
+        raise QPError(f"KKT certificate failed: stationarity {stat:.2e}, infeasibility {infeas:.2e}, "
+                      f"complementarity {comp:.2e} (tol {tol:.0e})")
+    return stat, infeas, comp
+
+
+def _null_space(AWn, n):
+    """Orthonormal basis of null(A_W) from a complete QR of the (independent) normalised rows."""
+    k = AWn.shape[0]
+    if k == 0:
+        return np.eye(n)
+    Q, _ = np.linalg.qr(AWn.T, mode="complete")
+    return Q[:, k:]
+
+
+def solve(P, q, A, l, u, x0, tol=1e-12, max_iter=20000, W0=None):
+    """Primal active-set QP.  ``x0`` must be feasible.  Returns (x, y, working_set), certified.
 
     ``working_set`` is a list of (row, side) with side +1 (upper) / -1 (lower).
     """
     P = np.asarray(P, np.float64)
     q = np.asarray(q, np.float64)
     A = np.asarray(A, np.float64)
+    l = np.asarray(l, np.float64)
+    u = np.asarray(u, np.float64)
     n, m = q.size, A.shape[0]
     x = np.array(x0, np.float64, copy=True)
-    scale = 1.0 + np.max(np.abs(np.concatenate([l[np.isfinite(l)], u[np.isfinite(u)], [0.0]])))
-    feas_tol = 1e-12 * scale
+    rn = np.linalg.norm(A, axis=1)
+    rn_safe = np.where(rn > 0, rn, 1.0)
+    An = A / rn_safe[:, None]
+    bsc_u = 1.0 + np.abs(np.where(np.isfinite(u), u, 0.0))
+    bsc_l = 1.0 + np.abs(np.where(np.isfinite(l), l, 0.0))
     Ax = A @ x
-    if np.any(Ax > u + 1e-9 * scale) or np.any(Ax < l - 1e-9 * scale):
+    if np.any(Ax - u > 1e-9 * bsc_u) or np.any(l - Ax > 1e-9 * bsc_l):
         raise QPError("starting point infeasible")
 
-    W: list[tuple[int, int]] = []
-    row_norm = np.linalg.norm(A, axis=1)
-
-    def independent(rows, cand):
+    def rank_ok(rows):
         if not rows:
-            return np.any(A[cand] != 0)
-        M = A[rows + [cand]]
-        return np.linalg.matrix_rank(M, tol=1e-10) == len(rows) + 1
+            return True
+        s = np.linalg.svd(An[rows], compute_uv=False)
+        return s[-1] > 1e-9 * s[0]
 
-    cand = W0 if W0 is not None else []
+    W: list[tuple[int, int]] = []
+    cand = list(W0) if W0 is not None else []
     if W0 is None:
         for i in range(m):
-            if u[i] - Ax[i] <= feas_tol:
+            if rn[i] == 0:
+                continue
+            if np.isfinite(u[i]) and u[i] - Ax[i] <= 1e-13 * bsc_u[i]:
                 cand.append((i, +1))
-            elif Ax[i] - l[i] <= feas_tol:
+            elif np.isfinite(l[i]) and Ax[i] - l[i] <= 1e-13 * bsc_l[i]:
                 cand.append((i, -1))
     for (i, s) in cand:
-        if len(W) < n and independent([r for r, _ in W], i):
+        if len(W) < n and rank_ok([r for r, _ in W] + [i]):
             W.append((i, s))
 
-    at_eqp_min = False
-    degenerate = False      # the last step had length 0: use Bland's rule to avoid cycling
+    degenerate = False      # the last step had length 0: Bland's rule against cycling
+    at_eqp_min = False      # the last step was a full Newton step: x minimises the EQP of W
     for _ in range(max_iter):
         rows = [r for r, _ in W]
         k = len(rows)
-        AW = A[rows] if k else np.zeros((0, n))
         g = P @ x + q
-        K = np.zeros((n + k, n + k))
-        K[:n, :n] = P
-        K[:n, n:] = AW.T
-        K[n:, :n] = AW
-        rhs = np.concatenate([-g, np.zeros(k)])
-        try:
-            sol = np.linalg.solve(K, rhs)
-        except np.linalg.LinAlgError as exc:
-            raise QPError(f"singular KKT with |W|={k}") from exc
-        p, lam = sol[:n], sol[n:]
-        if at_eqp_min or np.max(np.abs(p), initial=0.0) <= 1e-13 * (1.0 + np.max(np.abs(x))):
-            # stationary on the working set: check multiplier signs
-            worst, wj = -1e-12 * (1.0 + np.max(np.abs(lam), initial=0.0)), -1
-            thr = worst
+        Z = _null_space(An[rows], n)
+        p = np.zeros(n)
+        ray = False
+        if Z.shape[1]:
+            Zg = Z.T @ g
+            Hr = Z.T @ P @ Z
+            w, V = np.linalg.eigh(0.5 * (Hr + Hr.T))
+            wmax = max(float(np.max(np.abs(w))), 1e-300)
+            gh = V.T @ Zg
+            gsc = 1.0 + float(np.max(np.abs(g)))
+            zero = w <= 1e-12 * wmax
+            if np.any(zero & (np.abs(gh) > 1e-12 * gsc)):
+                # a descent direction of zero curvature: an unbounded ray until a row blocks
+                d = np.where(zero, -gh, 0.0)
+                p = Z @ (V @ d)
+                ray = True
+            else:
+                d = np.where(zero, 0.0, -gh / np.where(zero, 1.0, w))
+                p = Z @ (V @ d)
+        xsc = 1.0 + float(np.max(np.abs(x)))
+        pn = float(np.linalg.norm(p))
+        if at_eqp_min or (not ray and pn <= 1e-13 * xsc):
+            at_eqp_min = False
+            # stationary on the working set: multipliers from A_W' y = -g
+            if k:
+                lam = np.linalg.lstsq(A[rows].T, -g, rcond=None)[0]
+            else:
+                lam = np.zeros(0)
+            thr = -1e-12 * (1.0 + float(np.max(np.abs(lam), initial=0.0)))
+            wj, worst = -1, thr
             for j, (r, s) in enumerate(W):
                 v = lam[j] * s
                 if degenerate:
-                    # Bland: the wrong-signed row of lowest index
                     if v < thr and (wj < 0 or r < W[wj][0]):
                         wj = j
                 elif v < worst:
                     worst, wj = v, j
             if wj < 0:
-                # optimal working set: re-solve it directly for full accuracy
                 x, y = _solve_eqp(P, q, A, l, u, W)
+                certify(P, q, A, l, u, x, y)
                 return x, y, W
             W.pop(wj)
-            at_eqp_min = False
             continue
+        # ratio test over EVERY row outside the working set
         Ap = A @ p
         Ax = A @ x
-        alpha, block = 1.0, None
-        inW = set(rows)
-        pn = np.linalg.norm(p)
+        inW = np.zeros(m, bool)
+        inW[rows] = True
+        eps = 1e-11 * rn * pn
+        alpha, block = (np.inf if ray else 1.0), None
         for i in range(m):
-            # rows with A_i p ~ 0 (relative) do not move along p; a row that is
-            # linearly dependent on the working set is one of them (degenerate vertex)
-            if i in inW or abs(Ap[i]) <= 1e-10 * row_norm[i] * pn:
+            if inW[i]:
                 continue
-            if Ap[i] > 0 and np.isfinite(u[i]):
-                t = (u[i] - Ax[i]) / Ap[i]
-                if t < alpha and independent(rows, i):
-                    alpha, block = max(t, 0.0), (i, +1)
-            elif Ap[i] < 0 and np.isfinite(l[i]):
-                t = (l[i] - Ax[i]) / Ap[i]
-                if t < alpha and independent(rows, i):
-                    alpha, block = max(t, 0.0), (i, -1)
+            if Ap[i] > eps[i] and np.isfinite(u[i]):
+                t = max((u[i] - Ax[i]) / Ap[i], 0.0)
+                side = +1
+            elif Ap[i] < -eps[i] and np.isfinite(l[i]):
+                t = max((l[i] - Ax[i]) / Ap[i], 0.0)
+                side = -1
+            else:
+                continue
+            if t < alpha:          # ties keep the lowest row index (Bland)
+                alpha, block = t, (i, side)
+        if block is None and ray:
+            raise QPError("unbounded QP (descent ray with no blocking row)")
         x = x + alpha * p
         if block is not None:
+            if len(W) >= n:
+                raise QPError("working set overflow")
             W.append(block)
         degenerate = block is not None and alpha <= 0.0
-        at_eqp_min = block is None    # full step: x minimises the EQP of W
+        at_eqp_min = block is None
     raise QPError("active-set iteration limit")
 
 
@@ -154,9 +243,12 @@ def _solve_eqp(P, q, A, l, u, W):
     K[:n, n:] = AW.T
     K[n:, :n] = AW
     rhs = np.concatenate([-q, bW])
-    sol = np.linalg.solve(K, rhs)
+    try:
+        sol = np.linalg.solve(K, rhs)
+    except np.linalg.LinAlgError as exc:
+        raise QPError(f"singular KKT system of the final working set (|W|={k})") from exc
     # one step of iterative refinement
-    sol += np.linalg.solve(K, np.concatenate([-q, bW]) - K @ sol)
+    sol += np.linalg.solve(K, rhs - K @ sol)
     x, lam = sol[:n], sol[n:]
     y = np.zeros(A.shape[0])
     for j, r in enumerate(rows):

@@ -23,7 +23,7 @@ def test_library_is_built_for_gfx950():
     lib = _lib.load()
     info = lib.piadmm_build_info().decode()
     assert "gfx950" in info
-    assert lib.piadmm_abi_version() == 6
+    assert lib.piadmm_abi_version() == 7
 
 
 def test_exports_every_declared_symbol():
@@ -38,7 +38,7 @@ def test_exports_every_declared_symbol():
 
 def test_config_struct_layout():
     lib = _lib.load()
-    assert lib.piadmm_config_size() == ctypes.sizeof(_lib.PiadmmConfigC) == 288
+    assert lib.piadmm_config_size() == ctypes.sizeof(_lib.PiadmmConfigC) == 312   # ABI 7
     c = _lib.to_c(config.matlab_pi(H=30), n_agents=256, device=3)
     assert (c.n_agents, c.H, c.device, c.dual_mode, c.windup) == (256, 30, 3, 1, 1)
     # every dataclass field the struct carries is mirrored

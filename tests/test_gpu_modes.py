@@ -190,9 +190,9 @@ def test_checkpoint_resume_equals_uninterrupted_run(Solver, tmp_path, kind):
                             17, 20)
     with Solver(cfg, scn) as a:
         full = [a.mpc_step() for _ in range(k1)]
-        path = io.save_checkpoint(str(tmp_path / "ckpt"), a.step_state(), cfg)
+        path = io.save_checkpoint(str(tmp_path / "ckpt"), a.step_state(), cfg, scn)
         full += [a.mpc_step() for _ in range(k2 - k1)]
-    st = io.load_checkpoint(path, cfg)
+    st = io.load_checkpoint(path, cfg, scn)
     assert st["t"] == k1
     if kind != "global_pi":
         assert np.any(st["lam"] != 0.0)            # the carried duals are in the checkpoint

@@ -94,6 +94,30 @@ def test_global_pi_iterations_match_oracle(Solver):
     assert max(n) == cfg.max_outer
 
 
+@pytest.mark.parametrize("preset,trad", [("matlab_adp_pi", 0), ("matlab_adp_pi", 1), ("casadi_old_pi", 1)])
+def test_adaptive_gain_global_pi_iterations_match_oracle(Solver, preset, trad):
+    """The adaptive-gain global PI (matlab_adp_pi: ADMM_CVX_two_veh_intesection_adp_PI_antiwindup1.m
+    :121-147 -- K_I = 3 / d_min, K_P = min(5 / d_min, 3), the back-calculation added once, saturation
+    +-50, hat = lam = 1e-4 at each step's start) and both scripts' trad branch (lam += rho e + D),
+    iteration by iteration through the steps where the saturation engages and the loop runs long
+    (H = 10: up to 100 outer iterations per step), on the graph kernel."""
+    H = 10
+    cfg = config.PRESETS[preset](H=H, pi_trad=trad)
+    n_steps = 22
+    scn = scenario.intersection(H, n_steps=n_steps + 2)
+    orc = O.Oracle(cfg, scn)
+    n, sat = [], False
+    with Solver(cfg, scn) as s:
+        for t in range(n_steps):
+            n.append(step_by_iterations(s, orc, t, check_sd=not trad)[0])
+            sat |= bool(np.any(np.abs(s.state()["lam"]) == cfg.windup_sat))
+        rho = s.step_state()["rho_pi"]
+    np.testing.assert_allclose(rho, orc.rho_pi, rtol=TOL, atol=TOL)
+    assert max(n) >= 20                        # long loops: the PI law's dynamics are exercised
+    if preset == "matlab_adp_pi" and not trad:
+        assert sat                             # the saturation at +-50 engages
+
+
 def test_per_component_stop_keeps_stopped_components(Solver):
     """Several components stopping at different iterations (term_global = 0): a component whose
     stop rule fired keeps its state while the others iterate on; the step's stop comes when the

@@ -72,15 +72,29 @@ def test_checkpoint_round_trip(tmp_path):
     next time index through an .npz written and read without pickles; a checkpoint of another
     configuration is refused."""
     cfg = config.matlab_pi(H=8, warm_duals=1)
-    orc = O.Oracle(cfg, scenario.intersection(8, n_steps=6))
+    scn = scenario.intersection(8, n_steps=6)
+    orc = O.Oracle(cfg, scn)
     for _ in range(3):
         orc.mpc_step()
     hat, lam, S, D, last = orc.edge_state
     st = dict(xt=orc.xt, hat=hat, lam=lam, S=S, D=D, last_hat=last, rho_pi=orc.rho_pi, t=orc.t)
-    path = io.save_checkpoint(str(tmp_path / "c"), st, cfg)
-    back = io.load_checkpoint(path, cfg)
+    path = io.save_checkpoint(str(tmp_path / "c"), st, cfg, scn)
+    back = io.load_checkpoint(path, cfg, scn)
     assert back["t"] == 3
     for k in io.CHECKPOINT_KEYS:
         np.testing.assert_array_equal(back[k], np.asarray(st[k]))
     with pytest.raises(ValueError):
         io.load_checkpoint(path, cfg.replace(H=9))
+    # another scenario with the same agent and pair counts but other pairs: refused
+    other = scenario.crossing(3, 8, n_steps=6, pairs="chain")
+    assert other.n_agents != scn.n_agents or not np.array_equal(other.edges, scn.edges)
+    with pytest.raises(ValueError):
+        io.load_checkpoint(path, cfg, other)
+    # a checkpoint without a fingerprint is refused when the scenario is given
+    bare = io.save_checkpoint(str(tmp_path / "bare"), st, cfg)
+    with pytest.raises(ValueError):
+        io.load_checkpoint(bare, cfg, scn)
+    # non-finite pair state is refused
+    bad = dict(st, lam=np.where(np.arange(lam.size).reshape(lam.shape) == 3, np.nan, lam))
+    with pytest.raises(ValueError):
+        io.load_checkpoint(io.save_checkpoint(str(tmp_path / "nan"), bad, cfg, scn), cfg, scn)

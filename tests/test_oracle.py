@@ -108,6 +108,28 @@ def test_qp_rejects_infeasible_start():
         qp_exact.solve(P, np.zeros(2), np.eye(2), -np.ones(2), np.ones(2), np.array([5.0, 0.0]))
 
 
+def test_h40_crossing_step5_pair_qp_certifies():
+    """The pair QP on which round 4's solver returned an infeasible, non-KKT answer without raising
+    (the H = 40 four-vehicle crossing, step 5, iteration 0: 238 rows, 120 variables in slack form;
+    it violated the steering box by 1.75 rad with complementarity 34 -- its ratio test skipped rows
+    it judged dependent on the working set).  The null-space active set returns a certified answer:
+    every row feasible, stationarity / dual signs / complementarity at 1e-9 relative, a saturated
+    working set of 78 rows."""
+    d = load("qp_pair_H40_crossing_step5.npz")
+    P, q, A, lo, hi, x0 = d["P"], d["q"], d["A"], d["l"], d["u"], d["x0"]
+    x, y, W = qp_exact.solve(P, q, A, lo, hi, x0)
+    stat, infeas, comp = qp_exact.certify(P, q, A, lo, hi, x, y)
+    assert max(stat, infeas, comp) <= 1e-12
+    assert np.all(A @ x <= hi + 1e-12) and np.all(A @ x >= lo - 1e-12)
+    assert np.max(np.abs(x[:80])) <= np.pi / 6 + 1e-12
+    assert len(W) > 63                       # beyond one row per lane: the GPU's wide dual active set
+    # the certificate rejects a perturbed answer (it is what solve() applies before returning)
+    with pytest.raises(qp_exact.QPError):
+        qp_exact.certify(P, q, A, lo, hi, x + 1e-6, y)
+    with pytest.raises(qp_exact.QPError):
+        qp_exact.certify(P, q, A, lo, hi, x, -y)
+
+
 # ---------------------------------------------------------------- loop semantics
 @pytest.mark.parametrize("name", ["casadi_default_H10", "casadi_default_H15", "matlab_pi_H10", "matlab_pi_H8"])
 def test_oracle_runs_reproduce_fixtures(name):
@@ -257,18 +279,20 @@ def test_global_pi_law_matches_reference_statements():
     fused multiply-adds is platform-dependent (1 ulp in d_min, hence in K_P and rho)."""
     d = np.load(os.path.join(GOLD, "ref_global_pi.npz"))
     assert "casadi_old_PI_ADMM/main.py" in str(d["source"])
-    n_sat = 0
+    n_sat = n_trad = 0
     for k in range(int(d["n_cases"])):
         H = int(d[f"c{k}_H"])
         xt = d[f"c{k}_xt"]
-        cfg = config.casadi_old_pi(H=H)
+        trad = int(d[f"c{k}_trad"])
+        cfg = config.casadi_old_pi(H=H, pi_trad=trad)
+        n_trad += trad
         for j in range(int(d[f"c{k}_n"])):
             g = lambda n: d[f"c{k}_i{j}_{n}"]   # noqa: E731
             pos = g("pos_old").reshape(2, 2, H + 1)
             hat = g("hat").reshape(2, 2, H + 1).copy()
             S = g("S_in").reshape(2, 2, H + 1).copy()
             D = g("D_in").reshape(2, 2, H + 1).copy()
-            lam = np.zeros((2, 2, H + 1))
+            lam = g("lam_in").reshape(2, 2, H + 1).copy()
             rho = np.array([float(g("rho_in"))])
             dchk = O.dual_update_global_pi(cfg, xt, np.array([4.0, 8.0]), g("primal_u"), 0, 1, pos, hat, lam, S, D, rho, 0)
             rk, sk = O.pair_residuals_global_pi(pos[0], pos[1], hat, g("last").reshape(2, 2, H + 1), rho[0])
@@ -281,3 +305,64 @@ def test_global_pi_law_matches_reference_statements():
             np.testing.assert_allclose([rk, sk], [float(g("error_rk")), float(g("error_sk"))], **tol)
             n_sat += int(np.any(g("D_out") != 0))
     assert n_sat > 0          # the back-calculation branch is exercised
+    assert n_trad > 0         # and the trad branch (lam += rho e + D)
+
+
+@pytest.mark.parametrize("trad", [0, 1])
+def test_adaptive_gain_law_equals_the_matlab_statements(trad):
+    """The adaptive-gain global PI (matlab_adp_pi) against a line-by-line NumPy transliteration of
+    ADMM_CVX_two_veh_intesection_adp_PI_antiwindup1.m:121-152 (MATLAB is absent: parity with the
+    script's own execution is unpinned; this pins the oracle to its statements): K_I = 3 / dis_min,
+    K_P = min(5 / dis_min, 3), rho = max(1, min(5, 4 / dis_min)), lam = sum_err + K_P e and
+    sum_err += K_I e + diff_val (diff_val ONCE), or lam += rho e + diff_val (trad); saturation +-50
+    with diff_val over the whole array; residuals over both vehicles, no factor 2."""
+    rng = np.random.default_rng(7 + trad)
+    H = 10
+    cfg = config.matlab_adp_pi(H=H, pi_trad=trad)
+    spd = np.array([4.0, 8.0])
+    xt = np.array([[-10.0, 0.0, 0.0], [0.0, 20.0, -np.pi / 2]]) + rng.uniform(-1, 1, (2, 3)) * [4, 4, 0.2]
+    # the script's state (2 vehicles: 4 x (H+1) arrays), carried over chained iterations
+    sum_err, diff_val, rho_m = 0.0, 0.0, 1.0
+    dual = 1e-4 * np.ones((4, H + 1))
+    last = 1e-4 * np.ones((4, H + 1))
+    # the oracle's pair state
+    lam, S, D = dual.reshape(2, 2, H + 1).copy(), np.zeros((2, 2, H + 1)), np.zeros((2, 2, H + 1))
+    rho = np.array([1.0])
+    n_sat = 0
+    for it in range(8):
+        primal_u = np.round(rng.uniform(-np.pi / 6, np.pi / 6, size=(2, H)), 4)
+        pos_old = rng.normal(0, 3, size=(4, H + 1))
+        hat = pos_old + rng.normal(0, 6 if it % 2 else 25, size=(4, H + 1))
+        # --- the MATLAB statements, :121-152
+        xs, ys = zip(*[O.rollout_nonlinear(xt[v], primal_u[v], spd[v], 0.1, 1.0)[:2] for v in range(2)])
+        pos_veh1, pos_veh2 = np.vstack((xs[0], ys[0])), np.vstack((xs[1], ys[1]))
+        dis_vec = np.sqrt(np.diag((pos_veh1 - pos_veh2).T @ (pos_veh1 - pos_veh2)))
+        dis_min = np.min(dis_vec)
+        K_I = 3 / dis_min
+        K_P = min(5 / dis_min, 3)
+        rho_m = max(1, min(5, 4 / dis_min))
+        if trad == 1:
+            dual = dual + rho_m * (pos_old - hat) + diff_val
+        else:
+            dual = sum_err + K_P * (pos_old - hat)
+            sum_err = sum_err + K_I * (pos_old - hat) + diff_val
+        ori = dual
+        dual = np.minimum(50, np.maximum(dual, -50))
+        diff_val = (dual - ori) if np.sum(ori != dual) > 0 else 0
+        error_sk = np.sqrt(np.sum((rho_m * (last - hat)) ** 2))
+        error_rk = np.sqrt(np.sum((pos_old - hat) ** 2))
+        # --- the oracle
+        p3, h3 = pos_old.reshape(2, 2, H + 1), hat.reshape(2, 2, H + 1).copy()
+        dchk = O.dual_update_global_pi(cfg, xt, spd, primal_u, 0, 1, p3, h3, lam, S, D, rho, 0)
+        rk, sk = O.pair_residuals_global_pi(p3[0], p3[1], h3, last.reshape(2, 2, H + 1), rho[0])
+        tol = dict(rtol=1e-13, atol=1e-12)
+        np.testing.assert_allclose(lam.reshape(4, -1), dual, **tol)
+        np.testing.assert_allclose(D.reshape(4, -1), np.broadcast_to(diff_val, (4, H + 1)), **tol)
+        if trad == 0:
+            np.testing.assert_allclose(S.reshape(4, -1), np.broadcast_to(sum_err, (4, H + 1)), **tol)
+        np.testing.assert_allclose(rho[0], rho_m, **tol)
+        np.testing.assert_allclose(dchk, dis_vec[1], **tol)
+        np.testing.assert_allclose([rk, sk], [error_rk, error_sk], **tol)
+        n_sat += int(np.any(np.broadcast_to(diff_val, (4, H + 1)) != 0))
+        last = hat.copy()
+    assert n_sat > 0

@@ -34,3 +34,14 @@ print("slowest components (cycles/step): kernel setup_z xstep zstep zqp zred adm
 for k in order[:6]:
     print(f"  comp {k:4d}: " + " ".join(f"{st[k, j]/steps:9.0f}" for j in (9, 1, 2, 6, 7, 8, 14)) +
           f" | {cc[k, 2]/steps:5.2f} {cc[k, 4]/steps:7.1f} {cc[k, 6]/steps:6.1f}")
+
+# per wave (waves 0, 1: agents; 2: the pair; 3: the roller), mean over components, per step
+bufw = (ctypes.c_uint64 * (s.C * 256))()
+s._check(s.lib.piadmm_debug_stamps(s._h, bufw, s.C * 256))
+sw = np.array(bufw, dtype=np.float64).reshape(s.C, 4, 64).mean(axis=0) / steps
+kern = st[:, 9].mean() / steps / 4.0
+print("per wave, mean cycles per component and step (kernel per wave ~ %.0f):" % kern)
+print("  %-12s" % "phase" + "".join("%14s" % w for w in ("agent0", "agent1", "pair", "roller")))
+for i, n in enumerate(NAMES):
+    if np.any(sw[:, i] > 0):
+        print("  %-12s" % n + "".join("%14.0f" % sw[w, i] for w in range(4)))
