@@ -502,6 +502,10 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     const char* xs = std::getenv("PIADMM_X_SOLVER");
     A.x_gi = (xs && std::strcmp(xs, "pdas") == 0) ? 0 : (xs && std::strcmp(xs, "gi") == 0) ? 1
            : (xs && std::strcmp(xs, "gi_warm") == 0) ? 2 : (xs && std::strcmp(xs, "gi_cold_all") == 0) ? 4 : 3;
+    // PIADMM_NO_SPEC=1: the fused kernel's plain loop shape instead of the speculative one (the
+    // two shapes' equality test)
+    const char* ns = std::getenv("PIADMM_NO_SPEC");
+    A.no_spec = (ns && ns[0] == '1') ? 1 : 0;
   }
   A.N = N;
   A.E = n_edges;

@@ -365,11 +365,22 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
   } else {
   bool have = false;          // the x-step of iteration `it` is already in U (a kept speculation)
   int spec_st = 0;
+  // Determinism: the speculative x-step repeats the QP of the x-step in U (hat, lam unchanged
+  // since), so it is only run when that solve was certified without ADMM and left the parametric
+  // tables holding its working set: the repeat is then one cached-table hit -- the same reduced
+  // solve on the same tables and q, certified identically -- and changes no state (labels, tables,
+  // warm iterates, penalty).  A discarded speculation (a z-step or the stop came) gives its one
+  // reduced solve back to the counters, and the next x-step starts from exactly the plain loop's
+  // state.  An INEXACT x-QP (or one that needed ADMM, or whose tables hold another working set)
+  // is never speculated on (tests/test_gpu_modes.py: the two loop shapes are equal).
+  bool spec_ok = false;       // the x-step in U may be repeated speculatively
+  bool spec_ran = false;      // this iteration's speculative x-step ran
   int it = X.it0, phase = 0;  // phase 0: before barrier A(it); 1: before barrier B(it)
   while (it < X.it_end) {
     if (phase == 0) L.iters = it + 1;
     const int tgt = phase == 0 ? it : it + 1;         // the iteration this x-step belongs to
-    const bool dox = own && (phase == 0 ? !have : it + 1 < X.it_end);
+    const bool dox = own && (phase == 0 ? !have : (it + 1 < X.it_end && spec_ok));
+    if (phase == 1) spec_ran = dox;
     // -------- x-step (casadi/main.py:81-106)
     if (dox) {
       unsigned long long t_xs = STAMP_T();
@@ -386,9 +397,13 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
+      const int admm0 = n.admm_x;
       const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && tgt == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
+      // a repeat of this solve may be speculated only if it certified without ADMM and its
+      // working set's tables are held (the repeat is then one table hit)
+      spec_ok = !(stx & PIADMM_QP_INEXACT) && n.admm_x == admm0 && tables_match(qx, lab_x);
       if (phase == 0) {
         status_x |= stx;
         ++n.xqp;
@@ -422,14 +437,16 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     L.aliased = X.vd[3];
     L.dis_chk = *X.vdd;
     if (X.vd[1]) {
+      if (spec_ran && own) n.pdas_x -= 1;   // discarded by the stop: its one table hit
       L.stopped = true;
       break;
     }
     if (__builtin_expect(L.act, 0)) {
       load_cp();                                         // the speculation used the old hat, lam
+      if (spec_ran && own) n.pdas_x -= 1;   // discarded: its one table hit
       have = false;
     } else {
-      have = it + 1 < X.it_end;
+      have = spec_ran;
     }
     ++it;
     phase = 0;
@@ -937,7 +954,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   // is worth taking off the agents' chain -- measured: matlab_pi 256 x H30 0.534 -> 0.518 ms per
   // step; the linearised model's cheap rollout does not pay for the second barrier
   // (casadi_default 64 x H20 0.633 -> 0.677 ms)
-  X.spec = !X.coop && c.pos_model != 0;
+  X.spec = !X.coop && c.pos_model != 0 && !(flags & F_NOSPEC);
   X.roll = X.spec && blockDim.x == NWA * WAVE;   // launch_mpc_step adds the roller wave to this shape
   X.it0 = it0;
   const bool first = X.first;
@@ -1209,7 +1226,10 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     const char* e = std::getenv("PIADMM_NO_ROLLER");
     return e && e[0] == '1';
   }();
-  const int nt = (a.cfg.pos_model != 0 && !no_roller ? NWA : NWT) * WAVE;
+  // PIADMM_NO_SPEC=1 (DevArgs::no_spec): the plain loop shape (three waves) everywhere
+  const bool no_spec = a.no_spec != 0;
+  if (no_spec) flags |= F_NOSPEC;
+  const int nt = (a.cfg.pos_model != 0 && !no_roller && !no_spec ? NWA : NWT) * WAVE;
   DevArgs aa = a;
   void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
   return launch_rc(hipLaunchKernel(fn, dim3(a.C), dim3(nt), args, sh, s));

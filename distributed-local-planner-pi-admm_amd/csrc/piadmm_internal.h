@@ -49,6 +49,7 @@ struct DevArgs {
   int pair_warm;            // 1: the pair's dual active set starts from its last active set (PIADMM_PAIR_WARM=0: cold)
   int x_gi;                 // x-step working-set changes by the dual active set (1); the step's first x-QP
                             // without the labels' reduced solve (2), started cold (3); all cold (4); PIADMM_X_SOLVER
+  int no_spec;              // 1: k_mpc_step keeps the plain loop shape (PIADMM_NO_SPEC=1, read at set_scenario)
   // scenario (read-only during a step)
   const double* spd;        // N
   const double* ref;        // N*2*T
@@ -240,6 +241,9 @@ constexpr int F_DEVSTOP = 128;
 // With F_FIRST: only the step init (seeds, per-step pair reset), no iteration -- a component split
 // over workgroups resets the pairs its blocks own before ANY block's first x-step reads them.
 constexpr int F_INITONLY = 256;
+// k_mpc_step: the plain loop shape even where the speculative one would run (PIADMM_NO_SPEC=1; the
+// equality test of the two shapes, tests/test_gpu_modes.py)
+constexpr int F_NOSPEC = 512;
 
 int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 // candidate-pair detection (piadmm_detect.hip)

@@ -7,6 +7,9 @@
   run_matlab_pi_H40_mixed      tests/test_gpu_graph.py::test_mixed_components_and_horizons[40]:
                                two intersection tiles, a 3-vehicle chain (a pair QP beyond 63
                                rows at step 5), the two-vehicle intersection, a lone vehicle
+  run_matlab_pi_H63_tiled2     the lane limit H = 63 (tests/test_gpu_parity.py
+                               test_largest_horizon_against_the_oracle): two seeded intersection
+                               tiles, 8 MPC steps (pair QPs of 189 variables in slack form)
 
 Every QP of these runs is certified: oracle/qp_exact.py's solve() raises unless its answer passes
 the complete KKT certificate (stationarity, feasibility of every row, dual signs, complementarity
@@ -42,9 +45,13 @@ from piadmm import config, scenario  # noqa: E402
 H, K = 40, 12
 NAME = "run_matlab_pi_H40_crossing4"
 MIXED = "run_matlab_pi_H40_mixed"
+H63 = "run_matlab_pi_H63_tiled2"
+STEPS = {NAME: K, MIXED: K, H63: 8}
 
 
 def make(name=NAME):
+    if name == H63:
+        return config.matlab_pi(H=63), scenario.tiled(2, 63, n_steps=12, seed=1)
     if name == NAME:
         return config.matlab_pi(H=H), scenario.crossing(4, H, n_steps=K + 2, seed=1)
     if name == MIXED:
@@ -55,8 +62,10 @@ def make(name=NAME):
     raise KeyError(name)
 
 
-def run(name=NAME, n_steps=K):
+def run(name=NAME, n_steps=None):
     cfg, scn = make(name)
+    n_steps = STEPS[name] if n_steps is None else n_steps
+    H = cfg.H
     orc = O.Oracle(cfg, scn)
     M = cfg.max_outer
     out = {k: [] for k in ("xt", "u", "iters", "resid")}
@@ -77,7 +86,7 @@ def run(name=NAME, n_steps=K):
 
 
 if __name__ == "__main__":
-    for name in sys.argv[1:] or [NAME, MIXED]:
+    for name in sys.argv[1:] or [NAME, MIXED, H63]:
         res = run(name)
         path = os.path.join(ROOT, "tests", "golden", name + ".npz")
         np.savez_compressed(path, **res)

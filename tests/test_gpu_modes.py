@@ -240,3 +240,48 @@ def test_fp32_tables_config5_tolerance_study(Solver):
           f"rel dxt {dx_g:.2e}, iteration-count changes {it_changes}; counters {c32}")
     assert it_changes == 0
     assert max(du_o, dx_o, du_g, dx_g) <= 1e-5
+
+
+@pytest.mark.parametrize("case", ["bench_fixed", "natural", "inexact"])
+def test_speculative_loop_equals_plain_loop(Solver, monkeypatch, case):
+    """The fused kernel's speculative loop shape (the agent waves solve iteration it+1's x-step
+    while the pair wave rolls out, tests and decides iteration it; casadi/main.py:81-181) against
+    the plain one (PIADMM_NO_SPEC=1): the same iteration counts, QP status and work counters, and
+    states, controls and residual histories equal to rounding (1e-10: the two shapes are separately
+    inlined copies of the same statements, whose floating-point contractions the compiler may
+    schedule differently -- up to 1.4e-12 observed on the controls).  A speculation repeats a certified x-QP only; a
+    discarded one gives its work and the warm ADMM state back and leaves no table the plain loop
+    would not hold, so even uncertified (ADMM-capped) x-QPs see the plain loop's state.  Cases:
+    the bench's tiles (matlab_pi 256 x H30 shape, fixed 100 outer iterations), natural
+    per-component termination, and x-QPs forced uncertified (PIADMM_X_SOLVER=pdas with 3 ADMM
+    iterations: INEXACT answers depend on the warm state, which the speculation must not touch)."""
+    H = 30 if case == "bench_fixed" else 15
+    kw = dict(H=H)
+    if case == "bench_fixed":
+        kw.update(fixed_iters=1, term_global=1)
+    if case == "inexact":
+        kw.update(max_inner=3, fixed_iters=1, max_outer=12)
+        monkeypatch.setenv("PIADMM_X_SOLVER", "pdas")
+    cfg = config.matlab_pi(**kw)
+    n_tiles, n_steps = (32, 6) if case == "bench_fixed" else (16, 14)
+    scn = scenario.tiled(n_tiles, H, n_steps=n_steps + 2, seed=5)
+    runs = []
+    for nospec in ("0", "1"):
+        monkeypatch.setenv("PIADMM_NO_SPEC", nospec)
+        with Solver(cfg, scn) as s:
+            recs = [s.mpc_step() for _ in range(n_steps)]
+            runs.append((recs, s.counters(), s.state()))
+    (ra, ca, sa), (rb, cb, sb) = runs
+    tol = dict(rtol=1e-10, atol=1e-10)
+    for k, (a, b) in enumerate(zip(ra, rb)):
+        for f in ("iters", "status"):
+            np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f"{f} at step {k}")
+        for f in ("xt", "u", "resid"):
+            np.testing.assert_allclose(getattr(a, f), getattr(b, f), err_msg=f"{f} at step {k}", **tol)
+    for f in ("pos_old", "hat", "lam", "S", "D"):
+        np.testing.assert_allclose(sa[f], sb[f], err_msg=f, **tol)
+    assert ca == cb
+    if case == "inexact":
+        assert ca["inexact"] > 0                 # the uncertified path is exercised
+    else:
+        assert ca["inexact"] == 0

@@ -92,10 +92,31 @@ def test_horizon_limits_match_oracle(Solver, H):
             close(rg.u, ro.u)
 
 
-def test_largest_horizon_certified_and_tile_independent(Solver):
-    """H = 63 (the lane limit; the oracle's slack-form active set cycles on some of its pair
-    QPs, so parity there rests on the GPU's own KKT certificates): every QP certified, two
-    identical tiles bit-identical, the plan inside the steering box and rate limits."""
+def test_largest_horizon_against_the_oracle(Solver):
+    """H = 63 (the lane limit) against the oracle's golden run (oracle/gen_golden_wide.py
+    run_matlab_pi_H63_tiled2: two seeded intersection tiles, 8 MPC steps, every oracle QP
+    certified -- pair QPs of 189 variables in slack form, which round 4's oracle solver could
+    not finish): states and controls at 1e-8, iteration counts and residual histories equal,
+    every GPU QP certified, the plans inside the steering box and rate limits."""
+    from oracle import gen_golden_wide as G
+    g = np.load(os.path.join(GOLD, G.H63 + ".npz"))
+    cfg, scn = G.make(G.H63)
+    with Solver(cfg, scn) as s:
+        for k in range(int(g["n_steps"])):
+            r = s.mpc_step()
+            np.testing.assert_array_equal(r.status, 0, err_msg=f"step {k}")
+            np.testing.assert_array_equal(r.iters, g["iters"][k], err_msg=f"step {k}")
+            close(r.xt, g["xt"][k])
+            close(r.u, g["u"][k])
+            for c in range(s.C):
+                n = int(g["iters"][k][c])
+                close(r.resid[c, :n], g["resid"][k][c][:n])
+            assert np.all(np.abs(r.u) <= cfg.u_max + 1e-9)
+            assert np.all(np.abs(np.diff(r.u, axis=1)) <= cfg.du_max + 1e-9)
+
+
+def test_largest_horizon_tile_independent(Solver):
+    """H = 63: two identical tiles stay bit-identical over 8 steps."""
     H = 63
     cfg = config.matlab_pi(H=H)
     scn = scenario.tiled(2, H, n_steps=12, perturb=False)
@@ -105,8 +126,6 @@ def test_largest_horizon_certified_and_tile_independent(Solver):
             np.testing.assert_array_equal(r.status, 0)
             np.testing.assert_array_equal(r.xt[0:2], r.xt[2:4])
             np.testing.assert_array_equal(r.u[0:2], r.u[2:4])
-            assert np.all(np.abs(r.u) <= cfg.u_max + 1e-9)
-            assert np.all(np.abs(np.diff(r.u, axis=1)) <= cfg.du_max + 1e-9)
 
 
 def test_isolated_agents_and_pairs_mixed(Solver):
