@@ -25,6 +25,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -643,14 +644,12 @@ __device__ int gi_solve(Ws& S, int& steps) {
 // ---------------------------------------------------------------------------------------------
 // the SQP
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs, int n,
-                                                 double* __restrict__ out, int* __restrict__ ist,
-                                                 unsigned long long* __restrict__ stamps, WsG* __restrict__ qg) {
-  __shared__ Ws S;
+// One local NLP (record pb) on this wave; S is the workgroup's LDS state (reinitialised here).
+__device__ __forceinline__ void sqp_one(Ws& S, int pb, const double* __restrict__ recs, double* __restrict__ out,
+                                        int* __restrict__ ist, unsigned long long* __restrict__ stamps,
+                                        WsG* __restrict__ qg) {
   OST_DECL
   const int lane = threadIdx.x;
-  const int pb = blockIdx.x;
-  if (pb >= n) return;
   WsG& Q = qg[pb];
   const double* rec = recs + (size_t)pb * REC;
 
@@ -1152,6 +1151,21 @@ __global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs
 #endif
 }
 
+// Workgroup b (one wave) solves problem order[b]: the workgroup dispatcher starts workgroups in
+// index order as the CUs' slots free up, so `order` -- the host's longest-first schedule from the
+// last solve's work (piadmm_obca_run) -- makes the launch a longest-processing-time-first list
+// schedule: the long problems start while the CUs are full and the short ones fill in behind
+// them, instead of a long problem placed last setting the launch's end.
+__global__ void __launch_bounds__(64) k_obca_sqp(const double* __restrict__ recs, int n,
+                                                 double* __restrict__ out, int* __restrict__ ist,
+                                                 unsigned long long* __restrict__ stamps, WsG* __restrict__ qg,
+                                                 const int* __restrict__ order) {
+  __shared__ Ws S;
+  if ((int)blockIdx.x >= n) return;
+  const int pb = order[blockIdx.x];
+  sqp_one(S, pb, recs, out, ist, stamps, qg);
+}
+
 }  // namespace obca
 
 // ---------------------------------------------------------------------------------------------
@@ -1166,6 +1180,10 @@ struct piadmm_obca_s {
   int* d_ist = nullptr;
   obca::WsG* d_qg = nullptr;   // per-problem linearisation blocks (HBM)
   unsigned long long* d_stamps = nullptr;
+  int* d_order = nullptr;       // the launch's problem order (longest first; cap ints)
+  std::vector<int> order;       // host copy of the order
+  std::vector<int> cost;        // the last solve's status / SQP iterations / QP steps per problem
+  int cost_n = 0;               // batch size of the last solve (0: none yet)
   int cap = 0, n = 0;
   std::string err;
 };
@@ -1194,6 +1212,10 @@ int ensure(piadmm_obca_t h, int n) {
   OHIP(h, hipMalloc(&h->d_out, (size_t)n * obca::OUT * sizeof(double)));
   OHIP(h, hipMalloc(&h->d_ist, (size_t)n * 3 * sizeof(int)));
   OHIP(h, hipMalloc(&h->d_qg, (size_t)n * sizeof(obca::WsG)));
+  if (h->d_order) (void)hipFree(h->d_order);
+  h->d_order = nullptr;
+  h->cost_n = 0;
+  OHIP(h, hipMalloc(&h->d_order, (size_t)n * sizeof(int)));
   h->cap = n;
   return 0;
 }
@@ -1209,10 +1231,39 @@ int check_recs(piadmm_obca_t h, const double* recs, int n) {
   return 0;
 }
 
+// The schedule of the next launches: problems by decreasing work of the last solve of this batch
+// size (QP steps, then SQP iterations; the index breaks ties), or in index order when none ran
+// yet.  The work each problem does does not depend on the order (tests/test_gpu_obca.py).
+int schedule(piadmm_obca_t h) {
+  const int n = h->n;
+  h->order.resize(n);
+  for (int i = 0; i < n; ++i) h->order[i] = i;
+  if (h->cost_n == n) {
+    // the last solve's work (waits for its launches: the batch is rescheduled between runs)
+    h->cost.resize((size_t)3 * n);
+    OHIP(h, hipMemcpyAsync(h->cost.data(), h->d_ist, (size_t)n * 3 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    OHIP(h, hipStreamSynchronize(h->stream));
+    const int* c = h->cost.data();
+    std::stable_sort(h->order.begin(), h->order.end(), [&](int a, int b) {
+      if (c[3 * a + 2] != c[3 * b + 2]) return c[3 * a + 2] > c[3 * b + 2];
+      return c[3 * a + 1] > c[3 * b + 1];
+    });
+  }
+  OHIP(h, hipStreamSynchronize(h->stream));    // no earlier launch still reads the order
+  OHIP(h, hipMemcpy(h->d_order, h->order.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice));
+  return 0;
+}
+
 int launch(piadmm_obca_t h) {
   hipLaunchKernelGGL(obca::k_obca_sqp, dim3(h->n), dim3(64), 0, h->stream, h->d_rec, h->n, h->d_out, h->d_ist,
-                     h->d_stamps, h->d_qg);
+                     h->d_stamps, h->d_qg, h->d_order);
   OHIP(h, hipGetLastError());
+  return 0;
+}
+
+// After the launches of a run: their work becomes the next run's schedule.
+int record_cost(piadmm_obca_t h) {
+  h->cost_n = h->n;
   return 0;
 }
 }  // namespace
@@ -1241,6 +1292,7 @@ int32_t piadmm_obca_destroy(piadmm_obca_t h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->d_rec) { (void)hipFree(h->d_rec); (void)hipFree(h->d_out); (void)hipFree(h->d_ist); (void)hipFree(h->d_qg); }
   if (h->d_stamps) (void)hipFree(h->d_stamps);
+  if (h->d_order) (void)hipFree(h->d_order);
   if (h->e0) (void)hipEventDestroy(h->e0);
   if (h->e1) (void)hipEventDestroy(h->e1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1269,15 +1321,17 @@ int32_t piadmm_obca_run(piadmm_obca_t h, int32_t repeats) {
   if (!h) return PIADMM_E_ARG;
   if (h->n <= 0) return fail(h, PIADMM_E_STATE, "obca_run before obca_upload");
   OHIP(h, hipSetDevice(h->device));
+  if (int rc = schedule(h)) return rc;
   for (int r = 0; r < repeats; ++r)
     if (int rc = launch(h)) return rc;
-  return 0;
+  return record_cost(h);
 }
 
 int32_t piadmm_obca_time(piadmm_obca_t h, int32_t repeats, float* ms) {
   if (!h || !ms || repeats <= 0) return PIADMM_E_ARG;
   if (h->n <= 0) return fail(h, PIADMM_E_STATE, "obca_time before obca_upload");
   OHIP(h, hipSetDevice(h->device));
+  if (int rc = schedule(h)) return rc;
   OHIP(h, hipEventRecord(h->e0, h->stream));
   for (int r = 0; r < repeats; ++r)
     if (int rc = launch(h)) return rc;
@@ -1286,7 +1340,7 @@ int32_t piadmm_obca_time(piadmm_obca_t h, int32_t repeats, float* ms) {
   float t = 0.f;
   OHIP(h, hipEventElapsedTime(&t, h->e0, h->e1));
   *ms = t / (float)repeats;
-  return 0;
+  return record_cost(h);
 }
 
 int32_t piadmm_obca_download(piadmm_obca_t h, double* out, int32_t* status3, int32_t n) {

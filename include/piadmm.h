@@ -342,7 +342,10 @@ int32_t piadmm_obca_destroy(piadmm_obca_t h);
 const char* piadmm_obca_last_error(piadmm_obca_t h);
 /* upload + one launch + download (synchronous) */
 int32_t piadmm_obca_solve(piadmm_obca_t h, const double* recs, int32_t n, double* out, int32_t* status3);
-/* resident batch: upload once, launch (async on the handle's stream), time, download */
+/* resident batch: upload once, launch (async on the handle's stream), time, download.  Block b of
+ * a launch solves problem order[b]: longest first by the QP steps each problem took in the last run
+ * of a batch of the same size (index order before any), so the longest problems start in the first
+ * dispatch wave; the answers do not depend on the order. */
 int32_t piadmm_obca_upload(piadmm_obca_t h, const double* recs, int32_t n);
 int32_t piadmm_obca_run(piadmm_obca_t h, int32_t repeats);
 int32_t piadmm_obca_time(piadmm_obca_t h, int32_t repeats, float* ms_per_launch);
