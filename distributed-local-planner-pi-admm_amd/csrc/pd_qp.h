@@ -1287,6 +1287,128 @@ __device__ __forceinline__ void y_axpy(double* Y, int H, double* vbuf_, double c
   wsync();
 }
 
+// ---- Row-access passes (graph kernel, LDS mode: gi_solve<NV, true>).  Lane a walks ROW a of the
+// symmetric S^-1 (the same matrix and storage; stride ld rounded up to even, so each row starts
+// on 16 bytes) and of the transposed columns Yt[v*H + l][a] (stride YLD), two doubles per LDS
+// access (ds_read_b128 / ds_write_b128) instead of one: tools/gi_ubench.hip measured the m = 50
+// passes at 1312 / 1836 / 3336 cycles (S^-1 v / Y axpy / bordering) against 2212 / 2920 / 5252
+// for the lane = column passes.  Row entries beyond m hold other data (the region also serves
+// the PDAS factor), so the last partial batch masks them.
+typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) dv2 ldsd2;
+constexpr int YLD = GYLD;   // stride of the transposed dual active-set columns (>= 63 + 1, even)
+__device__ __forceinline__ int rows_ld(int fld) { return (fld + 1) & ~1; }
+
+// row[j] += coef * vb[j] over j < m (one lane's row of S^-1; the last batch's entries beyond m
+// are written back unchanged: vb is zero there)
+__device__ __forceinline__ void rank1_row(ldsd* row_, const ldsd* vb, double coef, int m_) {
+  const int m = unif(m_);
+  ldsd2* row = (ldsd2*)row_;
+  const ldsd2* v2 = (const ldsd2*)vb;
+  for (int j0 = 0; j0 < m; j0 += 8) {
+    dv2 sv[4], wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sv[u] = row[(j0 >> 1) + u];
+      wv[u] = v2[(j0 >> 1) + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sv[u].x += wv[u].x * coef;
+      sv[u].y += wv[u].y * coef;
+      row[(j0 >> 1) + u] = sv[u];
+    }
+  }
+}
+
+__device__ __forceinline__ double sinv_rows(double* Si_, int ld_, double* vbuf_, double v, int m_) {
+  const int l = lid();
+  const int m = unif(m_), ld = unif(ld_);
+  ldsd* vb = lds_ptr(vbuf_);
+  put_bcast(vb, v, m);
+  const ldsd2* row = (const ldsd2*)(lds_ptr(Si_) + ((l < m) ? l : 0) * ld);
+  const ldsd2* v2 = (const ldsd2*)vb;
+  double a0 = 0.0, a1 = 0.0;
+  const int mf = m & ~7;
+  for (int j0 = 0; j0 < mf; j0 += 8) {
+    dv2 sv[4], wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sv[u] = row[(j0 >> 1) + u];
+      wv[u] = v2[(j0 >> 1) + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0 += sv[u].x * wv[u].x;
+      a1 += sv[u].y * wv[u].y;
+    }
+  }
+  if (mf < m) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (mf + 2 * u < m) {
+        const dv2 sv = row[(mf >> 1) + u], wv = v2[(mf >> 1) + u];
+        a0 += sv.x * wv.x;
+        if (mf + 2 * u + 1 < m) a1 += sv.y * wv.y;
+      }
+    }
+  }
+  wsync();
+  return (l < m) ? a0 + a1 : 0.0;
+}
+
+// z[v] -= sum_{a < m} coef_a Yt[v*H + l][a] (lane = variable)
+template <int NV>
+__device__ __forceinline__ void y_axpy_rows(double* Y_, int H_, double* vbuf_, double coef, int m_, double* z) {
+  const int l = lid(), H = unif(H_), m = unif(m_);
+  ldsd* vb = lds_ptr(vbuf_);
+  put_bcast(vb, coef, m);
+  const int lc = (l < H) ? l : 0;
+  const ldsd2* yr[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) yr[v] = (const ldsd2*)(lds_ptr(Y_) + (v * H + lc) * YLD);
+  const ldsd2* c2 = (const ldsd2*)vb;
+  const int mf = m & ~7;
+  for (int a0 = 0; a0 < mf; a0 += 8) {
+    dv2 cv[4], yv[4][NV];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      cv[u] = c2[(a0 >> 1) + u];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) yv[u][v] = yr[v][(a0 >> 1) + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) z[v] -= cv[u].x * yv[u][v].x + cv[u].y * yv[u][v].y;
+  }
+  if (mf < m) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (mf + 2 * u < m) {
+        const dv2 cv = c2[(mf >> 1) + u];
+        const bool two = mf + 2 * u + 1 < m;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const dv2 yv = yr[v][(mf >> 1) + u];
+          z[v] -= two ? cv.x * yv.x + cv.y * yv.y : cv.x * yv.x;
+        }
+      }
+    }
+  }
+  wsync();
+}
+
+template <bool ROWS>
+__device__ __forceinline__ double sinv_any(double* Si, int ld, double* vbuf, double v, int m) {
+  if constexpr (ROWS) return sinv_rows(Si, ld, vbuf, v, m);
+  else return sinv_gemv(Si, ld, vbuf, v, m);
+}
+template <int NV, bool ROWS>
+__device__ __forceinline__ void y_axpy_any(double* Y, int H, double* vbuf, double coef, int m, double* z) {
+  if constexpr (ROWS) y_axpy_rows<NV>(Y, H, vbuf, coef, m, z);
+  else y_axpy<NV>(Y, H, vbuf, coef, m, z);
+}
 // P^-1 n for the one-sided constraint (row id, sign sg): lane = variable (one value per vehicle)
 template <int NV>
 __device__ __forceinline__ void pinv_row(const QP<NV>& P, int row, double sg, double* out) {
@@ -1319,7 +1441,7 @@ constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t
 #else
 #define GI_DBG(...) ((void)0)
 #endif
-template <int NV>
+template <int NV, bool ROWS = false>
 __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, signed char* lab, double* x, double* y,
                                          int& nsteps, signed char* flab = nullptr, bool use_wlab = true,
                                          bool prebuild = false) {
@@ -1329,7 +1451,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   // (use_wlab = false: a cold start although wlab points at labels -- a flag, not a null
   // pointer selected at the call site, so that the caller's label array stays in registers)
   constexpr int NR = QP<NV>::NR;
-  const int l = lid(), H = P.H, ld = P.fld, H2 = NV * H;
+  const int l = lid(), H = P.H, ld = ROWS ? rows_ld(P.fld) : P.fld, H2 = NV * H;
   double* vb_ax = P.vb + 192;      // [192, 192 + NR*H): (A v) by row id
   double* vbuf = P.vb + 128;       // [128, 192): broadcast operand of the LDS passes
   int* wc = P.ib;                  // active constraint codes 2*row + side
@@ -1337,6 +1459,9 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   ldsd* Sil = lds_ptr(Si);
   ldsd* vbl = lds_ptr(vbuf);
   double* Y = P.Y;
+  // element (a, v, l) of the dual active-set columns: column a (lane = variable), or row v*H + l
+  // of the transposed layout (ROWS)
+  auto yi = [&](int a, int v, int ll) -> int { return ROWS ? (v * H + ll) * YLD + a : a * H2 + v * H + ll; };
   const int cap = min(P.mmax - 1, P.ycap);
   P.gi_full = false;
   if (P.y_in_k) P.kready = false;  // Y overwrites the K_s^-1 region
@@ -1400,18 +1525,22 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     put_bcast(vbl, r, m);
     if (l < m) {
       const double rl = r * id;
-      ldsd* col = Sil + l;
-      const int mu = unif(m), ldu = unif(ld);
-      for (int j0 = 0; j0 < mu; j0 += SINV_U) {
-        double sv[SINV_U], rv[SINV_U];
+      if constexpr (ROWS) {
+        rank1_row(Sil + l * ld, vbl, rl, m);
+      } else {
+        ldsd* col = Sil + l;
+        const int mu = unif(m), ldu = unif(ld);
+        for (int j0 = 0; j0 < mu; j0 += SINV_U) {
+          double sv[SINV_U], rv[SINV_U];
 #pragma unroll
-        for (int u = 0; u < SINV_U; ++u) {
-          sv[u] = col[unif(min(j0 + u, mu - 1) * ldu)];
-          rv[u] = vbl[j0 + u];
+          for (int u = 0; u < SINV_U; ++u) {
+            sv[u] = col[unif(min(j0 + u, mu - 1) * ldu)];
+            rv[u] = vbl[j0 + u];
+          }
+#pragma unroll
+          for (int u = 0; u < SINV_U; ++u)
+            if (j0 + u < mu) col[unif((j0 + u) * ldu)] = sv[u] + rv[u] * rl;
         }
-#pragma unroll
-        for (int u = 0; u < SINV_U; ++u)
-          if (j0 + u < mu) col[unif((j0 + u) * ldu)] = sv[u] + rv[u] * rl;
       }
       Sil[m * ld + l] = -rl;      // row m, column l
       Sil[l * ld + m] = -rl;      // row l, column m
@@ -1423,7 +1552,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     }
     if (l < H) {
 #pragma unroll
-      for (int v = 0; v < NV; ++v) Y[m * H2 + v * H + l] = yp[v];
+      for (int v = 0; v < NV; ++v) Y[yi(m, v, l)] = yp[v];
     }
     if (l == pk) wbits |= 1 << (2 * ps + (pc & 1));
     ++m;
@@ -1442,18 +1571,22 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     put_bcast(vbl, c, m);
     if (l < m && l != k) {
       const double cl = c / d;
-      ldsd* col = Sil + l;
-      const int mu = unif(m), ldu = unif(ld);
-      for (int j0 = 0; j0 < mu; j0 += SINV_U) {
-        double sv[SINV_U], cv[SINV_U];
+      if constexpr (ROWS) {
+        rank1_row(Sil + l * ld, vbl, -cl, m);
+      } else {
+        ldsd* col = Sil + l;
+        const int mu = unif(m), ldu = unif(ld);
+        for (int j0 = 0; j0 < mu; j0 += SINV_U) {
+          double sv[SINV_U], cv[SINV_U];
 #pragma unroll
-        for (int u = 0; u < SINV_U; ++u) {
-          sv[u] = col[unif(min(j0 + u, mu - 1) * ldu)];
-          cv[u] = vbl[j0 + u];
+          for (int u = 0; u < SINV_U; ++u) {
+            sv[u] = col[unif(min(j0 + u, mu - 1) * ldu)];
+            cv[u] = vbl[j0 + u];
+          }
+#pragma unroll
+          for (int u = 0; u < SINV_U; ++u)
+            if (j0 + u < mu) col[unif((j0 + u) * ldu)] = sv[u] - cv[u] * cl;
         }
-#pragma unroll
-        for (int u = 0; u < SINV_U; ++u)
-          if (j0 + u < mu) col[unif((j0 + u) * ldu)] = sv[u] - cv[u] * cl;
       }
     }
     wsync();
@@ -1474,7 +1607,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       const double ulast = rdl(ua, last);
       if (l < H) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) Y[k * H2 + v * H + l] = Y[last * H2 + v * H + l];
+        for (int v = 0; v < NV; ++v) Y[yi(k, v, l)] = Y[yi(last, v, l)];
       }
       wsync();
       if (l == k) {
@@ -1505,12 +1638,12 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       const double blo = P.hinge(rs) ? 0.0 : ((rs & 1) ? -P.dumax : -P.umax);   // hinge: hi = lo = h
       rhs = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
     }
-    return sinv_gemv(Si, ld, vbuf, rhs, m);
+    return sinv_any<ROWS>(Si, ld, vbuf, rhs, m);
   };
   auto x_of = [&](double lam) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) xc[v] = x0[v];
-    y_axpy<NV>(Y, H, vbuf, lam, m, xc);
+    y_axpy_any<NV, ROWS>(Y, H, vbuf, lam, m, xc);
   };
 
   // On failure (flab != nullptr): the current working set as PDAS labels -- a start for the
@@ -1532,7 +1665,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     double yp[NV];
     const double spp = prep(pc, yp);
     const double va = nvec();
-    const double r = sinv_gemv(Si, ld, vbuf, va, m);
+    const double r = sinv_any<ROWS>(Si, ld, vbuf, va, m);
     const double delta = spp - wsum(va * r);
     if (delta > DEP_TOL * spp) append(pc, yp, r, delta, 0.0);
     if (NV == 2) STAMP_CNT(ST_N_WARMROW, 1);
@@ -1661,14 +1794,14 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       unsigned long long t_gv = STAMP_T();
       if (NV == 2) STAMP_CNT(ST_SUM_M, m);
       const double va = nvec();
-      const double r = sinv_gemv(Si, ld, vbuf, va, m);     // S^-1 N y_p
+      const double r = sinv_any<ROWS>(Si, ld, vbuf, va, m);     // S^-1 N y_p
       if (NV == 2) STAMP_ADD(ST_GI_FWD, t_gv);
       unsigned long long t_yp = STAMP_T();
       // z = y_p - Y r
       double z[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) z[v] = yp[v];
-      y_axpy<NV>(Y, H, vbuf, r, m, z);
+      y_axpy_any<NV, ROWS>(Y, H, vbuf, r, m, z);
       const double lpp2 = spp - wsum(va * r);                  // n_p' z
       if (NV == 2) STAMP_ADD(ST_GI_YPASS, t_yp);
       STAMP_ADD(ST_GI_SOLVE, t_gv);
@@ -1707,7 +1840,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
         {
           const int lc = (l < H) ? l : 0;
 #pragma unroll
-          for (int v = 0; v < NV; ++v) x0[v] += P.beta * Y[k * H2 + v * H + lc];
+          for (int v = 0; v < NV; ++v) x0[v] += P.beta * Y[yi(k, v, lc)];
         }
         drop(k);
         STAMP_ADD(ST_GI_UPD, t_gu);
@@ -1751,7 +1884,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
 #pragma unroll 1
     for (int rf = 0; rf < 3; ++rf) {
       const double dl = eqp_lam(xc);
-      y_axpy<NV>(Y, H, vbuf, dl, m, xc);
+      y_axpy_any<NV, ROWS>(Y, H, vbuf, dl, m, xc);
       lam += dl;
     }
     const int myc = (l < m) ? wc[l] : 0;
@@ -1795,7 +1928,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
         if (l < H)
           for (int a = 0; a < m; ++a)
 #pragma unroll
-            for (int v = 0; v < NV; ++v) sY[a * H2 + v * H + l] = Y[a * H2 + v * H + l];
+            for (int v = 0; v < NV; ++v) sY[a * H2 + v * H + l] = Y[yi(a, v, l)];
         sY[WAVE * H2 + l] = lin ? 1.0 : 0.0;   // the hinge regimes of the final state
       }
     }
@@ -1812,9 +1945,10 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
 // bordering pass each).  The hinge rows' regimes (linear or zero) of that final state come with
 // it, so the solve resumes from exactly the state it ended in.  Not under the global-PI law (the
 // pair's penalty changes every iteration).
+template <bool ROWS = false>
 __device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
   constexpr int NV = 2;
-  const int l = lid(), H = P.H, H2 = NV * H, ld = P.fld;
+  const int l = lid(), H = P.H, H2 = NV * H, ld = ROWS ? rows_ld(P.fld) : P.fld;
   if (!P.snap || !P.gws || !P.gws_warm) return;
   const int gm = P.gws[0], gt = P.gws[1];
   if (gt != P.tstep || gm <= 0 || gm > min(P.mmax - 1, P.ycap)) return;
@@ -1843,7 +1977,7 @@ __device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int w = 0; w < NV; ++w)
-          if (a0 + u < gm) P.Y[(a0 + u) * H2 + w * H + l] = v[u][w];
+          if (a0 + u < gm) P.Y[ROWS ? (w * H + l) * YLD + a0 + u : (a0 + u) * H2 + w * H + l] = v[u][w];
     }
   }
   if (l < gm) P.ib[l] = code;
@@ -2316,7 +2450,7 @@ __device__ __forceinline__ void warm_to_scaled(QP<NV>& P, double* xs, double* zs
 #define PIADMM_ADAPT_EVERY 25
 #endif
 constexpr int ADAPT_EVERY = PIADMM_ADAPT_EVERY;
-template <int NV, bool TWO, int XU = XGEMV_U>
+template <int NV, bool TWO, int XU = XGEMV_U, bool ROWS = false>
 __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
                                         bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
                                         double* x_out, int& n_admm, int& n_pdas, int& n_gi,
@@ -2344,7 +2478,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         int ngi = 0;
         signed char glab[NR];
         ensure_q(P);
-        if (gi_solve(P, flab, glab, x, y, ngi, nullptr, gi_first < 2)) {
+        if (gi_solve<NV, ROWS>(P, flab, glab, x, y, ngi, nullptr, gi_first < 2)) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = glab[s];
           // the dual active set's own answer (exact solve of its final working set + one step
@@ -2385,8 +2519,8 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       int ngi = 0;
       signed char glab[NR];
       signed char clab[NR];
-      if constexpr (NV == 2) gi_snap_restore(P);
-      if (gi_solve(P, nullptr, glab, x, y, ngi, clab)) {
+      if constexpr (NV == 2) gi_snap_restore<ROWS>(P);
+      if (gi_solve<NV, ROWS>(P, nullptr, glab, x, y, ngi, clab)) {
         signed char nl[NR];
         ok = kkt_check(P, glab, x, y, nl);
 #ifdef PIADMM_GI_DEBUG

@@ -130,8 +130,8 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, int it, 
   double ustar[1];
   unsigned long long t_q = STAMP_T();
   const int gi0 = n.gi;
-  const int st = qp_solve<1, false, 8>(qx, xs, zs, ys, lab, warm, c.max_inner, c.polish_every, W.fac, qx.fld, ustar,
-                                       n.admm_x, n.pdas_x, n.gi);
+  const int st = qp_solve<1, false, 8, !BIG>(qx, xs, zs, ys, lab, warm, c.max_inner, c.polish_every, W.fac, qx.fld,
+                                             ustar, n.admm_x, n.pdas_x, n.gi);
   STAMP_ADD(ST_XQP, t_q);
   STAMP_CNT(ST_N_GIX, n.gi - gi0);
   ++n.xqp;
@@ -310,8 +310,8 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
   double uh[2];
   unsigned long long t_zq = STAMP_T();
   const int giz0 = n.gi;
-  const int st = qp_solve<2, BIG>(qe, xs, zs, ys, lab, warm, c.max_inner, c.polish_every, BIG ? Ke : W.fac,
-                                  BIG ? 2 * H : LD, uh, n.admm_z, n.pdas_z, n.gi);
+  const int st = qp_solve<2, BIG, XGEMV_U, !BIG>(qe, xs, zs, ys, lab, warm, c.max_inner, c.polish_every,
+                                                 BIG ? Ke : W.fac, BIG ? 2 * H : LD, uh, n.admm_z, n.pdas_z, n.gi);
   STAMP_ADD(ST_ZQP, t_zq);
   STAMP_CNT(ST_N_GIZ, n.gi - giz0);
   STAMP_CNT(ST_N_ZQP, 1);
@@ -565,7 +565,7 @@ __device__ __forceinline__ void g_step_final(const DevArgs& A, int ci, int w) {
 template <bool BIG, bool TIES>
 __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
                                                 int& nbar) {
-  extern __shared__ double lds[];
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int s_int[GW * 272];
   __shared__ double s_sc[8];
   __shared__ int s_cnt[GW][8];
@@ -577,9 +577,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
   const int e0 = A.comp_eptr[ci], e1 = A.comp_eptr[ci + 1];
   const int a0 = A.comp_aptr[ci], a1 = A.comp_aptr[ci + 1];
   // ---- LDS carve (graph_lds_bytes in piadmm_internal.h)
-  size_t fac_n = 64 * LD;
-  const size_t xr = (size_t)xrows(H) * (xrows(H) + 1);
-  if (xr > fac_n) fac_n = xr;
+  const size_t fac_n = graph_fac(H);       // even counts throughout: every region on 16 bytes
   const size_t ylds_n = graph_ylds(H);
   double* wbase = lds + (size_t)w * (fac_n + 512 + 256 + ylds_n);
   GWave W;

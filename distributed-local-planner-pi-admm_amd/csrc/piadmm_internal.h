@@ -221,13 +221,20 @@ inline __host__ __device__ constexpr size_t giw_stride(int H) {
 constexpr int GZMAX = 1024;   // pairs per component whose colliding pairs are balanced over the waves
 // Dual active-set columns P^-1 n_a in LDS per wave (H <= HMAX; beyond, in HBM): the pair's
 // 2H-long columns (63 of them) or the x-step's H-long ones, in turn.
+// LDS mode stores them transposed (row v*H + l holds the m coefficients of variable l, stride
+// GYLD: pd_qp.h gi_solve<NV, true>), so a lane reads its row two doubles at a time.
 constexpr int GYCAP = 63;
-constexpr size_t graph_ylds(int H) { return H <= HMAX ? (size_t)GYCAP * 2 * H : 0; }
+constexpr int GYLD = 66;
+constexpr size_t graph_ylds(int H) { return H <= HMAX ? (size_t)2 * H * GYLD : 0; }
+// The per-wave factor scratch: the pair's PDAS factor (64 x LD) or its dual active set's S^-1
+// (rows of even stride LD + 1), the x-step's factor or S^-1 (xrows x (xrows + 2) covers both).
+inline __host__ __device__ size_t graph_fac(int H) {
+  size_t fac = 64 * (LD + 1);
+  const size_t xr = (size_t)xrows(H) * (xrows(H) + 2);
+  return xr > fac ? xr : fac;
+}
 inline size_t graph_lds_bytes(int H) {
-  size_t fac = 64 * LD;                                   // pair factor scratch (largest)
-  const size_t xr = (size_t)xrows(H) * (xrows(H) + 1);    // x-step factor scratch (same region)
-  if (xr > fac) fac = xr;
-  return (GW * (fac + 512 + 256 + graph_ylds(H)) + 64) * sizeof(double);  // + vectors, diagonals, Y
+  return (GW * (graph_fac(H) + 512 + 256 + graph_ylds(H)) + 64) * sizeof(double);  // + vectors, diagonals, Y
 }
 // Graph launches also use these flags: F_XPHASE / F_ZPHASE restrict an iteration launch to
 // its x-step or its z-step + termination half (the exchange of a sharded job sits between).
