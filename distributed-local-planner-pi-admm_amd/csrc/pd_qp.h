@@ -1287,7 +1287,7 @@ __device__ __forceinline__ void y_axpy(double* Y, int H, double* vbuf_, double c
   wsync();
 }
 
-// ---- Row-access passes (graph kernel, LDS mode: gi_solve<NV, true>).  Lane a walks ROW a of the
+// ---- Row-access passes (graph kernel, LDS mode: gi_solve<NV, RM_S | RM_Y>).  Lane a walks ROW a of the
 // symmetric S^-1 (the same matrix and storage; stride ld rounded up to even, so each row starts
 // on 16 bytes) and of the transposed columns Yt[v*H + l][a] (stride YLD), two doubles per LDS
 // access (ds_read_b128 / ds_write_b128) instead of one: tools/gi_ubench.hip measured the m = 50
@@ -1296,6 +1296,7 @@ __device__ __forceinline__ void y_axpy(double* Y, int H, double* vbuf_, double c
 // the PDAS factor), so the last partial batch masks them.
 typedef double dv2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) dv2 ldsd2;
+constexpr int RM_S = 1, RM_Y = 2;   // gi_solve's row-access modes
 constexpr int YLD = GYLD;   // stride of the transposed dual active-set columns (>= 63 + 1, even)
 __device__ __forceinline__ int rows_ld(int fld) { return (fld + 1) & ~1; }
 
@@ -1441,7 +1442,8 @@ constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t
 #else
 #define GI_DBG(...) ((void)0)
 #endif
-template <int NV, bool ROWS = false>
+// RM: row-access passes (bit RM_S: S^-1; bit RM_Y: the transposed Y columns); 0 = lane = column
+template <int NV, int RM = 0>
 __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, signed char* lab, double* x, double* y,
                                          int& nsteps, signed char* flab = nullptr, bool use_wlab = true,
                                          bool prebuild = false) {
@@ -1451,7 +1453,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   // (use_wlab = false: a cold start although wlab points at labels -- a flag, not a null
   // pointer selected at the call site, so that the caller's label array stays in registers)
   constexpr int NR = QP<NV>::NR;
-  const int l = lid(), H = P.H, ld = ROWS ? rows_ld(P.fld) : P.fld, H2 = NV * H;
+  constexpr bool RS = (RM & RM_S) != 0, RY = (RM & RM_Y) != 0;
+  const int l = lid(), H = P.H, ld = RS ? rows_ld(P.fld) : P.fld, H2 = NV * H;
   double* vb_ax = P.vb + 192;      // [192, 192 + NR*H): (A v) by row id
   double* vbuf = P.vb + 128;       // [128, 192): broadcast operand of the LDS passes
   int* wc = P.ib;                  // active constraint codes 2*row + side
@@ -1460,8 +1463,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   ldsd* vbl = lds_ptr(vbuf);
   double* Y = P.Y;
   // element (a, v, l) of the dual active-set columns: column a (lane = variable), or row v*H + l
-  // of the transposed layout (ROWS)
-  auto yi = [&](int a, int v, int ll) -> int { return ROWS ? (v * H + ll) * YLD + a : a * H2 + v * H + ll; };
+  // of the transposed layout (RY)
+  auto yi = [&](int a, int v, int ll) -> int { return RY ? (v * H + ll) * YLD + a : a * H2 + v * H + ll; };
   const int cap = min(P.mmax - 1, P.ycap);
   P.gi_full = false;
   if (P.y_in_k) P.kready = false;  // Y overwrites the K_s^-1 region
@@ -1525,7 +1528,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     put_bcast(vbl, r, m);
     if (l < m) {
       const double rl = r * id;
-      if constexpr (ROWS) {
+      if constexpr (RS) {
         rank1_row(Sil + l * ld, vbl, rl, m);
       } else {
         ldsd* col = Sil + l;
@@ -1571,7 +1574,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     put_bcast(vbl, c, m);
     if (l < m && l != k) {
       const double cl = c / d;
-      if constexpr (ROWS) {
+      if constexpr (RS) {
         rank1_row(Sil + l * ld, vbl, -cl, m);
       } else {
         ldsd* col = Sil + l;
@@ -1638,12 +1641,12 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       const double blo = P.hinge(rs) ? 0.0 : ((rs & 1) ? -P.dumax : -P.umax);   // hinge: hi = lo = h
       rhs = (myc & 1) ? -(vb_ax[rw] + blo + blo) : vb_ax[rw];
     }
-    return sinv_any<ROWS>(Si, ld, vbuf, rhs, m);
+    return sinv_any<RS>(Si, ld, vbuf, rhs, m);
   };
   auto x_of = [&](double lam) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) xc[v] = x0[v];
-    y_axpy_any<NV, ROWS>(Y, H, vbuf, lam, m, xc);
+    y_axpy_any<NV, RY>(Y, H, vbuf, lam, m, xc);
   };
 
   // On failure (flab != nullptr): the current working set as PDAS labels -- a start for the
@@ -1665,7 +1668,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     double yp[NV];
     const double spp = prep(pc, yp);
     const double va = nvec();
-    const double r = sinv_any<ROWS>(Si, ld, vbuf, va, m);
+    const double r = sinv_any<RS>(Si, ld, vbuf, va, m);
     const double delta = spp - wsum(va * r);
     if (delta > DEP_TOL * spp) append(pc, yp, r, delta, 0.0);
     if (NV == 2) STAMP_CNT(ST_N_WARMROW, 1);
@@ -1794,14 +1797,14 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       unsigned long long t_gv = STAMP_T();
       if (NV == 2) STAMP_CNT(ST_SUM_M, m);
       const double va = nvec();
-      const double r = sinv_any<ROWS>(Si, ld, vbuf, va, m);     // S^-1 N y_p
+      const double r = sinv_any<RS>(Si, ld, vbuf, va, m);     // S^-1 N y_p
       if (NV == 2) STAMP_ADD(ST_GI_FWD, t_gv);
       unsigned long long t_yp = STAMP_T();
       // z = y_p - Y r
       double z[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) z[v] = yp[v];
-      y_axpy_any<NV, ROWS>(Y, H, vbuf, r, m, z);
+      y_axpy_any<NV, RY>(Y, H, vbuf, r, m, z);
       const double lpp2 = spp - wsum(va * r);                  // n_p' z
       if (NV == 2) STAMP_ADD(ST_GI_YPASS, t_yp);
       STAMP_ADD(ST_GI_SOLVE, t_gv);
@@ -1884,7 +1887,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
 #pragma unroll 1
     for (int rf = 0; rf < 3; ++rf) {
       const double dl = eqp_lam(xc);
-      y_axpy_any<NV, ROWS>(Y, H, vbuf, dl, m, xc);
+      y_axpy_any<NV, RY>(Y, H, vbuf, dl, m, xc);
       lam += dl;
     }
     const int myc = (l < m) ? wc[l] : 0;
@@ -1945,10 +1948,11 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
 // bordering pass each).  The hinge rows' regimes (linear or zero) of that final state come with
 // it, so the solve resumes from exactly the state it ended in.  Not under the global-PI law (the
 // pair's penalty changes every iteration).
-template <bool ROWS = false>
+template <int RM = 0>
 __device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
   constexpr int NV = 2;
-  const int l = lid(), H = P.H, H2 = NV * H, ld = ROWS ? rows_ld(P.fld) : P.fld;
+  constexpr bool RS = (RM & RM_S) != 0, RY = (RM & RM_Y) != 0;
+  const int l = lid(), H = P.H, H2 = NV * H, ld = RS ? rows_ld(P.fld) : P.fld;
   if (!P.snap || !P.gws || !P.gws_warm) return;
   const int gm = P.gws[0], gt = P.gws[1];
   if (gt != P.tstep || gm <= 0 || gm > min(P.mmax - 1, P.ycap)) return;
@@ -1977,7 +1981,7 @@ __device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int w = 0; w < NV; ++w)
-          if (a0 + u < gm) P.Y[ROWS ? (w * H + l) * YLD + a0 + u : (a0 + u) * H2 + w * H + l] = v[u][w];
+          if (a0 + u < gm) P.Y[RY ? (w * H + l) * YLD + a0 + u : (a0 + u) * H2 + w * H + l] = v[u][w];
     }
   }
   if (l < gm) P.ib[l] = code;
@@ -2450,7 +2454,7 @@ __device__ __forceinline__ void warm_to_scaled(QP<NV>& P, double* xs, double* zs
 #define PIADMM_ADAPT_EVERY 25
 #endif
 constexpr int ADAPT_EVERY = PIADMM_ADAPT_EVERY;
-template <int NV, bool TWO, int XU = XGEMV_U, bool ROWS = false>
+template <int NV, bool TWO, int XU = XGEMV_U, int RM = 0>
 __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, double* ys, signed char* lab,
                                         bool warm_lab, int max_inner, int polish_every, double* kscr, int kld,
                                         double* x_out, int& n_admm, int& n_pdas, int& n_gi,
@@ -2478,7 +2482,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         int ngi = 0;
         signed char glab[NR];
         ensure_q(P);
-        if (gi_solve<NV, ROWS>(P, flab, glab, x, y, ngi, nullptr, gi_first < 2)) {
+        if (gi_solve<NV, RM>(P, flab, glab, x, y, ngi, nullptr, gi_first < 2)) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = glab[s];
           // the dual active set's own answer (exact solve of its final working set + one step
@@ -2519,8 +2523,8 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       int ngi = 0;
       signed char glab[NR];
       signed char clab[NR];
-      if constexpr (NV == 2) gi_snap_restore<ROWS>(P);
-      if (gi_solve<NV, ROWS>(P, nullptr, glab, x, y, ngi, clab)) {
+      if constexpr (NV == 2) gi_snap_restore<RM>(P);
+      if (gi_solve<NV, RM>(P, nullptr, glab, x, y, ngi, clab)) {
         signed char nl[NR];
         ok = kkt_check(P, glab, x, y, nl);
 #ifdef PIADMM_GI_DEBUG

@@ -178,7 +178,7 @@ struct WaveCnt {
 // the whole step.  The pair's state never lives here: the pair wave owns it.
 template <bool BIG, bool TIES>
 __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
-  extern __shared__ double lds[];
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   const piadmm_config_t& c = A.cfg;
   const int H = X.H, H1 = X.H1, w = X.w, l = X.l, ci = X.ci, e = X.e, t = X.t;
   const bool big = BIG, f32 = X.f32, first = X.first;
@@ -192,9 +192,9 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     else { Kx = p; p += 2 * H * H; }                     // 2 x H*H   agent K_s^-1
     Gx = p; p += 2 * (H * H + H);                        // 2 x (H*H+H) agent polish G | g
     p += f32 ? 2 * H * H : 4 * H * H;                    // pair K_s^-1 (the pair wave's)
-    p += 64 * LD;                                        // pair scratch (the pair wave's)
-    xfac = p + w * HMAX * (HMAX + 1);                    // NW x HMAX x (HMAX+1)
-    xt_all = p + NW * HMAX * (HMAX + 1);                 // NW x (HMAX+1) x XLD
+    p += 64 * (LD + 1);                                  // pair scratch (the pair wave's)
+    xfac = p + w * HMAX * (HMAX + 2);                    // NW x HMAX x (HMAX+2)
+    xt_all = p + NW * HMAX * (HMAX + 2);                 // NW x (HMAX+1) x XLD
   } else {
     xfac = lds + 64 * LD + w * xrows(H) * (xrows(H) + 1);   // NW x xrows(H) x (xrows+1)
   }
@@ -331,7 +331,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? 0 : RM_S>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && it == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
@@ -398,7 +398,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int admm0 = n.admm_x;
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? 0 : RM_S>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && tgt == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       // a repeat of this solve may be speculated only if it certified without ADMM and its
@@ -510,7 +510,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
 // (casadi/main.py:121-181).  Its QP state stays in this wave's registers for the whole step.
 template <bool BIG, bool TIES>
 __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
-  extern __shared__ double lds[];
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   const piadmm_config_t& c = A.cfg;
   const int H = X.H, H1 = X.H1, l = X.l, ci = X.ci, e = X.e, t = X.t;
   const bool big = BIG, f32 = X.f32, first = X.first;
@@ -620,7 +620,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     signed char ld[5];
     int nd = 0;
     unsigned long long t_pb = STAMP_T();
-    gi_solve(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
+    gi_solve<2, BIG ? 0 : RM_S>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
     STAMP_ADD(ST_ZR_SOLVE, t_pb);
   }
   for (int it = X.it0; it < X.it_end; ++it) {
@@ -702,7 +702,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       unsigned long long t_zq = STAMP_T();
       // K_s^-1 of the pair is built in the LDS scratch and copied (2H <= 64), or in place
       // (big mode, two columns per lane, in HBM)
-      const int ste = qp_solve<2, BIG>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
+      const int ste = qp_solve<2, BIG, XGEMV_U, BIG ? 0 : RM_S>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
                                big ? Ke : scr, big ? 2 * H : LD, uh,
                                n.admm_z, n.pdas_z, n.gi);
       STAMP_ADD(ST_ZQP, t_zq);
@@ -897,7 +897,7 @@ __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
 template <bool BIG, bool TIES>
 __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
                                               int& nbar) {
-  extern __shared__ double lds[];
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int s_int[NWT * 272];   // per wave: x ids [128], z ids [128], fstate x, fstate z
   __shared__ int s_vd[4];
   __shared__ double s_vdd;
@@ -926,7 +926,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   double* vec_all;
   if (!BIG) {
     vec_all = lds + (X.f32 ? kxf_words(H) : 2 * H * H) + 2 * (H * H + H) + (X.f32 ? 2 * H * H : 4 * H * H) +
-              64 * LD + NW * HMAX * (HMAX + 1) + NW * (HMAX + 1) * XLD;   // NWT x 512
+              64 * (LD + 1) + NW * HMAX * (HMAX + 2) + NW * (HMAX + 1) * XLD;   // NWT x 512
   } else {
     vec_all = lds + 64 * LD + NW * xrows(H) * (xrows(H) + 1);             // NWT x 512
   }

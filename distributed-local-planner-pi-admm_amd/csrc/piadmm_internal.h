@@ -182,8 +182,9 @@ inline size_t lds_bytes(int H, int precision = 0) {
     d += f32 ? kxf_words(H) : 2 * (size_t)H * H;   // agent K_s^-1 (2 agents; fp32: half)
     d += 2 * ((size_t)H * H + H);    // agent polish G | g (2 agents)
     d += (f32 ? 2 : 4) * (size_t)H * H;   // pair K_s^-1 (2H x 2H)
-    d += 64 * LD;                    // pair matrix scratch (wave 0)
-    d += NW * HMAX * (HMAX + 1);     // per-wave x-step scratch / Cholesky factor
+    d += 64 * (LD + 1);              // pair matrix scratch (PDAS factor, or the dual active set's
+                                     // S^-1 in rows of even stride: pd_qp.h gi_solve RM_S)
+    d += NW * HMAX * (HMAX + 2);     // per-wave x-step scratch / Cholesky factor / S^-1 rows
     d += NW * (HMAX + 1) * XLD;      // per-wave x-step parametric table X' | beta
   } else {
     d += 64 * LD;                    // pair matrix scratch (wave 0)
