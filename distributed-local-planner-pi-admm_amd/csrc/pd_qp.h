@@ -48,6 +48,7 @@ struct QP {
   double* Y;              // pair: dual active-set columns P^-1 n_a (shares the K_s^-1 region)
   int ycap;               // pair: columns Y holds
   bool y_in_k;            // Y shares the K_s^-1 region (a GI solve invalidates K_s^-1)
+  int yld = GYLD;         // row stride of the transposed Y (gi_solve RM_Y; even, >= ycap)
   bool scaled;            // Ruiz scaling computed (the pair computes it only when ADMM is needed)
   bool wraw;              // the warm ADMM state holds the last certified (x, y) unscaled (zs unset):
                           // converted to the scaled (xs, zs, ys) only when ADMM actually runs
@@ -1289,7 +1290,7 @@ __device__ __forceinline__ void y_axpy(double* Y, int H, double* vbuf_, double c
 
 // ---- Row-access passes (graph kernel, LDS mode: gi_solve<NV, RM_S | RM_Y>).  Lane a walks ROW a of the
 // symmetric S^-1 (the same matrix and storage; stride ld rounded up to even, so each row starts
-// on 16 bytes) and of the transposed columns Yt[v*H + l][a] (stride YLD), two doubles per LDS
+// on 16 bytes) and of the transposed columns Yt[v*H + l][a] (stride P.yld), two doubles per LDS
 // access (ds_read_b128 / ds_write_b128) instead of one: tools/gi_ubench.hip measured the m = 50
 // passes at 1312 / 1836 / 3336 cycles (S^-1 v / Y axpy / bordering) against 2212 / 2920 / 5252
 // for the lane = column passes.  Row entries beyond m hold other data (the region also serves
@@ -1297,7 +1298,6 @@ __device__ __forceinline__ void y_axpy(double* Y, int H, double* vbuf_, double c
 typedef double dv2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) dv2 ldsd2;
 constexpr int RM_S = 1, RM_Y = 2;   // gi_solve's row-access modes
-constexpr int YLD = GYLD;   // stride of the transposed dual active-set columns (>= 63 + 1, even)
 __device__ __forceinline__ int rows_ld(int fld) { return (fld + 1) & ~1; }
 
 // row[j] += coef * vb[j] over j < m (one lane's row of S^-1; the last batch's entries beyond m
@@ -1360,14 +1360,15 @@ __device__ __forceinline__ double sinv_rows(double* Si_, int ld_, double* vbuf_,
 
 // z[v] -= sum_{a < m} coef_a Yt[v*H + l][a] (lane = variable)
 template <int NV>
-__device__ __forceinline__ void y_axpy_rows(double* Y_, int H_, double* vbuf_, double coef, int m_, double* z) {
-  const int l = lid(), H = unif(H_), m = unif(m_);
+__device__ __forceinline__ void y_axpy_rows(double* Y_, int H_, int yld_, double* vbuf_, double coef, int m_,
+                                            double* z) {
+  const int l = lid(), H = unif(H_), m = unif(m_), yld = unif(yld_);
   ldsd* vb = lds_ptr(vbuf_);
   put_bcast(vb, coef, m);
   const int lc = (l < H) ? l : 0;
   const ldsd2* yr[NV];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) yr[v] = (const ldsd2*)(lds_ptr(Y_) + (v * H + lc) * YLD);
+  for (int v = 0; v < NV; ++v) yr[v] = (const ldsd2*)(lds_ptr(Y_) + (v * H + lc) * yld);
   const ldsd2* c2 = (const ldsd2*)vb;
   const int mf = m & ~7;
   for (int a0 = 0; a0 < mf; a0 += 8) {
@@ -1406,8 +1407,8 @@ __device__ __forceinline__ double sinv_any(double* Si, int ld, double* vbuf, dou
   else return sinv_gemv(Si, ld, vbuf, v, m);
 }
 template <int NV, bool ROWS>
-__device__ __forceinline__ void y_axpy_any(double* Y, int H, double* vbuf, double coef, int m, double* z) {
-  if constexpr (ROWS) y_axpy_rows<NV>(Y, H, vbuf, coef, m, z);
+__device__ __forceinline__ void y_axpy_any(double* Y, int H, int yld, double* vbuf, double coef, int m, double* z) {
+  if constexpr (ROWS) y_axpy_rows<NV>(Y, H, yld, vbuf, coef, m, z);
   else y_axpy<NV>(Y, H, vbuf, coef, m, z);
 }
 // P^-1 n for the one-sided constraint (row id, sign sg): lane = variable (one value per vehicle)
@@ -1464,7 +1465,8 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   double* Y = P.Y;
   // element (a, v, l) of the dual active-set columns: column a (lane = variable), or row v*H + l
   // of the transposed layout (RY)
-  auto yi = [&](int a, int v, int ll) -> int { return RY ? (v * H + ll) * YLD + a : a * H2 + v * H + ll; };
+  const int yld = RY ? unif(P.yld) : 0;
+  auto yi = [&](int a, int v, int ll) -> int { return RY ? (v * H + ll) * yld + a : a * H2 + v * H + ll; };
   const int cap = min(P.mmax - 1, P.ycap);
   P.gi_full = false;
   if (P.y_in_k) P.kready = false;  // Y overwrites the K_s^-1 region
@@ -1646,7 +1648,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   auto x_of = [&](double lam) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) xc[v] = x0[v];
-    y_axpy_any<NV, RY>(Y, H, vbuf, lam, m, xc);
+    y_axpy_any<NV, RY>(Y, H, yld, vbuf, lam, m, xc);
   };
 
   // On failure (flab != nullptr): the current working set as PDAS labels -- a start for the
@@ -1804,7 +1806,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
       double z[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) z[v] = yp[v];
-      y_axpy_any<NV, RY>(Y, H, vbuf, r, m, z);
+      y_axpy_any<NV, RY>(Y, H, yld, vbuf, r, m, z);
       const double lpp2 = spp - wsum(va * r);                  // n_p' z
       if (NV == 2) STAMP_ADD(ST_GI_YPASS, t_yp);
       STAMP_ADD(ST_GI_SOLVE, t_gv);
@@ -1887,7 +1889,7 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
 #pragma unroll 1
     for (int rf = 0; rf < 3; ++rf) {
       const double dl = eqp_lam(xc);
-      y_axpy_any<NV, RY>(Y, H, vbuf, dl, m, xc);
+      y_axpy_any<NV, RY>(Y, H, yld, vbuf, dl, m, xc);
       lam += dl;
     }
     const int myc = (l < m) ? wc[l] : 0;
@@ -1981,7 +1983,7 @@ __device__ __forceinline__ void gi_snap_restore(QP<2>& P) {
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int w = 0; w < NV; ++w)
-          if (a0 + u < gm) P.Y[RY ? (w * H + l) * YLD + a0 + u : (a0 + u) * H2 + w * H + l] = v[u][w];
+          if (a0 + u < gm) P.Y[RY ? (w * H + l) * P.yld + a0 + u : (a0 + u) * H2 + w * H + l] = v[u][w];
     }
   }
   if (l < gm) P.ib[l] = code;

@@ -575,6 +575,12 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     // dual active-set columns in the K_s^-1 region (4H^2 doubles, or 2H^2 with fp32 images)
     qe.Y = Ke ? Ke : (double*)Kef;
     qe.ycap = A.pair_gi ? ((Ke ? 4 : 2) * H * H) / (2 * H) : 0;
+    // LDS mode: the columns transposed (2H rows of stride yld, pd_qp.h gi_solve RM_Y) in the same
+    // region -- stride 2H (fp64), H rounded down to even (fp32 images)
+    if (!big) {
+      qe.yld = Ke ? 2 * H : (H & ~1);
+      qe.ycap = min(qe.ycap, qe.yld);
+    }
     qe.y_in_k = true;
     qe.gws = A.gi_ws + (size_t)e * GI_WS;
     qe.gws_warm = A.pair_warm != 0;
@@ -620,7 +626,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     signed char ld[5];
     int nd = 0;
     unsigned long long t_pb = STAMP_T();
-    gi_solve<2, BIG ? 0 : RM_S>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
+    gi_solve<2, BIG ? 0 : RM_S | RM_Y>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
     STAMP_ADD(ST_ZR_SOLVE, t_pb);
   }
   for (int it = X.it0; it < X.it_end; ++it) {
@@ -702,7 +708,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       unsigned long long t_zq = STAMP_T();
       // K_s^-1 of the pair is built in the LDS scratch and copied (2H <= 64), or in place
       // (big mode, two columns per lane, in HBM)
-      const int ste = qp_solve<2, BIG, XGEMV_U, BIG ? 0 : RM_S>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
+      const int ste = qp_solve<2, BIG, XGEMV_U, BIG ? 0 : RM_S | RM_Y>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
                                big ? Ke : scr, big ? 2 * H : LD, uh,
                                n.admm_z, n.pdas_z, n.gi);
       STAMP_ADD(ST_ZQP, t_zq);
