@@ -51,6 +51,8 @@ enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL
 // address_space(3) view (ds_read / ds_write); in_lds() tells the two apart at run time where a
 // pointer is LDS in one mode and HBM in another (a uniform branch).
 typedef __attribute__((address_space(3))) double ldsd;
+typedef double dv2 __attribute__((ext_vector_type(2)));     // two doubles: 16-byte LDS accesses
+typedef __attribute__((address_space(3))) dv2 ldsd2;
 __device__ __forceinline__ ldsd* lds_ptr(double* p) { return (ldsd*)p; }
 __device__ __forceinline__ const ldsd* lds_ptr(const double* p) { return (const ldsd*)p; }
 typedef __attribute__((address_space(1))) double gbld;      // HBM (global) view

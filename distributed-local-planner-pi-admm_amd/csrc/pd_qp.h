@@ -699,6 +699,10 @@ __device__ __forceinline__ bool reduced_solve(const QP<NV>& P, const signed char
 // with Y = P^-1 A_W', S = A_W Y, X = S^-1 Y', beta = S^-1 b.  X' (rows = variables) and
 // beta (row H) are rebuilt in LDS only when W or the bound side of one of its rows changes;
 // a hit costs one fused pass over P^-1 and X' plus the x recovery.
+// TT (fused kernel, LDS mode): the tables transposed -- X T' as rows a of stride xld (beta at
+// column H), G T' as rows of stride gt_ld(H) (g after the H rows) -- so the hit pass reads a
+// lane's own row two doubles at a time (reduced_solve_x).
+template <bool TT = false>
 __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, const int* ids, const double* vb_b) {
   const int l = lid(), H = P.H, ld = P.fld;
   ldsd* fac = lds_ptr(P.fac);       // the wave's LDS scratch
@@ -740,7 +744,9 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   auto tables = [&](auto XTp, auto Gp) {
   const int li = (l <= H) ? l : H;
   const bool own = l <= H;
-  auto xr = XTp + li * P.xld;
+  const int gld = gt_ld(H);
+  // element (li, a) of X' (lane li = time index, or H: the right-hand side b / beta)
+  auto xr = [&](int a) -> auto& { return TT ? XTp[a * P.xld + li] : XTp[li * P.xld + a]; };
   constexpr int XB = 4;
   for (int a0 = 0; a0 < m; a0 += XB) {
     int o[XB][2];
@@ -763,7 +769,7 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
       const int a = a0 + u;
       if (a < m) {
         const double v = (l < H) ? cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1] : vb_b[a];
-        if (own) xr[a] = v;
+        if (own) xr(a) = v;
       }
     }
   }
@@ -771,36 +777,36 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   // L L' sol = rhs for every lane's right-hand side (L broadcast from fac, lane-own sol)
   constexpr int TB = 8;
   for (int a = 0; a < m; ++a) {
-    double acc = xr[a];
+    double acc = xr(a);
     for (int b0 = 0; b0 < a; b0 += TB) {
       double Lv[TB], sv[TB];
 #pragma unroll
       for (int u = 0; u < TB; ++u) {
         const int b = min(b0 + u, a - 1);
         Lv[u] = (b0 + u < a) ? fac[a * ld + b] : 0.0;
-        sv[u] = xr[b];
+        sv[u] = xr(b);
       }
 #pragma unroll
       for (int u = 0; u < TB; ++u) acc -= Lv[u] * sv[u];
     }
     acc *= P.fdiag[64 + a];
-    if (own) xr[a] = acc;
+    if (own) xr(a) = acc;
   }
   for (int a = m - 1; a >= 0; --a) {
-    double acc = xr[a];
+    double acc = xr(a);
     for (int b0 = a + 1; b0 < m; b0 += TB) {
       double Lv[TB], sv[TB];
 #pragma unroll
       for (int u = 0; u < TB; ++u) {
         const int b = min(b0 + u, m - 1);
         Lv[u] = (b0 + u < m) ? fac[b * ld + a] : 0.0;
-        sv[u] = xr[b];
+        sv[u] = xr(b);
       }
 #pragma unroll
       for (int u = 0; u < TB; ++u) acc -= Lv[u] * sv[u];
     }
     acc *= P.fdiag[64 + a];
-    if (own) xr[a] = acc;
+    if (own) xr(a) = acc;
   }
   if (P.gmem) gsync();
   else wsync();
@@ -825,7 +831,8 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
         if (a0 + u < m && l < H) fac[(a0 + u) * ld + l] = cf[u][0] * tv[u][0] + cf[u][1] * tv[u][1];
     }
     wsync();
-    const auto xj = XTp + lc * P.xld;
+    // X'[lc][a]: lane lc's time row of X'
+    auto xj = [&](int a) -> double { return TT ? XTp[a * P.xld + lc] : XTp[lc * P.xld + a]; };
     constexpr int GB = 8;
     for (int i0 = 0; i0 < H; i0 += GB) {
       double acc[GB], pv[GB];
@@ -835,21 +842,22 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
         pv[u] = P.Pinv[min(i0 + u, H - 1) * H + lc];
       }
       for (int a = 0; a < m; ++a) {
-        const double xja = xj[a];
+        const double xja = xj(a);
         const ldsd* ya = fac + a * ld + i0;
 #pragma unroll
         for (int u = 0; u < GB; ++u) acc[u] += ya[u] * xja;     // rows past H are never stored
       }
 #pragma unroll
-      for (int u = 0; u < GB; ++u)
-        if (l < H && i0 + u < H) Gp[(i0 + u) * H + l] = pv[u] - acc[u];
+      for (int u = 0; u < GB; ++u)   // (G is symmetric: TT stores lane l's column as its row)
+        if (l < H && i0 + u < H) Gp[TT ? l * gld + i0 + u : (i0 + u) * H + l] = pv[u] - acc[u];
     }
     double gacc = 0.0;
-    for (int a = 0; a < m; ++a) gacc += fac[a * ld + lc] * XTp[H * P.xld + a];
-    if (l < H) Gp[H * H + l] = gacc;
+    for (int a = 0; a < m; ++a) gacc += fac[a * ld + lc] * XTp[TT ? a * P.xld + H : H * P.xld + a];
+    if (l < H) Gp[TT ? H * gld + l : H * H + l] = gacc;
+    if (TT && gld > H && l < H) Gp[l * gld + H] = 0.0;   // the row's pad: read (times q = 0) by the pass
     if (P.gmem) gsync();
     else wsync();
-    if (P.t32) {
+    if (!TT && P.t32) {
       // precision 2: fp32 images of the unfolded G and X' (the fp64 tables stay: the fallback)
       float* G32 = P.t32;
       float* X32 = P.t32 + H * H;
@@ -865,11 +873,12 @@ __device__ __forceinline__ bool param_build_x(const QP<1>& P, int m, int myid, c
   {
     double s1 = 0.0, s2 = 0.0, t1 = 0.0, t2 = 0.0;
     const int la = (l < m) ? l : 0;
+    const int lg = (l < H) ? l : 0;
     for (int k = 0; k < H; ++k) {
-      const double gk = Gp[k * H + (l < H ? l : 0)];
-      const double xk = XTp[k * P.xld + la];
-      if (l < H) Gp[k * H + l] = s2;
-      if (l < m) XTp[k * P.xld + l] = t2;
+      const double gk = Gp[TT ? lg * gld + k : k * H + lg];
+      const double xk = XTp[TT ? la * P.xld + k : k * P.xld + la];
+      if (l < H) Gp[TT ? l * gld + k : k * H + l] = s2;
+      if (l < m) XTp[TT ? l * P.xld + k : k * P.xld + l] = t2;
       s1 += gk;
       s2 += s1;
       t1 += xk;
@@ -993,7 +1002,7 @@ __device__ __forceinline__ void hit32(const QP<1>& P, int m, const bool* inW, co
   wsync();
 }
 
-template <int XU>
+template <int XU, bool TT = false>
 __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed char* lab, double* x, double* y) {
   const int l = lid(), H = P.H;
   unsigned long long t_pre = STAMP_T();
@@ -1031,7 +1040,7 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
     }
     wsync();
     const int myid = (l < m) ? ids[l] : 0;
-    if (!param_build_x(P, m, myid, ids, vb_b)) {
+    if (!param_build_x<TT>(P, m, myid, ids, vb_b)) {
       if (l == 0) P.fstate[0] = -1;
       P.csig = -1;
       wsync();
@@ -1043,14 +1052,63 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
   (void)cids;
   wsync();
   STAMP_ADD(ST_RSX_PRE, t_pre);
-  if (P.t32) {                       // precision 2: fp32 tables + one fp64 refinement step
+  if (!TT && P.t32) {                // precision 2: fp32 tables + one fp64 refinement step
     hit32<XU>(P, m, inW, pos, lab, x, y);
     return true;
   }
   unsigned long long t_rs = STAMP_T();
   // one fused pass: x = -G q + g (lane = variable), lam = -X q - beta (lane = W row)
   double ag = 0.0, ax = 0.0;
-  {
+  if constexpr (TT) {
+    // transposed tables: lane lc walks its row of G T', lane la its row of X T' (16-byte loads;
+    // pairs of time indices, the last one padded: q is zero there)
+    const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
+    const int gld = unif(gt_ld(H)), xs = unif(P.xld);
+    const ldsd2* gr = (const ldsd2*)(lds_ptr(P.G) + lc * gld);
+    const ldsd2* xr2 = (const ldsd2*)(lds_ptr(XT) + la * xs);
+    const ldsd2* q2 = (const ldsd2*)lds_ptr(vb_q);
+    const int hp = unif((H + 1) >> 1);
+    constexpr int U = 8;
+    double ag1 = 0.0, ax1 = 0.0;
+    const int hf = hp - hp % U;
+    for (int p0 = 0; p0 < hf; p0 += U) {
+      dv2 qv[U], gv[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        qv[u] = q2[p0 + u];
+        gv[u] = gr[p0 + u];
+        xv[u] = xr2[p0 + u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ag += gv[u].x * qv[u].x;
+        ag1 += gv[u].y * qv[u].y;
+        ax += xv[u].x * qv[u].x;
+        ax1 += xv[u].y * qv[u].y;
+      }
+    }
+    if (hf < hp) {
+      dv2 qv[U], gv[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int pi = min(hf + u, hp - 1);
+        qv[u] = q2[hf + u];            // zero beyond H (vb_q is zero-padded to 64)
+        gv[u] = gr[pi];
+        xv[u] = xr2[pi];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ag += gv[u].x * qv[u].x;
+        ag1 += gv[u].y * qv[u].y;
+        ax += xv[u].x * qv[u].x;
+        ax1 += xv[u].y * qv[u].y;
+      }
+    }
+    ag += ag1;
+    ax += ax1;
+    if (l < m) vb_lam[l] = -ax - XT[l * xs + H];
+    ag = P.G[H * gld + lc] - ag;
+  } else {
     const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
     const double* G = P.G;
     // full batches: row pointers advance by a stride, no clamp
@@ -1171,7 +1229,7 @@ __device__ __forceinline__ bool tables_match(const QP<NV>& P, const signed char*
   return wall(sig == P.csig);
 }
 
-template <int NV, int XU = XGEMV_U>
+template <int NV, int XU = XGEMV_U, bool TT = false>
 __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* x, double* y, int& nsolve,
                                      int steps = PDAS_STEPS) {
   constexpr int NR = QP<NV>::NR;
@@ -1180,7 +1238,7 @@ __device__ __forceinline__ bool pdas(const QP<NV>& P, signed char* lab, double* 
     ++nsolve;
     unsigned long long t_r = STAMP_T();
     bool rs_ok;
-    if constexpr (NV == 1) rs_ok = reduced_solve_x<XU>(P, lab, x, y);
+    if constexpr (NV == 1) rs_ok = reduced_solve_x<XU, TT>(P, lab, x, y);
     else rs_ok = reduced_solve(P, lab, x, y);
     STAMP_ADD(NV == 1 ? ST_XRED : ST_ZRED, t_r);
     if (__builtin_expect(!rs_ok, 0)) return false;
@@ -1295,9 +1353,8 @@ __device__ __forceinline__ void y_axpy(double* Y, int H, double* vbuf_, double c
 // passes at 1312 / 1836 / 3336 cycles (S^-1 v / Y axpy / bordering) against 2212 / 2920 / 5252
 // for the lane = column passes.  Row entries beyond m hold other data (the region also serves
 // the PDAS factor), so the last partial batch masks them.
-typedef double dv2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) dv2 ldsd2;
 constexpr int RM_S = 1, RM_Y = 2;   // gi_solve's row-access modes
+constexpr int RM_T = 4;             // the x-step's parametric tables transposed (param_build_x TT)
 __device__ __forceinline__ int rows_ld(int fld) { return (fld + 1) & ~1; }
 
 // row[j] += coef * vb[j] over j < m (one lane's row of S^-1; the last batch's entries beyond m
@@ -2479,7 +2536,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       // reduced solve on other labels costs a table rebuild (~20 us) and after a dual update or
       // at a step's first x-QP (gi_first: the previous step's labels shifted) rarely certifies,
       // so the dual active set starts from those labels directly
-      if ((gi_first == 0 || gi_first == 3) && tables_match(P, lab)) ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 1);
+      if ((gi_first == 0 || gi_first == 3) && tables_match(P, lab)) ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas, 1);
       if (__builtin_expect(!ok, 0)) {
         int ngi = 0;
         signed char glab[NR];
@@ -2496,18 +2553,18 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
           for (int s = 0; s < NR; ++s) stable &= !P.valid(s) || glab[s] == flab[s];
           if (wall(stable)) {
             // the working set held: build its tables now for the cheap hits that follow
-            ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+            ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas);
           } else {
             signed char nl[NR];
             ok = kkt_check(P, lab, x, y, nl);
-            if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+            if (!ok) ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas);
           }
         }
         n_gi += ngi;
         if (!ok) {
 #pragma unroll
           for (int s = 0; s < NR; ++s) lab[s] = flab[s];
-          ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+          ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas);
         }
       }
     } else {
@@ -2515,7 +2572,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       // moved since); label moves are left to the dual active set, warm-started from the same
       // active set -- each further PDAS step is a full Schur build + factorization (r03 stamps:
       // 3.25 of them per step on a crossing, nearly all followed by the dual active set anyway)
-      ok = pdas<NV, XU>(P, lab, x, y, n_pdas, NV == 2 ? 1 : PDAS_STEPS);
+      ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas, NV == 2 ? 1 : PDAS_STEPS);
     }
   }
   if constexpr (NV == 2) {
@@ -2548,7 +2605,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
 #endif
 #pragma unroll
         for (int s = 0; s < NR; ++s) lab[s] = glab[s];
-        if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+        if (!ok) ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas);
         GI_DBG("  after pdas ok=%d\n", (int)ok);
       } else if (TWO && P.gi_full && P.wide) {
         // the working set outgrew one row per lane: the wide dual active set (two per lane;
@@ -2561,14 +2618,14 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
         }
 #pragma unroll
         for (int s = 0; s < NR; ++s) lab[s] = ok ? glab[s] : clab[s];
-        if (!ok) ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 4 * PDAS_STEPS);
+        if (!ok) ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas, 4 * PDAS_STEPS);
       } else {
         // GI stopped (typically a hinge multiplier at its cap beta: that hinge is linear at the
         // optimum, which the dual active set does not model): polish from its working set with
         // the saturated row linear before falling back to ADMM
 #pragma unroll
         for (int s = 0; s < NR; ++s) lab[s] = clab[s];
-        ok = pdas<NV, XU>(P, lab, x, y, n_pdas, 4 * PDAS_STEPS);
+        ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas, 4 * PDAS_STEPS);
       }
       n_gi += ngi;
     }
@@ -2648,7 +2705,7 @@ __device__ __forceinline__ int qp_solve(QP<NV>& P, double* xs, double* zs, doubl
       if ((wall(same) || it % (8 * polish_every) == 0) && !wall(tried)) {
 #pragma unroll
         for (int s = 0; s < NR; ++s) flab[s] = lab[s];
-        ok = pdas<NV, XU>(P, lab, x, y, n_pdas);
+        ok = pdas<NV, XU, (RM & RM_T) != 0>(P, lab, x, y, n_pdas);
       }
     }
   }

@@ -190,11 +190,11 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     double* p = lds;
     if (f32) { Kxf = (float*)p; p += kxf_words(H); }     // 2 x H*H fp32 agent K_s^-1 (even per wave)
     else { Kx = p; p += 2 * H * H; }                     // 2 x H*H   agent K_s^-1
-    Gx = p; p += 2 * (H * H + H);                        // 2 x (H*H+H) agent polish G | g
+    Gx = p; p += 2 * gt_stride(H);                       // 2 x agent polish G T' | g (transposed)
     p += f32 ? 2 * H * H : 4 * H * H;                    // pair K_s^-1 (the pair wave's)
     p += 64 * (LD + 1);                                  // pair scratch (the pair wave's)
     xfac = p + w * HMAX * (HMAX + 2);                    // NW x HMAX x (HMAX+2)
-    xt_all = p + NW * HMAX * (HMAX + 2);                 // NW x (HMAX+1) x XLD
+    xt_all = p + NW * HMAX * (HMAX + 2);                 // NW x HMAX x XLDT (X' T' | beta, transposed)
   } else {
     xfac = lds + 64 * LD + w * xrows(H) * (xrows(H) + 1);   // NW x xrows(H) x (xrows+1)
   }
@@ -222,11 +222,11 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     qx.Kf = (!big && f32) ? Kxf + w * kxf_stride(H) : nullptr;
     qx.kf32 = !big && f32;                        // big mode: the x-step K stays fp64 in HBM
     qx.Pinv = A.Pinv_x + (size_t)a * H * H;    // L2-resident; read only when W changes
-    qx.G = big ? A.Gx_g + (size_t)a * (H * H + H) : Gx + w * (H * H + H);
+    qx.G = big ? A.Gx_g + (size_t)a * (H * H + H) : Gx + w * gt_stride(H);
     qx.vb = X.wm.vb;
     qx.fac = xfac;
-    qx.XT = big ? A.XT_g + (size_t)a * H1 * XLDG : xt_all + w * (HMAX + 1) * XLD;
-    qx.xld = big ? XLDG : XLD;
+    qx.XT = big ? A.XT_g + (size_t)a * H1 * XLDG : xt_all + w * HMAX * XLDT;
+    qx.xld = big ? XLDG : XLDT;
     qx.gmem = big;
     qx.fdiag = xdiag;
     qx.ib = xids;
@@ -331,7 +331,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? 0 : RM_S>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? 0 : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && it == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
@@ -398,7 +398,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int admm0 = n.admm_x;
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? 0 : RM_S>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? 0 : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && tgt == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       // a repeat of this solve may be speculated only if it certified without ADMM and its
@@ -521,7 +521,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
   if (!big) {
     double* p = lds;
     p += f32 ? kxf_words(H) : 2 * H * H;                 // agent K_s^-1 (the agent waves')
-    p += 2 * (H * H + H);                                // agent polish G | g (the agent waves')
+    p += 2 * gt_stride(H);                               // agent polish G T' | g (the agent waves')
     if (f32) { Kef = (float*)p; p += 2 * H * H; }        // 4*H*H fp32 pair K_s^-1
     else { Ke = p; p += 4 * H * H; }                     // 4*H*H     pair K_s^-1
     scr = p;                                             // 64 x LD   pair scratch
@@ -931,8 +931,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   // ---- LDS carve (lds_bytes() in piadmm_internal.h): the matrix regions are carved by the parts
   double* vec_all;
   if (!BIG) {
-    vec_all = lds + (X.f32 ? kxf_words(H) : 2 * H * H) + 2 * (H * H + H) + (X.f32 ? 2 * H * H : 4 * H * H) +
-              64 * (LD + 1) + NW * HMAX * (HMAX + 2) + NW * (HMAX + 1) * XLD;   // NWT x 512
+    vec_all = lds + (X.f32 ? kxf_words(H) : 2 * H * H) + 2 * gt_stride(H) + (X.f32 ? 2 * H * H : 4 * H * H) +
+              64 * (LD + 1) + NW * HMAX * (HMAX + 2) + NW * HMAX * XLDT;   // NWT x 512
   } else {
     vec_all = lds + 64 * LD + NW * xrows(H) * (xrows(H) + 1);             // NWT x 512
   }

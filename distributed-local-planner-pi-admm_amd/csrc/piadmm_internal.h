@@ -32,7 +32,10 @@ constexpr int HCAP = 64;     // storage stride of per-lane state: lane k <-> tim
 constexpr int HMAX = 32;     // largest H of the all-in-LDS layout ("LDS mode")
 constexpr int HBIG = 63;     // largest H supported (matrices in HBM / L2 beyond HMAX: "big mode")
 constexpr int LD = 65;       // odd LDS stride of the per-wave matrix scratch
-constexpr int XLD = HMAX + 1;  // odd LDS stride of the x-step parametric table X' (LDS mode)
+constexpr int XLDT = HMAX + 2; // LDS mode: stride of the transposed X' T' rows (a < HMAX; beta at column H)
+// LDS mode: the transposed G T' (H rows of even stride gt_ld, then g), per agent
+__host__ __device__ constexpr int gt_ld(int H) { return H + (H & 1); }
+__host__ __device__ constexpr int gt_stride(int H) { return H * gt_ld(H) + gt_ld(H); }
 constexpr int XLDG = 65;       // stride of X' in HBM (big mode: up to 64 working-set rows)
 constexpr int RUIZ_ITERS = 10;
 constexpr int PDAS_STEPS = 4;
@@ -180,12 +183,12 @@ inline size_t lds_bytes(int H, int precision = 0) {
   const bool f32 = precision == 1;
   if (H <= HMAX) {
     d += f32 ? kxf_words(H) : 2 * (size_t)H * H;   // agent K_s^-1 (2 agents; fp32: half)
-    d += 2 * ((size_t)H * H + H);    // agent polish G | g (2 agents)
+    d += 2 * (size_t)gt_stride(H);   // agent polish G T' | g (2 agents, transposed)
     d += (f32 ? 2 : 4) * (size_t)H * H;   // pair K_s^-1 (2H x 2H)
     d += 64 * (LD + 1);              // pair matrix scratch (PDAS factor, or the dual active set's
                                      // S^-1 in rows of even stride: pd_qp.h gi_solve RM_S)
     d += NW * HMAX * (HMAX + 2);     // per-wave x-step scratch / Cholesky factor / S^-1 rows
-    d += NW * (HMAX + 1) * XLD;      // per-wave x-step parametric table X' | beta
+    d += NW * HMAX * XLDT;           // per-wave x-step parametric table X' T' | beta (transposed)
   } else {
     d += 64 * LD;                    // pair matrix scratch (wave 0)
     d += NW * (size_t)xrows(H) * (xrows(H) + 1);   // per-wave x-step scratch / Cholesky factor
