@@ -196,7 +196,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     xfac = p + w * HMAX * (HMAX + 2);                    // NW x HMAX x (HMAX+2)
     xt_all = p + NW * HMAX * (HMAX + 2);                 // NW x HMAX x XLDT (X' T' | beta, transposed)
   } else {
-    xfac = lds + 64 * LD + w * xrows(H) * (xrows(H) + 1);   // NW x xrows(H) x (xrows+1)
+    xfac = lds + 64 * (LD + 1) + w * xrows(H) * (xrows(H) + 2);   // NW x xrows(H) x (xrows+2)
   }
   double* xdiag = X.vec_all + NWT * 512 + w * 128;       // NWT x 128 factor diagonals
   int* xids = X.wm.ib;
@@ -331,7 +331,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? 0 : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_S : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && it == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
@@ -398,7 +398,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int admm0 = n.admm_x;
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? 0 : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_S : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && tgt == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       // a repeat of this solve may be speculated only if it certified without ADMM and its
@@ -626,7 +626,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     signed char ld[5];
     int nd = 0;
     unsigned long long t_pb = STAMP_T();
-    gi_solve<2, BIG ? 0 : RM_S | RM_Y>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
+    gi_solve<2, BIG ? RM_S : RM_S | RM_Y>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
     STAMP_ADD(ST_ZR_SOLVE, t_pb);
   }
   for (int it = X.it0; it < X.it_end; ++it) {
@@ -708,7 +708,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       unsigned long long t_zq = STAMP_T();
       // K_s^-1 of the pair is built in the LDS scratch and copied (2H <= 64), or in place
       // (big mode, two columns per lane, in HBM)
-      const int ste = qp_solve<2, BIG, XGEMV_U, BIG ? 0 : RM_S | RM_Y>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
+      const int ste = qp_solve<2, BIG, XGEMV_U, BIG ? RM_S : RM_S | RM_Y>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
                                big ? Ke : scr, big ? 2 * H : LD, uh,
                                n.admm_z, n.pdas_z, n.gi);
       STAMP_ADD(ST_ZQP, t_zq);
@@ -934,7 +934,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     vec_all = lds + (X.f32 ? kxf_words(H) : 2 * H * H) + 2 * gt_stride(H) + (X.f32 ? 2 * H * H : 4 * H * H) +
               64 * (LD + 1) + NW * HMAX * (HMAX + 2) + NW * HMAX * XLDT;   // NWT x 512
   } else {
-    vec_all = lds + 64 * LD + NW * xrows(H) * (xrows(H) + 1);             // NWT x 512
+    vec_all = lds + 64 * (LD + 1) + NW * xrows(H) * (xrows(H) + 2);       // NWT x 512
   }
   X.vec_all = vec_all;
   double* fdiag_all = vec_all + NWT * 512;               // NWT x 128

@@ -130,7 +130,7 @@ __device__ __forceinline__ void g_xstep(const DevArgs& A, int a, int t, int it, 
   double ustar[1];
   unsigned long long t_q = STAMP_T();
   const int gi0 = n.gi;
-  const int st = qp_solve<1, false, 8, BIG ? 0 : RM_S | RM_Y>(qx, xs, zs, ys, lab, warm, c.max_inner, c.polish_every, W.fac, qx.fld,
+  const int st = qp_solve<1, false, 8, BIG ? RM_S : RM_S | RM_Y>(qx, xs, zs, ys, lab, warm, c.max_inner, c.polish_every, W.fac, qx.fld,
                                              ustar, n.admm_x, n.pdas_x, n.gi);
   STAMP_ADD(ST_XQP, t_q);
   STAMP_CNT(ST_N_GIX, n.gi - gi0);
@@ -310,7 +310,7 @@ __device__ __forceinline__ void g_zstep(const DevArgs& A, int e, int t, int it, 
   double uh[2];
   unsigned long long t_zq = STAMP_T();
   const int giz0 = n.gi;
-  const int st = qp_solve<2, BIG, XGEMV_U, BIG ? 0 : RM_S | RM_Y>(qe, xs, zs, ys, lab, warm, c.max_inner, c.polish_every,
+  const int st = qp_solve<2, BIG, XGEMV_U, BIG ? RM_S : RM_S | RM_Y>(qe, xs, zs, ys, lab, warm, c.max_inner, c.polish_every,
                                                  BIG ? Ke : W.fac, BIG ? 2 * H : LD, uh, n.admm_z, n.pdas_z, n.gi);
   STAMP_ADD(ST_ZQP, t_zq);
   STAMP_CNT(ST_N_GIZ, n.gi - giz0);

@@ -190,8 +190,8 @@ inline size_t lds_bytes(int H, int precision = 0) {
     d += NW * HMAX * (HMAX + 2);     // per-wave x-step scratch / Cholesky factor / S^-1 rows
     d += NW * HMAX * XLDT;           // per-wave x-step parametric table X' T' | beta (transposed)
   } else {
-    d += 64 * LD;                    // pair matrix scratch (wave 0)
-    d += NW * (size_t)xrows(H) * (xrows(H) + 1);   // per-wave x-step scratch / Cholesky factor
+    d += 64 * (LD + 1);              // pair matrix scratch (wave 0; S^-1 rows of even stride)
+    d += NW * (size_t)xrows(H) * (xrows(H) + 2);   // per-wave x-step scratch / Cholesky factor / S^-1 rows
   }
   d += NWT * 512;                  // per-wave vector buffers (agents, pair)
   d += NWT * 128;                  // per-wave factor diagonals (x-step or pair)
