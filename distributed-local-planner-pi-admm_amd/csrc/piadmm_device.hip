@@ -30,6 +30,17 @@
 
 namespace pd {
 
+// The dual active set's S^-1 passes in big mode walk rows (pd_qp.h gi_solve RM_S).  The phase-stamp
+// diagnostic build keeps big mode on the lane = column passes: with the stamps compiled in, this
+// ROCm's compiler rejects that instantiation ("Operand has incorrect register class" on an LDS
+// aperture compare).  The stamps are read for the LDS-mode kernel.
+#ifdef PIADMM_STAMPS
+constexpr int RM_BIG = 0;
+#else
+constexpr int RM_BIG = RM_S;
+#endif
+
+
 // ============================================================ the MPC-step kernel
 struct CompLds {
   double *pos, *xt, *seed, *u, *hat, *lam, *S, *D, *last, *sc;
@@ -331,7 +342,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_S : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_BIG : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && it == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       status_x |= stx;
@@ -398,7 +409,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int admm0 = n.admm_x;
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_S : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_BIG : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && tgt == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
       // a repeat of this solve may be speculated only if it certified without ADMM and its
@@ -626,7 +637,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     signed char ld[5];
     int nd = 0;
     unsigned long long t_pb = STAMP_T();
-    gi_solve<2, BIG ? RM_S : RM_S | RM_Y>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
+    gi_solve<2, BIG ? RM_BIG : RM_S | RM_Y>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
     STAMP_ADD(ST_ZR_SOLVE, t_pb);
   }
   for (int it = X.it0; it < X.it_end; ++it) {
@@ -708,7 +719,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       unsigned long long t_zq = STAMP_T();
       // K_s^-1 of the pair is built in the LDS scratch and copied (2H <= 64), or in place
       // (big mode, two columns per lane, in HBM)
-      const int ste = qp_solve<2, BIG, XGEMV_U, BIG ? RM_S : RM_S | RM_Y>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
+      const int ste = qp_solve<2, BIG, XGEMV_U, BIG ? RM_BIG : RM_S | RM_Y>(qe, xs_e, zs_e, ys_e, lab_e, warm_e, c.max_inner, c.polish_every,
                                big ? Ke : scr, big ? 2 * H : LD, uh,
                                n.admm_z, n.pdas_z, n.gi);
       STAMP_ADD(ST_ZQP, t_zq);
