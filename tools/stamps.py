@@ -12,12 +12,15 @@ NAMES = ['setup_x', 'setup_z', 'xstep', 'xqp', 'xred', 'xroll', 'zstep', 'zqp', 
 tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-natural = len(sys.argv) > 4 and sys.argv[4] == "natural"
+natural = len(sys.argv) > 4 and sys.argv[4] == "natural"   # argv[4]: natural | fixed
 cfg = config.matlab_pi(H=H, fixed_iters=0 if natural else 1, max_outer=100, term_global=int(natural))
-scn = scenario.tiled(tiles, H, n_steps=steps)
+warm = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # untimed steps first (step 0 builds the caches)
+scn = scenario.tiled(tiles, H, n_steps=warm + steps)
 s = PI_ADMM_MI355X(cfg, scn)
+if warm:
+    s.time_steps(0, warm)
 s.reset_counters()
-ms = s.time_steps(0, steps)
+ms = s.time_steps(warm, steps)
 cnt = s.counters()
 buf = (ctypes.c_uint64 * (s.C * 64))()
 s._check(s.lib.piadmm_debug_stamps(s._h, buf, s.C * 64))
