@@ -298,3 +298,29 @@ def test_large_connected_graph_split(Solver, monkeypatch):
     finally:
         s1.close()
         s2.close()
+
+
+def test_repeating_a_step_forgets_the_stored_active_sets(Solver):
+    """a pair's stored dual active set (S^-1, Y columns, codes) is valid only for the
+    MPC step that built it.  Solving the same t again (piadmm_mpc_step(h, t) twice: the second
+    starts from the propagated state, another geometry) must not restore it; the library forgets
+    the stored sets whenever a step does not continue the sequence (piadmm_capi.cpp
+    continue_sequence).  The repeat must equal the same step on a fresh handle started from that
+    state, with every QP certified."""
+    cfg = config.matlab_pi(H=15)
+    scn = scenario.concat([scenario.crossing(4, 15, n_steps=10, seed=2), scenario.crossing(3, 15, n_steps=10, seed=3)])
+    with Solver(cfg, scn) as a:
+        a.mpc_step(0)
+        a.mpc_step(1)
+        xt1 = a.xt.copy()
+        rep = a.mpc_step(1)
+        ca = a.counters()
+    with Solver(cfg, scn) as b:
+        b.set_xt(xt1)
+        ref = b.mpc_step(1)
+    np.testing.assert_array_equal(rep.status, 0)
+    np.testing.assert_array_equal(ref.status, 0)
+    np.testing.assert_array_equal(rep.iters, ref.iters)
+    close(rep.xt, ref.xt)
+    close(rep.u, ref.u)
+    assert ca["inexact"] == 0
