@@ -106,12 +106,19 @@ def algorithmic_bytes(cnt: dict, H: int) -> float:
     H1 = H + 1
     x_doubles = 3 + 1 + 2 * H1 + (2 * H1 + 2 * H1) + H + 2 * H1
     z_doubles = 4 * H1 + 4 * H1 + 6 + 4 + 4 * H1 + 12 * H1
-    b = 8.0 * (cnt["x_qps"] * x_doubles + cnt["z_qps"] * z_doubles)
-    if H > 32:
-        # big mode: the polish tables G (H^2+H) and X' (<= H1 x H) of each x-step QP
-        # and the pair's K_s^-1 (4H^2) per pair ADMM iteration stream from L2 / HBM
-        b += 8.0 * (cnt["x_qps"] * (H * H + H + H1 * H) + cnt["admm_z"] * 4 * H * H)
-    return b
+    return 8.0 * (cnt["x_qps"] * x_doubles + cnt["z_qps"] * z_doubles)
+
+
+def l2_table_bytes(cnt: dict, H: int) -> float:
+    """Big mode (H > 32): the x-step polish tables G (H^2 + H) and X' (<= H1 x H)
+    re-read by every x-step QP and the pair's K_s^-1 (4H^2) per pair ADMM iteration.  They are
+    per-scenario state (256 agents x ~40 KB at H = 50: ~10 MB) that stays resident in L2 / MALL, so
+    they are reported beside the roofline as L2 reads, not counted as HBM bytes (the PMC traffic
+    says what reached HBM)."""
+    if H <= 32:
+        return 0.0
+    H1 = H + 1
+    return 8.0 * (cnt["x_qps"] * (H * H + H + H1 * H) + cnt["admm_z"] * 4 * H * H)
 
 
 def latest_profile(kind: str, workload: str):
@@ -183,7 +190,7 @@ def cpu_baseline(wl: dict, budget_s: float, K: int) -> dict:
 
 
 def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_rank: int, dist, split="components",
-        share: int = 0, precision: int = 0):
+        share: int = 0, precision: int = 0, cold: bool = False):
     """Time K MPC steps of workload wl on this rank; returns (metrics, counters, solver info).
     share > 1 (strong scaling, one process): rank 0's share of a share-rank job alone on this GPU --
     its agents (and, interleaved, its ghosts), every collective a no-op (SURVEY.md 8e readiness)."""
@@ -260,6 +267,14 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
         xchg = (shard is not None and shard.n_slots > 0) or wl.get("kind") == "chain"
     finally:
         solver.close()
+    # the cold first step: MPC step 0 on a FRESH handle, its per-scenario caches (the agents' P^-1,
+    # K_s^-1 and scaling, the pairs' speed-only polish tables) built inside the timed launch -- the
+    # timed steps above replay t = 0 .. K-1 after the warmup built them, while B-opt builds its own
+    # inside every timed run (oracle/cpu_bopt.py).  hipEvents around that one launch.
+    cold_ms = None
+    if cold and dist is None and not share:
+        with PI_ADMM_MI355X(cfg, scn, device=local_rank % max(device_count(), 1), shard=shard) as fresh:
+            cold_ms = fresh.time_steps(0, 1)
     if dist is not None:
         import torch
         tt = torch.tensor([wall, ev_ms], dtype=torch.float64)
@@ -279,7 +294,7 @@ def run(wl: dict, natural: bool, K: int, W: int, rank: int, world: int, local_ra
         n_launch = -(-K // spl) if spl > 1 else int(job_iters) + K
     graph = xchg or wl.get("kind") in ("crossing", "chain")
     return dict(wall=wall, ev_ms=ev_ms, job_iters=job_iters, n_launch=n_launch, spl=spl, N=N, C=C, xchg=xchg,
-                kernel="pd::k_graph_step" if graph else "pd::k_mpc_step"), cnt
+                kernel="pd::k_graph_step" if graph else "pd::k_mpc_step", cold_ms=cold_ms), cnt
 
 
 def _obca_chunk(recs):
@@ -417,6 +432,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline timing (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-natural", action="store_true", help="skip the natural-termination co-headline")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold first step (a fresh handle's step 0)")
     ap.add_argument("--natural", action="store_true", help="natural termination as the headline itself")
     g = ap.add_mutually_exclusive_group()
     g.add_argument("--config2", action="store_true", help="BASELINE configs[1]: 64 agents x H20")
@@ -468,7 +484,8 @@ def main():
     K, W = args.steps, args.warmup
     if args.share and (not args.strong or world != 1):
         raise SystemExit("bench.py: --share needs --strong on one GPU")
-    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist, args.split, args.share, args.precision)
+    m, cnt = run(wl, args.natural, K, W, rank, world, local_rank, dist, args.split, args.share, args.precision,
+                 cold=not args.no_cold)
 
     # value = units all ranks processed / the max-over-ranks wall time.  Weak scaling: one unit =
     # one outer iteration of a rank's (256-agent) block, so all ranks processed world x job
@@ -531,6 +548,7 @@ def main():
             "kernel": m["kernel"], "avg_launch_ms": avg_launch_s * 1e3,
             "steps_per_launch": m["spl"], "launches": m["n_launch"],
             "algorithmic_bytes_per_launch": bytes_launch,
+            "l2_table_bytes_per_launch": l2_table_bytes(cnt, H) / m["n_launch"],
             "traffic_source": traffic["_file"] if traffic else None,
             "note": "not bandwidth-bound: the algorithmic bytes stay in LDS; see latency and DESIGN.md §5",
         },
@@ -547,6 +565,12 @@ def main():
         "fp64": None,
         "cpu_baseline": None,
     }
+    if m["cold_ms"] is not None:
+        line["cold_first_step"] = {
+            "ms": m["cold_ms"],
+            "note": "MPC step 0 on a fresh handle, per-scenario caches (P^-1, K_s^-1, pair polish tables) built "
+                    "inside (hipEvents); ms_per_step replays t = 0.. after the warmup built them, as a planner "
+                    "re-solving one scenario does -- B-opt builds its caches inside every timed run"}
     # latency model: the kernel runs one dependent QP chain per wave; cycles per wave per outer
     # iteration from this run's launch time, against the issue bound from the committed SQ counters
     # (VALU wave-instructions x 4 cycles: a wave64 fp64 VALU op occupies a 16-lane SIMD 4 cycles)

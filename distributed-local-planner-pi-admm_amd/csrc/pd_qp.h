@@ -1002,6 +1002,92 @@ __device__ __forceinline__ void hit32(const QP<1>& P, int m, const bool* inW, co
   wsync();
 }
 
+// The x-step hit's fused pass over the transposed tables (reduced_solve_x TT): lane rows gr (G T') and
+// xr2 (X T') against q2 = w', hp pairs of time indices in batches of 8 pairs, two accumulators per table
+// (even / odd time index), the last batch's pairs beyond hp clamped to pair hp - 1 against the
+// zero-padded q.  HPC > 0: hp compiled in (every load an immediate offset from the row bases, no loop
+// control, no clamp arithmetic); 0: hp at run time.  Both perform the same products and sums in the
+// same order, so their results are bit-identical.
+template <int HPC>
+__device__ __forceinline__ void hit_pass(const ldsd2* gr, const ldsd2* xr2, const ldsd2* q2, int hp_rt, double& ag,
+                                         double& ag1, double& ax, double& ax1) {
+  constexpr int U = 8;
+  if constexpr (HPC > 0) {
+    constexpr int HF = HPC - HPC % U;
+#pragma unroll
+    for (int p0 = 0; p0 < HF; p0 += U) {
+      dv2 qv[U], gv[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        qv[u] = q2[p0 + u];
+        gv[u] = gr[p0 + u];
+        xv[u] = xr2[p0 + u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ag += gv[u].x * qv[u].x;
+        ag1 += gv[u].y * qv[u].y;
+        ax += xv[u].x * qv[u].x;
+        ax1 += xv[u].y * qv[u].y;
+      }
+    }
+    if constexpr (HF < HPC) {
+      dv2 qv[U], gv[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        constexpr int last = HPC - 1;
+        const int pi = (HF + u < last) ? HF + u : last;
+        qv[u] = q2[HF + u];            // zero beyond H (vb_q is zero-padded to 64)
+        gv[u] = gr[pi];
+        xv[u] = xr2[pi];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ag += gv[u].x * qv[u].x;
+        ag1 += gv[u].y * qv[u].y;
+        ax += xv[u].x * qv[u].x;
+        ax1 += xv[u].y * qv[u].y;
+      }
+    }
+  } else {
+    const int hp = hp_rt;
+    const int hf = hp - hp % U;
+    for (int p0 = 0; p0 < hf; p0 += U) {
+      dv2 qv[U], gv[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        qv[u] = q2[p0 + u];
+        gv[u] = gr[p0 + u];
+        xv[u] = xr2[p0 + u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ag += gv[u].x * qv[u].x;
+        ag1 += gv[u].y * qv[u].y;
+        ax += xv[u].x * qv[u].x;
+        ax1 += xv[u].y * qv[u].y;
+      }
+    }
+    if (hf < hp) {
+      dv2 qv[U], gv[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int pi = min(hf + u, hp - 1);
+        qv[u] = q2[hf + u];            // zero beyond H (vb_q is zero-padded to 64)
+        gv[u] = gr[pi];
+        xv[u] = xr2[pi];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ag += gv[u].x * qv[u].x;
+        ag1 += gv[u].y * qv[u].y;
+        ax += xv[u].x * qv[u].x;
+        ax1 += xv[u].y * qv[u].y;
+      }
+    }
+  }
+}
+
 template <int XU, bool TT = false>
 __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed char* lab, double* x, double* y) {
   const int l = lid(), H = P.H;
@@ -1068,41 +1154,13 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
     const ldsd2* xr2 = (const ldsd2*)(lds_ptr(XT) + la * xs);
     const ldsd2* q2 = (const ldsd2*)lds_ptr(vb_q);
     const int hp = unif((H + 1) >> 1);
-    constexpr int U = 8;
     double ag1 = 0.0, ax1 = 0.0;
-    const int hf = hp - hp % U;
-    for (int p0 = 0; p0 < hf; p0 += U) {
-      dv2 qv[U], gv[U], xv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        qv[u] = q2[p0 + u];
-        gv[u] = gr[p0 + u];
-        xv[u] = xr2[p0 + u];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        ag += gv[u].x * qv[u].x;
-        ag1 += gv[u].y * qv[u].y;
-        ax += xv[u].x * qv[u].x;
-        ax1 += xv[u].y * qv[u].y;
-      }
-    }
-    if (hf < hp) {
-      dv2 qv[U], gv[U], xv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int pi = min(hf + u, hp - 1);
-        qv[u] = q2[hf + u];            // zero beyond H (vb_q is zero-padded to 64)
-        gv[u] = gr[pi];
-        xv[u] = xr2[pi];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        ag += gv[u].x * qv[u].x;
-        ag1 += gv[u].y * qv[u].y;
-        ax += xv[u].x * qv[u].x;
-        ax1 += xv[u].y * qv[u].y;
-      }
+    // BASELINE's horizons (10, 20, 30) with the pair count compiled in: immediate offsets, no loop
+    switch (hp) {
+      case 15: hit_pass<15>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+      case 10: hit_pass<10>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+      case 5: hit_pass<5>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+      default: hit_pass<0>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
     }
     ag += ag1;
     ax += ax1;
@@ -1227,6 +1285,71 @@ __device__ __forceinline__ bool tables_match(const QP<NV>& P, const signed char*
 #pragma unroll
   for (int s = 0; s < 2; ++s) sig |= ((P.valid(s) && lab[s] != FREE) ? (int)lab[s] : 0) << (2 * s);
   return wall(sig == P.csig);
+}
+
+// The repeat of a certified x-step table hit: the speculative x-step of piadmm_device.hip agent_part,
+// run only when the x-step in U certified without ADMM and the parametric tables hold its working
+// set (spec_ok), so this QP is that one again (q changes only in a z-step).  It is the same solve as
+// qp_solve's first branch on transposed tables (tables_match -> pdas, one step -> reduced_solve_x<XU,
+// true> -> kkt_check) -- the same pass, products, sums, certificate and counters -- without the
+// general solver's scaffolding: the signature is known to match, and the working-set multipliers
+// reach their rows through lane permutes instead of an LDS store, sync and gather.  Results are
+// bit-identical; on a failed certificate (not expected: the same QP certified before) it gives its
+// solve back to the counter and returns false, and the caller runs qp_solve.
+template <int XU>
+__device__ __forceinline__ bool xhit_repeat(QP<1>& P, const signed char* lab, double* xs, double* ys, double* x_out,
+                                            int& n_pdas) {
+  const int l = lid(), H = P.H;
+  bool inW[2];
+  int pos[2];
+  int m = 0;
+  const unsigned long long ltmask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    inW[s] = P.valid(s) && lab[s] != FREE;
+    const unsigned long long bm = __ballot(inW[s]);
+    pos[s] = m + __popcll(bm & ltmask);
+    m += __popcll(bm);
+  }
+  double* vb_q = P.vb;
+  vb_q[l] = (l < H) ? P.wq : 0.0;
+  wsync();
+  const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
+  const int gld = unif(gt_ld(H)), xsd = unif(P.xld);
+  const ldsd2* gr = (const ldsd2*)(lds_ptr(P.G) + lc * gld);
+  const ldsd2* xr2 = (const ldsd2*)(lds_ptr(P.XT) + la * xsd);
+  const ldsd2* q2 = (const ldsd2*)lds_ptr(vb_q);
+  const int hp = unif((H + 1) >> 1);
+  double ag = 0.0, ax = 0.0, ag1 = 0.0, ax1 = 0.0;
+  switch (hp) {
+    case 15: hit_pass<15>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+    case 10: hit_pass<10>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+    case 5: hit_pass<5>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+    default: hit_pass<0>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+  }
+  ag += ag1;
+  ax += ax1;
+  const ldsd* XT = lds_ptr(P.XT);
+  const double lam = (l < m) ? -ax - XT[l * xsd + H] : 0.0;          // lane a: multiplier of W row a
+  ag = lds_ptr(P.G)[H * gld + lc] - ag;
+  double x[1] = {(l < H) ? ag : 0.0}, y[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const double ys_ = __shfl(lam, pos[s]);
+    y[s] = inW[s] ? ys_ : 0.0;
+  }
+  ++n_pdas;
+  signed char nl[2];
+  if (__builtin_expect(!kkt_check(P, lab, x, y, nl), 0)) {
+    --n_pdas;
+    return false;
+  }
+  xs[0] = x[0];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) ys[s] = P.valid(s) ? y[s] : 0.0;
+  P.wraw = true;
+  x_out[0] = x[0];
+  return true;
 }
 
 template <int NV, int XU = XGEMV_U, bool TT = false>

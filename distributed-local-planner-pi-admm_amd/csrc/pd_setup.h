@@ -92,7 +92,7 @@ __device__ __forceinline__ void qp_common(const piadmm_config_t& c, int H, doubl
 __device__ __forceinline__ bool setup_agent(const DevArgs& A, int a, QP<1>& P, const Geo& g, double* xfac,
                                             double coef = -1.0) {
   const piadmm_config_t& c = A.cfg;
-  const int H = c.H, l = lid();
+  const int H = P.H, l = lid();   // (qp_common set P.H: a constant in the compiled-in horizon kernels)
   const bool in = l < H;
   P.coefP = coef >= 0.0 ? coef : 2.0 * c.Pnorm + c.rho * (double)A.nbr_cnt[a];
   P.mm[0] = g.mm;
@@ -148,7 +148,7 @@ __device__ __forceinline__ void setup_pair(const DevArgs& A, int e, QP<2>& P, co
                                            double c1x, double c1y, double c2x, double c2y, const double* seeds,
                                            double* scr, double* Ke_lds, double deff, double rho_pair = -1.0) {
   const piadmm_config_t& c = A.cfg;
-  const int H = c.H, n = 2 * H, l = lid();
+  const int H = P.H, n = 2 * H, l = lid();   // (set by the caller)
   const bool in = l < H;
   unsigned long long t_pre = STAMP_T();
   const double dbx = seeds[2] - seeds[0], dby = seeds[3] - seeds[1];

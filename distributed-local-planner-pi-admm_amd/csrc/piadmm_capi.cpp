@@ -147,6 +147,15 @@ int check_cfg(piadmm_ctx* h, const piadmm_config_t& c) {
     return fail(h, PIADMM_E_ARG, "pi_trad / ki_adapt select variants of the global PI law (dual_mode 2)");
   if (!std::isfinite(c.d_gain) || !std::isfinite(c.dual_init))
     return fail(h, PIADMM_E_ARG, "d_gain and dual_init must be finite");
+  // ABI 7 made the back-calculation gain of the global PI law a field: a zero-initialised config
+  // would silently drop the term of casadi_old_PI_ADMM/main.py:142 (d_gain 2) and of the adaptive
+  // script (1), so 0 is refused rather than taken as a variant
+  if (c.dual_mode == PIADMM_DUAL_PI_GLOBAL && c.d_gain == 0.0)
+    return fail(h, PIADMM_E_ARG, "global PI needs d_gain != 0 (2.0: casadi_old_PI_ADMM, 1.0: the adaptive-gain script)");
+  // warm_duals carries the previous step's shifted duals; dual_init sets every step's start
+  // values -- the reference's scripts never combine the two (the first step would be ambiguous)
+  if (c.warm_duals && c.dual_init != 0.0)
+    return fail(h, PIADMM_E_ARG, "warm_duals and a nonzero dual_init are exclusive");
   if (!(c.dt > 0) || !(c.L > 0) || !(c.rho > 0) || !(c.Pcost > 0) || c.Pnorm < 0 || c.beta < 0)
     return fail(h, PIADMM_E_ARG, "dt, L, rho, Pcost must be > 0; Pnorm, beta >= 0");
   if (c.max_inner <= 0 || c.polish_every <= 0) return fail(h, PIADMM_E_ARG, "max_inner, polish_every must be > 0");
@@ -506,6 +515,10 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     // two shapes' equality test)
     const char* ns = std::getenv("PIADMM_NO_SPEC");
     A.no_spec = (ns && ns[0] == '1') ? 1 : 0;
+    // PIADMM_NO_HC=1: the fused kernel with the horizon as a runtime value even where an
+    // instantiation for it exists (the equality test of the two)
+    const char* nh = std::getenv("PIADMM_NO_HC");
+    A.no_hc = (nh && nh[0] == '1') ? 1 : 0;
   }
   A.N = N;
   A.E = n_edges;
@@ -1036,8 +1049,10 @@ static int32_t sync_step_cap(piadmm_handle_t h) {
 
 // A step at t0 that does not continue the receding-horizon sequence forgets the pairs' stored
 // active sets (codes, step index, the snapshot's validity: pd_qp.h gi_solve / gi_snap_restore).
+// t_next: -1 = no step yet (nothing stored), -2 = the last run failed part-way (whatever is stored
+// may belong to any step: always forget it), else the step the last completed run leads to.
 static int32_t continue_sequence(piadmm_handle_t h, int32_t t0) {
-  if (h->t_next >= 0 && t0 != h->t_next && h->E)
+  if (h->t_next != -1 && t0 != h->t_next && h->E)
     HIPCHK(h, hipMemsetAsync(h->a.gi_ws, 0, (size_t)h->E * (2 + pd::WAVE) * sizeof(int), h->stream));
   return PIADMM_OK;
 }
@@ -1048,16 +1063,20 @@ static int32_t enqueue_steps(piadmm_handle_t h, int32_t t0, int32_t n) {
   if (h->step_open) return fail(h, PIADMM_E_STATE, "a host-stepped MPC step is open: piadmm_step_finish first");
   if (n < 0 || t0 < 0 || t0 + (n > 0 ? n - 1 : 0) + h->cfg.H + 1 > h->T)
     return fail(h, PIADMM_E_ARG, "time index out of the reference trajectory");
+  if (n == 0) return PIADMM_OK;    // nothing runs: the stored active sets and t_next stay as they are
   HIPCHK(h, hipSetDevice(h->cfg.device));
   if (int rc = continue_sequence(h, t0)) return rc;
-  h->t_next = t0 + n;
   if ((h->comm || h->xfn) && !h->cap_synced)
     if (int rc = sync_step_cap(h)) return rc;
   for (int i = 0; i < n;) {
     const int k = std::min(h->step_cap, n - i);
-    if (int rc = run_steps(h, t0 + i, k, i + k == n)) return rc;
+    if (int rc = run_steps(h, t0 + i, k, i + k == n)) {
+      h->t_next = -2;              // part of the sequence may have run: the next step forgets the sets
+      return rc;
+    }
     i += k;
   }
+  h->t_next = t0 + n;              // only a sequence enqueued in full continues at t0 + n
   return PIADMM_OK;
 }
 

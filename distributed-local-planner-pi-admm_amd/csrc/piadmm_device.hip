@@ -187,7 +187,7 @@ struct WaveCnt {
 // Wave w < na solves agent a0 + w's x-step every outer iteration (casadi/main.py:81-106); its
 // QP state (tables, labels, warm ADMM state) stays in this wave's registers and LDS regions for
 // the whole step.  The pair's state never lives here: the pair wave owns it.
-template <bool BIG, bool TIES>
+template <bool BIG, bool TIES, int HC>
 __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const piadmm_config_t& c = A.cfg;
@@ -207,7 +207,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     xfac = p + w * HMAX * (HMAX + 2);                    // NW x HMAX x (HMAX+2)
     xt_all = p + NW * HMAX * (HMAX + 2);                 // NW x HMAX x XLDT (X' T' | beta, transposed)
   } else {
-    xfac = lds + 64 * (LD + 1) + w * xrows(H) * (xrows(H) + 2);   // NW x xrows(H) x (xrows+2)
+    xfac = lds + 64 * (LD + 1) + w * xreg(H);            // NW x xrows(H) x (xrows+2), even counts
   }
   double* xdiag = X.vec_all + NWT * 512 + w * 128;       // NWT x 128 factor diagonals
   int* xids = X.wm.ib;
@@ -409,12 +409,26 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       double ustar[1];
       unsigned long long t_q = STAMP_T();
       const int admm0 = n.admm_x;
-      const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_BIG : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
+      // phase 1 repeats the certified table hit of the x-step in U (spec_ok): the lean repeat on the
+      // transposed tables (LDS mode), qp_solve when it does not certify (or in big mode)
+      const bool lean = !BIG && phase == 1 && xhit_repeat<XGEMV_U>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x);
+      const int stx = lean ? 0 : qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_BIG : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && tgt == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
+#ifdef PIADMM_XREP
+      // diagnostic build (libpiadmm_xrep.so, never the measured library): the same x-step solved
+      // PIADMM_XREP more times in place -- the step time's increase is the in-kernel cost of the
+      // repeated solves (a repeat of a certified solve is a table hit and changes no state)
+      for (int r = 0; r < PIADMM_XREP; ++r) {
+        int dx = 0, dp = 0, dg = 0;
+        double ud[1];
+        (void)qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_BIG : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, true, c.max_inner, c.polish_every, xfac,
+                               qx.fld, ud, dx, dp, dg, 0);
+      }
+#endif
       // a repeat of this solve may be speculated only if it certified without ADMM and its
       // working set's tables are held (the repeat is then one table hit)
-      spec_ok = !(stx & PIADMM_QP_INEXACT) && n.admm_x == admm0 && tables_match(qx, lab_x);
+      spec_ok = lean || (!(stx & PIADMM_QP_INEXACT) && n.admm_x == admm0 && tables_match(qx, lab_x));
       if (phase == 0) {
         status_x |= stx;
         ++n.xqp;
@@ -519,7 +533,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
 // Wave PW owns the component's pair (when it has one): the per-step pair setup (concurrent with
 // the agents' setups), the z-step QP, the hat rollouts, the dual update and the residuals
 // (casadi/main.py:121-181).  Its QP state stays in this wave's registers for the whole step.
-template <bool BIG, bool TIES>
+template <bool BIG, bool TIES, int HC>
 __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const piadmm_config_t& c = A.cfg;
@@ -654,6 +668,17 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       unsigned long long t_ro = STAMP_T();
       const double u = (l < H) ? S.u[(it & 1) * 2 * H + l] : 0.0;
       rollout_r(S.xt[0], S.xt[1], S.xt[2], ra_s[0], ra_s[0] / c.L, u, c, H, nonlin_pos, px, py, pth);
+#ifdef PIADMM_PREP
+      {
+        // diagnostic build (libpiadmm_prep.so, never the measured library): the pair wave's rollout
+        // done PIADMM_PREP more times per iteration -- prices the pair wave's chain (is it critical?)
+        for (int r = 0; r < PIADMM_PREP; ++r) {
+          double qx2, qy2, qt2;
+          rollout_r(S.xt[0], S.xt[1], S.xt[2], ra_s[0], ra_s[0] / c.L, u + px * 1e-300, c, H, nonlin_pos, qx2, qy2, qt2);
+          if (qx2 == -12345.678) S.sc[31] = qy2 + qt2;
+        }
+      }
+#endif
       if (l <= H) {
         pos[0 * H1 + l] = px;
         pos[1 * H1 + l] = py;
@@ -869,6 +894,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
 // the pair wave's chain before the verdict (two rollouts, the collision test) -- which the agent
 // waves wait for at barrier B -- holds one rollout, not two.  It takes the same barriers (A, B) and
 // stops with the pair wave's verdict.
+template <int HC>
 __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
   const piadmm_config_t& c = A.cfg;
   const int H = X.H, H1 = X.H1, l = X.l;
@@ -911,7 +937,7 @@ __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
 // iterations for the outputs and the propagation.
 // Wave layout: waves 0 and 1 run the agents' x-steps (agent_part), wave 2 the pair
 // (pair_part); the two loops take the same barriers and stop decisions.
-template <bool BIG, bool TIES>
+template <bool BIG, bool TIES, int HC>
 __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
                                               int& nbar) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -925,8 +951,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   X.vdd = &s_vdd;
   X.rflag = &s_rflag;
   if (threadIdx.x == 0) s_rflag = 0;   // (iterations count from it0 >= 0: the flag waits for it + 1)
-  X.H = c.H;
-  X.H1 = c.H + 1;
+  X.H = HC > 0 ? HC : c.H;      // HC: the horizon compiled in (mpc_fn), 0: runtime
+  X.H1 = X.H + 1;
   X.ci = blockIdx.x;
   X.w = threadIdx.x >> 6;
   X.l = lid();
@@ -945,7 +971,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
     vec_all = lds + (X.f32 ? kxf_words(H) : 2 * H * H) + 2 * gt_stride(H) + (X.f32 ? 2 * H * H : 4 * H * H) +
               64 * (LD + 1) + NW * HMAX * (HMAX + 2) + NW * HMAX * XLDT;   // NWT x 512
   } else {
-    vec_all = lds + 64 * (LD + 1) + NW * xrows(H) * (xrows(H) + 2);       // NWT x 512
+    vec_all = lds + 64 * (LD + 1) + NW * xreg(H);                          // NWT x 512
   }
   X.vec_all = vec_all;
   double* fdiag_all = vec_all + NWT * 512;               // NWT x 128
@@ -1045,9 +1071,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   L.act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
   L.dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
   WaveCnt n;
-  if (X.w < NW) agent_part<BIG, TIES>(A, X, L, nbar, n);
-  else if (X.w == PW) pair_part<BIG, TIES>(A, X, L, nbar, n);
-  else roll_part(A, X);
+  if (X.w < NW) agent_part<BIG, TIES, HC>(A, X, L, nbar, n);
+  else if (X.w == PW) pair_part<BIG, TIES, HC>(A, X, L, nbar, n);
+  else roll_part<HC>(A, X);
   __syncthreads();
   STAMP_ADD(ST_KERNEL, t_k);
   unsigned long long t_epi = STAMP_T();
@@ -1109,7 +1135,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 // waits for the slowest one of each step: the launch takes max_c sum_t instead of
 // sum_t max_c.  The step-to-step state (xt, labels, caches) goes through HBM inside one
 // workgroup (same CU: the barrier's workgroup-scope fences order it).
-template <bool BIG, bool TIES>
+template <bool BIG, bool TIES, int HC>
 __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
 #ifdef PIADMM_STAMPS
   for (int i = threadIdx.x; i < 64 * STAMP_WAVES; i += blockDim.x) s_stamps[i] = 0ull;
@@ -1125,7 +1151,7 @@ __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int 
   }
   int nbar = 0;   // grid barriers so far (coop): parity of the termination partials
   for (int k = 0; k < nsteps; ++k) {
-    mpc_step_body<BIG, TIES>(A, t0 + k, it0, it1, flags, k, nbar);
+    mpc_step_body<BIG, TIES, HC>(A, t0 + k, it0, it1, flags, k, nbar);
     __syncthreads();
   }
 #ifdef PIADMM_STAMPS
@@ -1210,10 +1236,34 @@ __global__ void k_pair_deff(DevArgs A) {
 }
 
 // The kernel instantiation: matrices in LDS / HBM (BIG), near-tie log compiled in or out (TIES: the log
-// costs 3-10 % of the fused kernel's time, so it is a separate instantiation, on when a handle asks for it)
-static const void* mpc_fn(bool big, bool ties) {
-  if (big) return ties ? (const void*)k_mpc_step<true, true> : (const void*)k_mpc_step<true, false>;
-  return ties ? (const void*)k_mpc_step<false, true> : (const void*)k_mpc_step<false, false>;
+// costs 3-10 % of the fused kernel's time, so it is a separate instantiation, on when a handle asks for it),
+// and the horizon: BASELINE's horizons (10, 20, 30; 50 in big mode) are compiled in, so that loop bounds,
+// strides and LDS offsets are constants; every other H (and the tie log) runs the runtime-H kernel.
+// PIADMM_NO_HC=1 (DevArgs::no_hc) forces the runtime-H kernel (A/B and equality tests).
+template <bool TIES>
+static const void* mpc_fn_rt(bool big) {
+  return big ? (const void*)k_mpc_step<true, TIES, 0> : (const void*)k_mpc_step<false, TIES, 0>;
+}
+static const void* mpc_fn(bool big, bool ties, int H, bool no_hc) {
+#ifdef PIADMM_ONLY_HC
+  // resource-report build of one instantiation (never linked)
+  (void)big; (void)ties; (void)H; (void)no_hc;
+  return (const void*)k_mpc_step<(PIADMM_ONLY_HC > HMAX), false, PIADMM_ONLY_HC>;
+#else
+  if (ties) return mpc_fn_rt<true>(big);
+#ifndef PIADMM_NO_HC_BUILD
+  if (!no_hc) {
+    switch (H) {
+      case 10: return (const void*)k_mpc_step<false, false, 10>;
+      case 20: return (const void*)k_mpc_step<false, false, 20>;
+      case 30: return (const void*)k_mpc_step<false, false, 30>;
+      case 50: return (const void*)k_mpc_step<true, false, 50>;
+      default: break;
+    }
+  }
+#endif
+  return mpc_fn_rt<false>(big);
+#endif
 }
 
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s) {
@@ -1226,7 +1276,7 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     last = a.stamps;
   }
 #endif
-  const void* fn = mpc_fn(big, a.tie_on != 0);
+  const void* fn = mpc_fn(big, a.tie_on != 0, a.cfg.H, a.no_hc != 0);
   if (set_dyn_lds(fn, sh) != 0) return -1;
   if (flags & F_COOP) {
     // every workgroup must be resident for the grid barrier: the cooperative launch fails
@@ -1260,7 +1310,7 @@ bool coop_fits(const DevArgs& a, int device) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return false;
   const size_t sh = lds_bytes(a.cfg.H, a.cfg.precision);
   const bool big = a.cfg.H > HMAX;
-  const void* fn = mpc_fn(big, a.tie_on != 0);
+  const void* fn = mpc_fn(big, a.tie_on != 0, a.cfg.H, a.no_hc != 0);
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return false;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NWT * WAVE, sh) != hipSuccess) return false;
   return (long long)per * ncu >= (long long)a.C;

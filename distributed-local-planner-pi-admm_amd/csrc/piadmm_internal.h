@@ -53,6 +53,7 @@ struct DevArgs {
   int x_gi;                 // x-step working-set changes by the dual active set (1); the step's first x-QP
                             // without the labels' reduced solve (2), started cold (3); all cold (4); PIADMM_X_SOLVER
   int no_spec;              // 1: k_mpc_step keeps the plain loop shape (PIADMM_NO_SPEC=1, read at set_scenario)
+  int no_hc;                // 1: k_mpc_step with the horizon at run time (PIADMM_NO_HC=1), not compiled in
   // scenario (read-only during a step)
   const double* spd;        // N
   const double* ref;        // N*2*T
@@ -165,6 +166,10 @@ struct DevArgs {
 // Big mode: rows of the per-wave x-step factor scratch (working sets of up to H + 2 rows:
 // a degenerate vertex can hold one or two dependent rows beyond the H variables).
 constexpr int xrows(int H) { return H + 2 < 64 ? H + 2 : 64; }
+// Big mode: doubles of one agent wave's x-step region (xrows x (xrows + 2)), rounded up to an even
+// count so that the next wave's region -- whose S^-1 rows the dual active set reads and writes with
+// 16-byte LDS accesses (pd_qp.h gi_solve RM_S) -- starts on 16 bytes for odd H as well.
+constexpr int xreg(int H) { return xrows(H) * (xrows(H) + 2) + ((xrows(H) * (xrows(H) + 2)) & 1); }
 // LDS the kernel declares statically (s_int, s_cnt, s_warm) on top of lds_bytes().
 constexpr size_t STATIC_LDS = NWT * 272 * 4 + NWA * 8 * 4 + 16 + 4 * 4 + 8 + 8;
 constexpr size_t MAX_LDS = 160 * 1024;
@@ -191,7 +196,7 @@ inline size_t lds_bytes(int H, int precision = 0) {
     d += NW * HMAX * XLDT;           // per-wave x-step parametric table X' T' | beta (transposed)
   } else {
     d += 64 * (LD + 1);              // pair matrix scratch (wave 0; S^-1 rows of even stride)
-    d += NW * (size_t)xrows(H) * (xrows(H) + 2);   // per-wave x-step scratch / Cholesky factor / S^-1 rows
+    d += NW * (size_t)xreg(H);       // per-wave x-step scratch / Cholesky factor / S^-1 rows (even counts)
   }
   d += NWT * 512;                  // per-wave vector buffers (agents, pair)
   d += NWT * 128;                  // per-wave factor diagonals (x-step or pair)

@@ -1310,6 +1310,9 @@ int32_t piadmm_obca_upload(piadmm_obca_t h, const double* recs, int32_t n) {
   // no batch until this upload succeeds: a failed reallocation or copy must not leave a batch size
   // that a later obca_run would launch on freed (null) buffers
   h->n = 0;
+  // a new batch: the longest-first order of the last run belongs to other problems (even when the
+  // size is the same), so the next run goes in index order and records this batch's work
+  h->cost_n = 0;
   if (int rc = ensure(h, n)) return rc;
   OHIP(h, hipMemcpyAsync(h->d_rec, recs, (size_t)n * obca::REC * sizeof(double), hipMemcpyHostToDevice, h->stream));
   OHIP(h, hipStreamSynchronize(h->stream));

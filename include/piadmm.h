@@ -108,9 +108,11 @@ typedef struct piadmm_config {
   /* ABI 7: the adaptive-gain global PI (ADMM_CVX_two_veh_intesection_adp_PI_antiwindup1.m:121-147) */
   int32_t ki_adapt;          /* 1: K_I = kI / d_min (K_I_coeff / dis_min, :127); 0: K_I = kI (casadi_old :135) */
   int32_t reserved1;
-  double d_gain;             /* S += K_I e + d_gain D: 2 (casadi_old_PI_ADMM/main.py:142), 1 (adp :135) */
+  double d_gain;             /* S += K_I e + d_gain D: 2 (casadi_old_PI_ADMM/main.py:142), 1 (adp :135).
+                                Set it to 2.0 to keep ABI 6's dual_mode 2 behaviour; with dual_mode 2 a
+                                zero (e.g. a zero-initialised struct) is refused with PIADMM_E_ARG */
   double dual_init;          /* hat, lam and last_hat at every MPC step's start: 0 (casadi/main.py:56-63,
-                                casadi_old :49-51) or 1e-4 (adp :59-61) */
+                                casadi_old :49-51) or 1e-4 (adp :59-61); nonzero excludes warm_duals */
 } piadmm_config_t;
 
 typedef struct piadmm_ctx* piadmm_handle_t;
@@ -342,10 +344,13 @@ int32_t piadmm_obca_destroy(piadmm_obca_t h);
 const char* piadmm_obca_last_error(piadmm_obca_t h);
 /* upload + one launch + download (synchronous) */
 int32_t piadmm_obca_solve(piadmm_obca_t h, const double* recs, int32_t n, double* out, int32_t* status3);
-/* resident batch: upload once, launch (async on the handle's stream), time, download.  Block b of
- * a launch solves problem order[b]: longest first by the QP steps each problem took in the last run
- * of a batch of the same size (index order before any), so the longest problems start in the first
- * dispatch wave; the answers do not depend on the order. */
+/* resident batch: upload once, launch, time, download.  Block b of a launch solves problem
+ * order[b]: longest first by the QP steps each problem took in the previous run of the SAME upload
+ * (index order on the first run after an upload), so the longest problems start in the first
+ * dispatch wave; the answers do not depend on the order.  piadmm_obca_run blocks: it reads the
+ * previous run's per-problem work back to the host (a device-to-host copy and stream syncs) and
+ * uploads the order before it enqueues its launches, which then run asynchronously on the handle's
+ * stream (piadmm_obca_download / _time synchronise). */
 int32_t piadmm_obca_upload(piadmm_obca_t h, const double* recs, int32_t n);
 int32_t piadmm_obca_run(piadmm_obca_t h, int32_t repeats);
 int32_t piadmm_obca_time(piadmm_obca_t h, int32_t repeats, float* ms_per_launch);

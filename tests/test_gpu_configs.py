@@ -10,6 +10,9 @@ it finishes in seconds, sampled tiles where it does not.  Tolerance: the north-s
 contract is 1e-5 relative on states and controls; these tests hold 1e-8 with identical
 outer-iteration counts and residual histories (1e-7).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -151,12 +154,14 @@ def test_gpu_equals_bopt_on_the_crossing_workload(Solver, kw, n_steps):
     decision near a threshold (profiles/crossing_sensitivity_r04.json; the near-tie logs are empty).
     So parity is stated against the job's own sensitivity, measured on the CPU baseline:
     (1) step by step from common inputs -- B-opt runs step k from the GPU's state: equal outer-
-        iteration counts, and the GPU's deviation no larger than B-opt's own deviation when that
-        state is perturbed at 1e-12 (relative; the largest over four perturbations: a single one
-        samples the sensitivity of a chaotic step by chance), or 1e-8 -- every one of the 20 steps
-        except chaotic ones, where that own deviation is macroscopic (> 1e-3: step 6, whose 1e-12
-        perturbations move controls by 0.1-0.3 rad, a rate bound's width): there only the
-        iteration counts and the QP certificates are asserted, and at most 2 such steps;
+        iteration counts on every step, and the GPU's deviation ("resync") held against the step's
+        own sensitivity env1 = B-opt's deviation when that state is perturbed at 1e-12 (relative;
+        the largest over four perturbations: a single one samples a chaotic step by chance):
+          - env1 <= 1e-6 (every step but one in practice): resync <= 1e-8, the contract's 1e-5
+            with three decades of margin, whatever the envelope;
+          - 1e-6 < env1 <= 1e-3 (a sensitive step, none observed): resync <= env1;
+          - env1 > 1e-3 (chaotic: step 6, whose 1e-12 perturbations move controls by 0.1-0.3 rad,
+            a rate bound's width): only the iteration counts and the QP certificates, at most 2;
     (2) free running -- the GPU's deviation from B-opt no larger than B-opt's own from a 1e-12
         perturbation of xt0, at every step before the parting (deviation > 1e-3)."""
     from oracle import cpu_bopt
@@ -190,11 +195,20 @@ def test_gpu_equals_bopt_on_the_crossing_workload(Solver, kw, n_steps):
         counts, events = s.near_ties()
     print(f"crossing {kw}: resync {['%.1e' % v for v in resync]}, one-step envelope {['%.1e' % v for v in env1]}, "
           f"free {['%.1e' % v for v in free]}, envelope {['%.1e' % v for v in env]}, near ties {counts}")
+    out = os.environ.get("PIADMM_EVIDENCE_DIR")
+    if out:                        # the per-step vectors of this run (profiles/r06/crossing_parity_*.json)
+        os.makedirs(out, exist_ok=True)
+        tag = "fixed" if kw.get("fixed_iters") else "natural"
+        with open(os.path.join(out, f"crossing_parity_{tag}.json"), "w") as f:
+            json.dump({"config": kw, "n_steps": n_steps, "resync": resync, "env1": env1, "free": free,
+                       "env": env, "near_ties": counts}, f, indent=1)
     chaotic = [k for k in range(n_steps) if env1[k] > 1e-3]
     assert len(chaotic) <= 2, (chaotic, env1)
     for k in range(n_steps):
-        if k not in chaotic:
-            assert resync[k] <= max(1e-8, env1[k]), (k, resync, env1)
+        if env1[k] <= 1e-6:
+            assert resync[k] <= 1e-8, (k, resync, env1)
+        elif k not in chaotic:
+            assert resync[k] <= env1[k], (k, resync, env1)
     part = next((k for k in range(n_steps) if env[k] > 1e-3), n_steps)
     for k in range(part):
         assert free[k] <= max(env[k], 1e-9), (k, free[:part], env[:part])

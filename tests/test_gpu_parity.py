@@ -75,10 +75,12 @@ def test_gpu_state_matches_oracle(Solver):
     np.testing.assert_array_equal(st["iters"], ro.iters)
 
 
-@pytest.mark.parametrize("H", [3, 5, 32, 33, 40, 50])
+@pytest.mark.parametrize("H", [3, 5, 32, 33, 40, 41, 50])
 def test_horizon_limits_match_oracle(Solver, H):
     """H <= 32: every matrix of a component in LDS; H > 32 ("big mode"): the agent and pair
-    K_s^-1, G and X' in HBM / L2, the pair's K built in place with two columns per lane."""
+    K_s^-1, G and X' in HBM / L2, the pair's K built in place with two columns per lane.  Odd H in
+    big mode (33, 41): xrows(H) is odd, so the agent waves' LDS regions are rounded to even counts
+    (piadmm_internal.h xreg) for the 16-byte row passes over S^-1."""
     cfg = config.matlab_pi(H=H)
     n = 12 if H <= 32 else 3          # the oracle's dense active set is slow at H > 32
     scn = scenario.tiled(2, H, n_steps=12, seed=H)

@@ -1,0 +1,9 @@
+set -o pipefail
+O=gpurun_out/r06b
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 120 tools/xhit_ubench > $O/xhit.log 2>&1 || exit 1
+cat $O/xhit.log
+bash tools/gpu_ab.sh r06b_ab 2 libpiadmm.so || exit 1
+PIADMM_EVIDENCE_DIR=$O timeout -k 10 900 python3 -u -m pytest -x -v -s --timeout 400 --timeout-method thread -m gpu tests/test_gpu_two_process.py "tests/test_gpu_modes.py::test_speculative_loop_equals_plain_loop" "tests/test_gpu_parity.py::test_horizon_limits_match_oracle" "tests/test_gpu_configs.py::test_gpu_equals_bopt_on_the_crossing_workload" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -15 $O/tests.log

@@ -9,7 +9,7 @@ TAG=${1:-r02}
 OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--no-cpu --no-natural --warmup 20"   # a 20-step warmup launch, then the 20-step timed launch (equal launches)
+ARGS="--no-cpu --no-natural --no-cold --warmup 20"   # a 20-step warmup launch, then the 20-step timed launch (equal launches)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o bench --output-format csv -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o bench --output-format csv -- python3 bench.py $ARGS > $OUT/write.log 2>&1
