@@ -618,6 +618,17 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     del lib
+    if os.environ.get("PIADMM_BENCH_UNLOAD") == "1":
+        _lib.unload()
+    if os.environ.get("PIADMM_BENCH_RESET") == "1":
+        # diagnostic (the exit fault under rocprofv3 after a cooperative launch):
+        # tear the device's HIP state down while the profiler is still attached
+        import ctypes
+        ctypes.CDLL("libamdhip64.so").hipDeviceReset()
+    if os.environ.get("PIADMM_BENCH_MAPS"):
+        # diagnostic: the process's mappings at exit (which libraries the exit handlers run in)
+        with open("/proc/self/maps") as f, open(os.environ["PIADMM_BENCH_MAPS"], "w") as g:
+            g.write(f.read())
 
 
 if __name__ == "__main__":

@@ -1217,19 +1217,14 @@ __device__ __forceinline__ bool reduced_solve_x(const QP<1>& P, const signed cha
   return true;
 }
 
-// KKT test of (x, y) for labels lab; on failure fills new labels (PDAS update).
+// KKT test of (x, y) for labels lab at multiplier tolerance ty; on failure fills new labels (PDAS
+// update).  yfail: some multiplier test of this lane failed at ty.
 template <int NV>
-__device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* lab, const double* x, const double* y,
-                          signed char* nlab) {
+__device__ __forceinline__ bool kkt_eval(const QP<NV>& P, const signed char* lab, const double* x, const double* y,
+                                         const double* ax, double ty, signed char* nlab, bool& yfail) {
   constexpr int NR = QP<NV>::NR;
-  double ax[NR];
-  A_mul(P, x, ax);
-  double ym = 0.0;
-#pragma unroll
-  for (int s = 0; s < NR; ++s) ym = fmax(ym, fabs(y[s]));
-  ym = wmax(ym);
-  const double ty = P.tol * (1.0 + ym);
   bool ok = true;
+  yfail = false;
 #pragma unroll
   for (int s = 0; s < NR; ++s) {
     if (!P.valid(s)) {
@@ -1255,7 +1250,9 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
       } else {
         // a kink row must sit at h: the reduced solve drops a dependent row, which is only
         // right when the dropped equation is implied by the others (consistent labels)
-        ok &= (y[s] <= ty) && (y[s] >= -P.beta - ty) && fabs(ax[s] - h) <= tp;
+        const bool yok = (y[s] <= ty) && (y[s] >= -P.beta - ty);
+        yfail |= !yok;
+        ok &= yok && fabs(ax[s] - h) <= tp;
         nlab[s] = (y[s] > ty) ? HZERO : ((y[s] < -P.beta - ty) ? HLINEAR : HKINK);
       }
     } else {
@@ -1264,14 +1261,42 @@ __device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* la
         ok &= !vl && !vu;
         nlab[s] = vl ? LOWER : (vu ? UPPER : FREE);
       } else if (lab[s] == LOWER) {
-        ok &= (y[s] <= ty) && fabs(ax[s] - P.lo(s)) <= tp;   // equality too (dropped rows)
+        const bool yok = y[s] <= ty;
+        yfail |= !yok;
+        ok &= yok && fabs(ax[s] - P.lo(s)) <= tp;   // equality too (dropped rows)
         nlab[s] = (y[s] > ty) ? FREE : LOWER;
       } else {
-        ok &= (y[s] >= -ty) && fabs(ax[s] - P.hi(s)) <= tp;
+        const bool yok = y[s] >= -ty;
+        yfail |= !yok;
+        ok &= yok && fabs(ax[s] - P.hi(s)) <= tp;
         nlab[s] = (y[s] < -ty) ? FREE : UPPER;
       }
     }
     ok &= isfinite(x[0]) && isfinite(y[s]);
+  }
+  return ok;
+}
+
+// KKT test of (x, y) for labels lab; on failure fills new labels (PDAS update).  The multiplier
+// tolerance is tol (1 + max |y|); the tests are first evaluated at its lower bound tol, and only
+// when one of them fails there is the wave max formed and the test repeated: a multiplier test that
+// passes at tol passes at any larger tolerance with the same label decision, so the outcome and
+// the labels are exactly those of the test at tol (1 + max |y|), without the wave reduction in the
+// common case (every multiplier inside its sign band).
+template <int NV>
+__device__ __forceinline__ bool kkt_check(const QP<NV>& P, const signed char* lab, const double* x, const double* y,
+                          signed char* nlab) {
+  constexpr int NR = QP<NV>::NR;
+  double ax[NR];
+  A_mul(P, x, ax);
+  bool yfail;
+  bool ok = kkt_eval(P, lab, x, y, ax, P.tol, nlab, yfail);
+  if (__builtin_expect(wany(yfail), 0)) {
+    double ym = 0.0;
+#pragma unroll
+    for (int s = 0; s < NR; ++s) ym = fmax(ym, fabs(y[s]));
+    ym = wmax(ym);
+    ok = kkt_eval(P, lab, x, y, ax, P.tol * (1.0 + ym), nlab, yfail);
   }
   return wall(ok);
 }

@@ -137,6 +137,20 @@ def load(path: str | None = None):
     return lib
 
 
+def unload():
+    """dlclose libpiadmm.so once every handle is closed (bench.py's exit): its code object is then
+    unregistered from the HIP runtime while the runtime -- and a profiler's tool library, when one
+    is preloaded -- are still fully alive, instead of from the library destructors that run at
+    process exit after the profiler has finalised (the round-5 exit fault)."""
+    global _lib
+    if _lib is None:
+        return
+    import _ctypes
+    h = _lib._handle
+    _lib = None
+    _ctypes.dlclose(h)
+
+
 def check(rc: int, handle=None):
     if rc != 0:
         msg = load().piadmm_last_error(handle)

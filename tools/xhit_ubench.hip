@@ -82,6 +82,9 @@ __global__ void __launch_bounds__(256) k_xhit(int reps, int Harg, unsigned long 
   P.csig = opaque[threadIdx.x & 63];                  // 0: the tables hold the empty working set
   if (l == 0) P.fstate[0] = 0;
   double xs[1] = {0.0}, zs[2] = {0.0, 0.0}, ys[2] = {0.0, 0.0};
+  piadmm_config_t cfg{};
+  cfg.dt = 0.1;
+  cfg.L = 2.7;
   // labels, signature and w' from memory (opaque to the compiler, as in k_mpc_step)
   signed char lab[2] = {(signed char)opaque[64 + l], (signed char)opaque[128 + l]};
   int na = 0, np = 0, ng = 0, bad = 0;
@@ -138,6 +141,63 @@ __global__ void __launch_bounds__(256) k_xhit(int reps, int Harg, unsigned long 
       const double u = around(ustar[0], 4);
       if (l < H) uo[l] = u;
       acc += u;
+    } else if constexpr (OP == 10 || OP == 11) {
+      // the speculative loop's protocol: waves 0, 1 run the lean repeat (OP 10) or nothing (OP 11)
+      // between barriers A and B, every other wave only takes the two barriers
+      if (OP == 10 && wv < 2) {
+        P.wq = (l < H) ? wq0 : 0.0;
+        double ustar[1];
+        bad += xhit_repeat<XGEMV_U>(P, lab, xs, ys, ustar, np) ? 0 : 1;
+        const double u = around(ustar[0], 4);
+        if (l < H) uo[l] = u;
+        acc += u;
+      }
+      __syncthreads();            // B
+      acc += uo[63] * 1e-30;      // (the verdict read)
+      __syncthreads();            // A
+    } else if constexpr (OP == 12) {
+      // a minimal replica of k_mpc_step's speculative loop (piadmm_device.hip agent_part / pair_part /
+      // roll_part): waves 0, 1 the agents' lean repeat + rounding + control store; wave 2 the pair's
+      // rollout of agent 0, the wait for the roller's flag, the collision test, the residual record
+      // and the verdict; wave 3 the roller's rollout of agent 1 and its flag; barriers A and B
+      __shared__ double s_u[2][64], s_pos[4][64];
+      __shared__ int s_vd[4], s_flag;
+      if (rep == 0 && threadIdx.x == 0) s_flag = 0;
+      __syncthreads();                                     // A
+      if (wv < 2) {
+        P.wq = (l < H) ? wq0 : 0.0;
+        double ustar[1];
+        bad += xhit_repeat<XGEMV_U>(P, lab, xs, ys, ustar, np) ? 0 : 1;
+        const double u = around(ustar[0], 4);
+        if (l < H) s_u[wv][l] = u;
+        acc += u;
+      } else if (wv == 2) {
+        double px, py, pth;
+        const double u = (l < H) ? s_u[0][l] : 0.0;
+        rollout_r(1.0, 2.0, 0.3, 10.0, 10.0 / 2.7, u, cfg, H, true, px, py, pth);
+        if (l <= H) { s_pos[0][l] = px; s_pos[1][l] = py; }
+        while (__hip_atomic_load(&s_flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != rep + 1)
+          __builtin_amdgcn_s_sleep(1);
+        wsync();
+        bool hit = false;
+        if (l <= H) {
+          const double dx = s_pos[0][l] - s_pos[2][l], dy = s_pos[1][l] - s_pos[3][l];
+          hit = dx * dx + dy * dy < 1e-6;
+        }
+        const bool act = wany(hit);
+        if (l == 0) {
+          sink[64 + (rep & 63)] = act ? 1.0 : 0.0;         // the residual record's global store
+          s_vd[0] = act; s_vd[1] = 0; s_vd[2] = 1; s_vd[3] = 0;
+        }
+      } else {
+        double px, py, pth;
+        const double u = (l < H) ? s_u[1][l] : 0.0;
+        rollout_r(-1.0, 2.0, 1.3, 9.0, 9.0 / 2.7, u, cfg, H, true, px, py, pth);
+        if (l <= H) { s_pos[2][l] = px; s_pos[3][l] = py; }
+        if (l == 0) __hip_atomic_store(&s_flag, rep + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __syncthreads();                                     // B
+      acc += s_vd[0] * 1e-30;                              // (the verdict read)
     } else if constexpr (OP == 6) {
       acc = wmax(acc + 1e-3 * opaque[192 + l]) * 1e-9;
     } else if constexpr (OP == 7) {
@@ -196,6 +256,9 @@ int main() {
   run<0, true>("qp_solve (hit)", reps);
   run<4, true>("x-step block (w', solve, round)", reps);
   run<2, true>("reduced_solve_x", reps);
+  run<12, false, 4>("speculative-loop replica (4 waves)", reps);
+  run<11, false, 4>("2 barriers, 4 waves, no work", reps);
+  run<10, false, 4>("lean repeat on 2 waves + 2 barriers", reps);
   run<4, false, 2>("x-step block (w', solve, round)", reps);
   run<4, false, 4>("x-step block (w', solve, round)", reps);
   run<4, true, 2>("x-step block (w', solve, round)", reps);
