@@ -387,7 +387,77 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
   bool spec_ok = false;       // the x-step in U may be repeated speculatively
   bool spec_ran = false;      // this iteration's speculative x-step ran
   int it = X.it0, phase = 0;  // phase 0: before barrier A(it); 1: before barrier B(it)
+  bool done = false;
   while (it < X.it_end) {
+    // ---- the steady state (r06): iterations whose x-step is a kept speculation and whose repeat
+    // is the lean table hit run in this compact loop -- barrier A(it), the repeat for it+1, barrier
+    // B(it), the verdict -- whose body holds none of the general solver's code, so its few live
+    // values stay in registers (the same barriers, statements and counters as the general loop
+    // below, which takes over at the first iteration that needs more: a z-step, the stop, the last
+    // iteration, a repeat that does not certify)
+    if (!BIG && phase == 0 && have) {
+      while (true) {
+        L.iters = it + 1;
+        if (own) {                                       // the kept speculation counts now
+          status_x |= spec_st;
+          ++n.xqp;
+          n.inexact += (spec_st & PIADMM_QP_INEXACT) ? 1 : 0;
+        }
+        unsigned long long t_sa = STAMP_T();
+        __syncthreads();                                 // A(it)
+        STAMP_ADD(ST_SYNC_A, t_sa);
+        const bool dox = own && it + 1 < X.it_end;       // (spec_ok holds: have)
+        spec_ran = dox;
+        if (dox) {
+          unsigned long long t_xs = STAMP_T();
+          const bool tl = l <= H;
+          double vx = 2.0 * c.Pnorm * (cx_own - rx_own), vy = 2.0 * c.Pnorm * (cy_own - ry_own);
+          if (cpl) {
+            vx = vx + c.rho * cpx;
+            vy = vy + c.rho * cpy;
+          }
+          const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
+          const double wsh = shdn(wt, 1);
+          qx.wq = (l < H) ? wsh : 0.0;
+          qx.qvalid = false;
+          double ustar[1];
+          if (__builtin_expect(!xhit_repeat<XGEMV_U>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x), 0)) {
+            phase = 1;                                   // the general loop's phase-1 x-step, then B(it)
+            break;
+          }
+          spec_st = 0;
+          warm_x = true;
+          const double u = around(ustar[0], c.round_decimals);
+          if (TIES && c.round_decimals >= 0) round_ties(A, t, it + 1, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
+          if (l < H) S.u[((it + 1) & 1) * 2 * H + w * H + l] = u;
+          STAMP_ADD(ST_XSTEP, t_xs);
+        }
+        unsigned long long t_sb = STAMP_T();
+        __syncthreads();                                 // B(it): the pair wave's verdict on iteration it
+        STAMP_ADD(ST_SYNC_B, t_sb);
+        L.act = X.vd[0] != 0;
+        L.flag = X.vd[2];
+        L.aliased = X.vd[3];
+        L.dis_chk = *X.vdd;
+        if (X.vd[1]) {
+          if (spec_ran && own) n.pdas_x -= 1;           // discarded by the stop: its one table hit
+          L.stopped = true;
+          done = true;
+          break;
+        }
+        if (__builtin_expect(L.act, 0)) {
+          load_cp();                                     // the speculation used the old hat, lam
+          if (spec_ran && own) n.pdas_x -= 1;           // discarded: its one table hit
+          have = false;
+        } else {
+          have = spec_ran;
+        }
+        ++it;
+        if (!have || it >= X.it_end) break;
+      }
+      if (done) break;
+      continue;
+    }
     if (phase == 0) L.iters = it + 1;
     const int tgt = phase == 0 ? it : it + 1;         // the iteration this x-step belongs to
     const bool dox = own && (phase == 0 ? !have : (it + 1 < X.it_end && spec_ok));
@@ -654,9 +724,70 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     gi_solve<2, BIG ? RM_BIG : RM_S | RM_Y>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
     STAMP_ADD(ST_ZR_SOLVE, t_pb);
   }
+  bool resume = false;   // the compact loop ran barrier A, the rollouts and the test of iteration it
   for (int it = X.it0; it < X.it_end; ++it) {
-    L.iters = it + 1;
+    if (specm && X.roll && !resume) {
+      // ---- the steady state (r06): iterations in which no pair collides run in this compact loop
+      // -- barrier A, the rollouts, the collision test, the residual record, the stop decision, the
+      // verdict, barrier B -- whose body holds none of the z-step's code (agent_part's compact loop
+      // is its counterpart).  At the first colliding iteration (or the no-edge-ever stop) the
+      // general body below takes over after the test, for the same iteration.
+      while (true) {
+        L.iters = it + 1;
+        double* const ps = S.pos + (it & 1) * 4 * H1;
+        unsigned long long t_sa = STAMP_T();
+        __syncthreads();                                 // A: every agent's controls of iteration it
+        STAMP_ADD(ST_SYNC_A, t_sa);
+        {
+          const bool nonlin_pos = c.pos_model != 0;
+          double px, py, pth;
+          unsigned long long t_ro = STAMP_T();
+          const double u = (l < H) ? S.u[(it & 1) * 2 * H + l] : 0.0;
+          rollout_r(S.xt[0], S.xt[1], S.xt[2], ra_s[0], ra_s[0] / c.L, u, c, H, nonlin_pos, px, py, pth);
+          if (l <= H) {
+            ps[0 * H1 + l] = px;
+            ps[1 * H1 + l] = py;
+          }
+          STAMP_ADD(ST_XQ, t_ro);
+          unsigned long long t_rw = STAMP_T();
+          while (__hip_atomic_load(X.rflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != it + 1)
+            __builtin_amdgcn_s_sleep(1);
+          STAMP_ADD(ST_XROLL, t_rw);
+          wsync();
+        }
+        L.act = collide<TIES>(A, X, ps, it);
+        if (__builtin_expect(L.act || (L.flag == 0 && !c.fixed_iters && !X.global), 0)) {
+          resume = true;                                 // the general body, from the test on
+          break;
+        }
+        L.flag = 1;
+        // the residual record of an iteration without a z-step (rk = sk = 0; hat unchanged)
+        unsigned long long t_tw = STAMP_T();
+        wsync();
+        if (l == 0) {
+          X.resid[2 * it + 0] = 0.0;
+          X.resid[2 * it + 1] = 0.0;
+        }
+        STAMP_ADD(ST_TERMW, t_tw);
+        const bool stop = iter_tail<TIES>(A, X, L, it, nbar);
+        if (l == 0) {
+          X.vd[0] = 0;
+          X.vd[1] = stop ? 1 : 0;
+          X.vd[2] = L.flag;
+          X.vd[3] = L.aliased;
+          *X.vdd = L.dis_chk;
+        }
+        unsigned long long t_sb = STAMP_T();
+        __syncthreads();                                 // B: the verdict
+        STAMP_ADD(ST_SYNC_B, t_sb);
+        if (stop) break;
+        if (++it >= X.it_end) break;
+      }
+      if (!resume) break;                                // stopped, or the last iteration is done
+    }
     double* const pos = S.pos + (it & 1) * 4 * H1;
+    if (!resume) {
+    L.iters = it + 1;
     unsigned long long t_sa = STAMP_T();
     __syncthreads();                                     // A: every agent's positions / controls
     STAMP_ADD(ST_SYNC_A, t_sa);
@@ -710,6 +841,8 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
       wsync();
     }
     L.act = collide<TIES>(A, X, pos, it);
+    }
+    resume = false;
     if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
       L.stopped = true;
       if (specm) {
