@@ -515,10 +515,6 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
     // two shapes' equality test)
     const char* ns = std::getenv("PIADMM_NO_SPEC");
     A.no_spec = (ns && ns[0] == '1') ? 1 : 0;
-    // PIADMM_NO_HC=1: the fused kernel with the horizon as a runtime value even where an
-    // instantiation for it exists (the equality test of the two)
-    const char* nh = std::getenv("PIADMM_NO_HC");
-    A.no_hc = (nh && nh[0] == '1') ? 1 : 0;
   }
   A.N = N;
   A.E = n_edges;

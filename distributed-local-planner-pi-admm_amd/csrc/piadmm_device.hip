@@ -187,7 +187,7 @@ struct WaveCnt {
 // Wave w < na solves agent a0 + w's x-step every outer iteration (casadi/main.py:81-106); its
 // QP state (tables, labels, warm ADMM state) stays in this wave's registers and LDS regions for
 // the whole step.  The pair's state never lives here: the pair wave owns it.
-template <bool BIG, bool TIES, int HC>
+template <bool BIG, bool TIES, int SH>
 __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const piadmm_config_t& c = A.cfg;
@@ -322,9 +322,72 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
   //  * in-kernel global termination (coop): every wave takes part in the grid barrier of the stop
   //    test, so the agents roll out their own controls and every wave runs the collision test
   //    (barrier A, then B only after a z-step).
-  const bool specm = X.spec;
-  if (!specm) {
-  for (int it = X.it0; it < X.it_end; ++it) {
+  constexpr bool specm = SH == 1;
+  if constexpr (!specm) {
+  // rep_ok: the last x-step certified without ADMM, the tables hold its working set and no z-step
+  // has changed its consensus term since -- the next x-step is that QP again (the lean repeat)
+  bool rep_ok = false, done = false;
+  int it = X.it0;
+  while (it < X.it_end) {
+    // ---- the steady state (r06, plain shape): the compact loop of iterations whose x-step is the
+    // lean repeat (agent_part's speculative-shape counterpart below); the general body takes over
+    // at the first iteration whose repeat does not certify, and after a z-step
+    if (!BIG && own && rep_ok) {
+      bool lean_fail = false;
+      while (true) {
+        L.iters = it + 1;
+        double* const ps = S.pos + (it & 1) * 4 * H1;
+        unsigned long long t_xs = STAMP_T();
+        const bool tl = l <= H;
+        double vx = 2.0 * c.Pnorm * (cx_own - rx_own), vy = 2.0 * c.Pnorm * (cy_own - ry_own);
+        if (cpl) {
+          vx = vx + c.rho * cpx;
+          vy = vy + c.rho * cpy;
+        }
+        const double wt = tl ? gx.ax * vx + gx.ay * vy : 0.0;
+        const double wsh = shdn(wt, 1);
+        qx.wq = (l < H) ? wsh : 0.0;
+        qx.qvalid = false;
+        double ustar[1];
+        if (__builtin_expect(!xhit_repeat<XGEMV_U>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x), 0)) {
+          lean_fail = true;                              // iteration it from the top, general body
+          break;
+        }
+        ++n.xqp;
+        warm_x = true;
+        const double u = around(ustar[0], c.round_decimals);
+        if (TIES && c.round_decimals >= 0) round_ties(A, t, it, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
+        double px, py, pth;
+        rollout_r(rl_x0, rl_y0, rl_th0, rl_s, rl_sl, (l < H) ? u : 0.0, c, H, nonlin_pos, px, py, pth);
+        if (l <= H) {
+          ps[(w * 2 + 0) * H1 + l] = px;
+          ps[(w * 2 + 1) * H1 + l] = py;
+        }
+        if (l < H) S.u[(it & 1) * 2 * H + w * H + l] = u;
+        STAMP_ADD(ST_XSTEP, t_xs);
+        __syncthreads();                                 // A: every agent's positions
+        L.act = collide<TIES>(A, X, ps, it);
+        if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop (:115-116)
+          L.stopped = true;
+          done = true;
+          break;
+        }
+        L.flag = 1;
+        if (__builtin_expect(L.act, 0)) {
+          __syncthreads();                               // B: hat, lam, S, D, last, S.sc
+          load_cp();
+          rep_ok = false;
+        }
+        if (iter_tail<TIES>(A, X, L, it, nbar)) {
+          done = true;
+          break;
+        }
+        if (++it >= X.it_end || !rep_ok) break;
+      }
+      if (done) break;
+      if (!lean_fail) continue;
+      rep_ok = false;
+    }
     L.iters = it + 1;
     double* const pos = S.pos + (it & 1) * 4 * H1;
     if (own) {
@@ -342,9 +405,11 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       STAMP_ADD(ST_XQ, t_xs);
       double ustar[1];
       unsigned long long t_q = STAMP_T();
+      const int admm0 = n.admm_x;
       const int stx = qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_BIG : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && it == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
+      rep_ok = !(stx & PIADMM_QP_INEXACT) && n.admm_x == admm0 && tables_match(qx, lab_x);
       status_x |= stx;
       ++n.xqp;
       n.inexact += (stx & PIADMM_QP_INEXACT) ? 1 : 0;
@@ -370,8 +435,10 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     if (__builtin_expect(L.act, 0)) {
       __syncthreads();                                   // B: hat, lam, S, D, last, S.sc
       load_cp();
+      rep_ok = false;
     }
     if (iter_tail<TIES>(A, X, L, it, nbar)) break;
+    ++it;
   }
   } else {
   bool have = false;          // the x-step of iteration `it` is already in U (a kept speculation)
@@ -425,6 +492,13 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
             phase = 1;                                   // the general loop's phase-1 x-step, then B(it)
             break;
           }
+#ifdef PIADMM_XREP
+          for (int r = 0; r < PIADMM_XREP; ++r) {        // (diagnostic build: the lean repeat again)
+            double ud[1];
+            int dp = 0;
+            (void)xhit_repeat<XGEMV_U>(qx, lab_x, xs_x, ys_x, ud, dp);
+          }
+#endif
           spec_st = 0;
           warm_x = true;
           const double u = around(ustar[0], c.round_decimals);
@@ -603,7 +677,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
 // Wave PW owns the component's pair (when it has one): the per-step pair setup (concurrent with
 // the agents' setups), the z-step QP, the hat rollouts, the dual update and the residuals
 // (casadi/main.py:121-181).  Its QP state stays in this wave's registers for the whole step.
-template <bool BIG, bool TIES, int HC>
+template <bool BIG, bool TIES, int SH>
 __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar, WaveCnt& n) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const piadmm_config_t& c = A.cfg;
@@ -707,7 +781,7 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
 
   // speculative loop shape (agent_part): this wave also rolls the agents' controls out and
   // publishes the iteration's verdict (X.vd) before barrier B
-  const bool specm = X.spec;
+  constexpr bool specm = SH == 1;
   // the agents' start states and speeds (the per-iteration rollouts of the speculative shape)
   double ra_s[2] = {0.0, 0.0};
   if (specm)
@@ -726,6 +800,36 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
   }
   bool resume = false;   // the compact loop ran barrier A, the rollouts and the test of iteration it
   for (int it = X.it0; it < X.it_end; ++it) {
+    if (!specm && !resume) {
+      // ---- the steady state (r06, plain shape): iterations in which no pair collides -- barrier
+      // A, the collision test, the residual record, the stop test (in-kernel grid barrier included)
+      // -- in a compact loop; at the first colliding iteration (or the no-edge-ever stop) the
+      // general body below takes over after the test, for the same iteration
+      bool stop = false;
+      while (true) {
+        L.iters = it + 1;
+        double* const ps = S.pos + (it & 1) * 4 * H1;
+        unsigned long long t_sa = STAMP_T();
+        __syncthreads();                                 // A: every agent's positions
+        STAMP_ADD(ST_SYNC_A, t_sa);
+        L.act = collide<TIES>(A, X, ps, it);
+        if (__builtin_expect(L.act || (L.flag == 0 && !c.fixed_iters && !X.global), 0)) {
+          resume = true;
+          break;
+        }
+        L.flag = 1;
+        unsigned long long t_tw = STAMP_T();
+        wsync();
+        if (l == 0) {
+          X.resid[2 * it + 0] = 0.0;
+          X.resid[2 * it + 1] = 0.0;
+        }
+        STAMP_ADD(ST_TERMW, t_tw);
+        stop = iter_tail<TIES>(A, X, L, it, nbar);
+        if (stop || ++it >= X.it_end) break;
+      }
+      if (!resume) break;
+    }
     if (specm && X.roll && !resume) {
       // ---- the steady state (r06): iterations in which no pair collides run in this compact loop
       // -- barrier A, the rollouts, the collision test, the residual record, the stop decision, the
@@ -744,6 +848,13 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
           unsigned long long t_ro = STAMP_T();
           const double u = (l < H) ? S.u[(it & 1) * 2 * H + l] : 0.0;
           rollout_r(S.xt[0], S.xt[1], S.xt[2], ra_s[0], ra_s[0] / c.L, u, c, H, nonlin_pos, px, py, pth);
+#ifdef PIADMM_PREP
+          for (int r = 0; r < PIADMM_PREP; ++r) {        // (diagnostic build: the rollout again)
+            double qx2, qy2, qt2;
+            rollout_r(S.xt[0], S.xt[1], S.xt[2], ra_s[0], ra_s[0] / c.L, u + px * 1e-300, c, H, nonlin_pos, qx2, qy2, qt2);
+            if (qx2 == -12345.678) S.sc[31] = qy2 + qt2;
+          }
+#endif
           if (l <= H) {
             ps[0 * H1 + l] = px;
             ps[1 * H1 + l] = py;
@@ -1027,7 +1138,6 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
 // the pair wave's chain before the verdict (two rollouts, the collision test) -- which the agent
 // waves wait for at barrier B -- holds one rollout, not two.  It takes the same barriers (A, B) and
 // stops with the pair wave's verdict.
-template <int HC>
 __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
   const piadmm_config_t& c = A.cfg;
   const int H = X.H, H1 = X.H1, l = X.l;
@@ -1070,7 +1180,7 @@ __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
 // iterations for the outputs and the propagation.
 // Wave layout: waves 0 and 1 run the agents' x-steps (agent_part), wave 2 the pair
 // (pair_part); the two loops take the same barriers and stop decisions.
-template <bool BIG, bool TIES, int HC>
+template <bool BIG, bool TIES, int SH>
 __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, int it1, int flags, int slot,
                                               int& nbar) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1084,8 +1194,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   X.vdd = &s_vdd;
   X.rflag = &s_rflag;
   if (threadIdx.x == 0) s_rflag = 0;   // (iterations count from it0 >= 0: the flag waits for it + 1)
-  X.H = HC > 0 ? HC : c.H;      // HC: the horizon compiled in (mpc_fn), 0: runtime
-  X.H1 = X.H + 1;
+  X.H = c.H;
+  X.H1 = c.H + 1;
   X.ci = blockIdx.x;
   X.w = threadIdx.x >> 6;
   X.l = lid();
@@ -1130,7 +1240,8 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   // is worth taking off the agents' chain -- measured: matlab_pi 256 x H30 0.534 -> 0.518 ms per
   // step; the linearised model's cheap rollout does not pay for the second barrier
   // (casadi_default 64 x H20 0.633 -> 0.677 ms)
-  X.spec = !X.coop && c.pos_model != 0 && !(flags & F_NOSPEC);
+  X.spec = SH == 1;
+  // (launch_mpc_step: SH = 1 iff no in-kernel grid barrier, the nonlinear position model and no F_NOSPEC)
   X.roll = X.spec && blockDim.x == NWA * WAVE;   // launch_mpc_step adds the roller wave to this shape
   X.it0 = it0;
   const bool first = X.first;
@@ -1204,9 +1315,9 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   L.act = (!first && e >= 0) ? A.edge_active[e] != 0 : false;
   L.dis_chk = (!first && e >= 0) ? A.dischk[e] : NAN;
   WaveCnt n;
-  if (X.w < NW) agent_part<BIG, TIES, HC>(A, X, L, nbar, n);
-  else if (X.w == PW) pair_part<BIG, TIES, HC>(A, X, L, nbar, n);
-  else roll_part<HC>(A, X);
+  if (X.w < NW) agent_part<BIG, TIES, SH>(A, X, L, nbar, n);
+  else if (X.w == PW) pair_part<BIG, TIES, SH>(A, X, L, nbar, n);
+  else if constexpr (SH == 1) roll_part(A, X);
   __syncthreads();
   STAMP_ADD(ST_KERNEL, t_k);
   unsigned long long t_epi = STAMP_T();
@@ -1268,7 +1379,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
 // waits for the slowest one of each step: the launch takes max_c sum_t instead of
 // sum_t max_c.  The step-to-step state (xt, labels, caches) goes through HBM inside one
 // workgroup (same CU: the barrier's workgroup-scope fences order it).
-template <bool BIG, bool TIES, int HC>
+template <bool BIG, bool TIES, int SH>
 __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int nsteps, int it0, int it1, int flags) {
 #ifdef PIADMM_STAMPS
   for (int i = threadIdx.x; i < 64 * STAMP_WAVES; i += blockDim.x) s_stamps[i] = 0ull;
@@ -1284,7 +1395,7 @@ __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int 
   }
   int nbar = 0;   // grid barriers so far (coop): parity of the termination partials
   for (int k = 0; k < nsteps; ++k) {
-    mpc_step_body<BIG, TIES, HC>(A, t0 + k, it0, it1, flags, k, nbar);
+    mpc_step_body<BIG, TIES, SH>(A, t0 + k, it0, it1, flags, k, nbar);
     __syncthreads();
   }
 #ifdef PIADMM_STAMPS
@@ -1294,6 +1405,7 @@ __global__ void __launch_bounds__(NWA * WAVE) k_mpc_step(DevArgs A, int t0, int 
 #endif
 }
 
+#ifndef PIADMM_SPEC_TU
 // Global termination partials of outer iteration `it` (one workgroup of NW*WAVE threads):
 // rk, sk summed over components, active pairs, pairs with a distance check, pairs failing it.
 // The summation order is the in-kernel (cooperative) stop test's: thread k accumulates
@@ -1368,48 +1480,57 @@ __global__ void k_pair_deff(DevArgs A) {
   A.deff[e] = d;
 }
 
-// The kernel instantiation: matrices in LDS / HBM (BIG), near-tie log compiled in or out (TIES: the log
-// costs 3-10 % of the fused kernel's time, so it is a separate instantiation, on when a handle asks for it),
-// and the horizon: BASELINE's horizons (10, 20, 30; 50 in big mode) are compiled in, so that loop bounds,
-// strides and LDS offsets are constants; every other H (and the tie log) runs the runtime-H kernel.
-// PIADMM_NO_HC=1 (DevArgs::no_hc) forces the runtime-H kernel (A/B and equality tests).
-template <bool TIES>
-static const void* mpc_fn_rt(bool big) {
-  return big ? (const void*)k_mpc_step<true, TIES, 0> : (const void*)k_mpc_step<false, TIES, 0>;
+#endif
+
+// The kernel instantiations: matrices in LDS / HBM (BIG); the near-tie log compiled in or out (TIES:
+// the log costs 3-10 % of the fused kernel's time, so it is a separate instantiation, on when a handle
+// asks for it); and the loop shape (SH: 0 plain, 1 speculative).  The two shapes are separate kernels
+// in separate translation units (this file; piadmm_device_spec.hip includes it with PIADMM_SPEC_TU):
+// each kernel holds one loop shape, so the register allocation of one shape's hot loops is not shaped
+// by the other's code, and the two compile in parallel.
+#ifdef PIADMM_SPEC_TU
+const void* mpc_fn_spec(bool big, bool ties) {
+  if (big) return ties ? (const void*)k_mpc_step<true, true, 1> : (const void*)k_mpc_step<true, false, 1>;
+  return ties ? (const void*)k_mpc_step<false, true, 1> : (const void*)k_mpc_step<false, false, 1>;
 }
-static const void* mpc_fn(bool big, bool ties, int H, bool no_hc) {
-#ifdef PIADMM_ONLY_HC
-  // resource-report build of one instantiation (never linked)
-  (void)big; (void)ties; (void)H; (void)no_hc;
-  return (const void*)k_mpc_step<(PIADMM_ONLY_HC > HMAX), false, PIADMM_ONLY_HC>;
+#ifdef PIADMM_STAMPS
+int spec_set_stamps(unsigned long long* p) {     // this translation unit's copy of g_stamps
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(void*)) == hipSuccess ? 0 : -1;
+}
+#endif
 #else
-  if (ties) return mpc_fn_rt<true>(big);
-#ifndef PIADMM_NO_HC_BUILD
-  if (!no_hc) {
-    switch (H) {
-      case 10: return (const void*)k_mpc_step<false, false, 10>;
-      case 20: return (const void*)k_mpc_step<false, false, 20>;
-      case 30: return (const void*)k_mpc_step<false, false, 30>;
-      case 50: return (const void*)k_mpc_step<true, false, 50>;
-      default: break;
-    }
-  }
+const void* mpc_fn_spec(bool big, bool ties);    // piadmm_device_spec.hip
+#ifdef PIADMM_STAMPS
+int spec_set_stamps(unsigned long long* p);
 #endif
-  return mpc_fn_rt<false>(big);
-#endif
+static const void* mpc_fn(bool big, bool ties, bool spec) {
+  if (spec) return mpc_fn_spec(big, ties);
+  if (big) return ties ? (const void*)k_mpc_step<true, true, 0> : (const void*)k_mpc_step<true, false, 0>;
+  return ties ? (const void*)k_mpc_step<false, true, 0> : (const void*)k_mpc_step<false, false, 0>;
+}
+
+// The speculative loop shape where it pays: no in-kernel grid barrier (F_COOP), the nonlinear
+// position model (MATLAB's dynamic_update_local, a sincos rollout per iteration, worth taking off
+// the agents' chain -- measured: matlab_pi 256 x H30 0.534 -> 0.518 ms per step; the linearised
+// model's cheap rollout does not pay for the second barrier, casadi_default 64 x H20 0.633 -> 0.677
+// ms), and not PIADMM_NO_SPEC=1 (DevArgs::no_spec, the plain loop everywhere).
+static bool spec_shape(const DevArgs& a, int flags) {
+  return !(flags & F_COOP) && a.cfg.pos_model != 0 && !(flags & F_NOSPEC) && a.no_spec == 0;
 }
 
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s) {
   const size_t sh = lds_bytes(a.cfg.H, a.cfg.precision);
   const bool big = a.cfg.H > HMAX;
+  const bool spec = spec_shape(a, flags);
 #ifdef PIADMM_STAMPS
   static unsigned long long* last = nullptr;
   if (a.stamps != last) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &a.stamps, sizeof(void*)) != hipSuccess) return -1;
+    if (spec_set_stamps(a.stamps) != 0) return -1;
     last = a.stamps;
   }
 #endif
-  const void* fn = mpc_fn(big, a.tie_on != 0, a.cfg.H, a.no_hc != 0);
+  const void* fn = mpc_fn(big, a.tie_on != 0, spec);
   if (set_dyn_lds(fn, sh) != 0) return -1;
   if (flags & F_COOP) {
     // every workgroup must be resident for the grid barrier: the cooperative launch fails
@@ -1420,16 +1541,13 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NWT * WAVE), args, (unsigned)sh, s));
   }
   (void)hipGetLastError();   // a stale error of an earlier runtime call is not this launch's
-  // the speculative loop (no grid barrier, the nonlinear position model: mpc_step_body) runs with
-  // the roller wave; PIADMM_NO_ROLLER=1 keeps three waves (the pair wave rolls both agents out)
+  // the speculative loop runs with the roller wave; PIADMM_NO_ROLLER=1 keeps three waves (the pair
+  // wave rolls both agents out)
   static const bool no_roller = [] {
     const char* e = std::getenv("PIADMM_NO_ROLLER");
     return e && e[0] == '1';
   }();
-  // PIADMM_NO_SPEC=1 (DevArgs::no_spec): the plain loop shape (three waves) everywhere
-  const bool no_spec = a.no_spec != 0;
-  if (no_spec) flags |= F_NOSPEC;
-  const int nt = (a.cfg.pos_model != 0 && !no_roller && !no_spec ? NWA : NWT) * WAVE;
+  const int nt = (spec && !no_roller ? NWA : NWT) * WAVE;
   DevArgs aa = a;
   void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
   return launch_rc(hipLaunchKernel(fn, dim3(a.C), dim3(nt), args, sh, s));
@@ -1443,7 +1561,7 @@ bool coop_fits(const DevArgs& a, int device) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return false;
   const size_t sh = lds_bytes(a.cfg.H, a.cfg.precision);
   const bool big = a.cfg.H > HMAX;
-  const void* fn = mpc_fn(big, a.tie_on != 0, a.cfg.H, a.no_hc != 0);
+  const void* fn = mpc_fn(big, a.tie_on != 0, false);   // (the cooperative launch runs the plain shape)
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return false;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NWT * WAVE, sh) != hipSuccess) return false;
   return (long long)per * ncu >= (long long)a.C;
@@ -1527,5 +1645,7 @@ int launch_pair_deff(const DevArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_pair_deff, dim3((a.E + 255) / 256), dim3(256), 0, s, a);
   return launch_rc(hipGetLastError());
 }
+
+#endif  // PIADMM_SPEC_TU
 
 }  // namespace pd

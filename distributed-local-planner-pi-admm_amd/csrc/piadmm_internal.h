@@ -53,7 +53,6 @@ struct DevArgs {
   int x_gi;                 // x-step working-set changes by the dual active set (1); the step's first x-QP
                             // without the labels' reduced solve (2), started cold (3); all cold (4); PIADMM_X_SOLVER
   int no_spec;              // 1: k_mpc_step keeps the plain loop shape (PIADMM_NO_SPEC=1, read at set_scenario)
-  int no_hc;                // 1: k_mpc_step with the horizon at run time (PIADMM_NO_HC=1), not compiled in
   // scenario (read-only during a step)
   const double* spd;        // N
   const double* ref;        // N*2*T
