@@ -1321,7 +1321,9 @@ __device__ __forceinline__ bool tables_match(const QP<NV>& P, const signed char*
 // reach their rows through lane permutes instead of an LDS store, sync and gather.  Results are
 // bit-identical; on a failed certificate (not expected: the same QP certified before) it gives its
 // solve back to the counter and returns false, and the caller runs qp_solve.
-template <int XU>
+// TT: the transposed LDS tables (LDS mode, reduced_solve_x<XU, true>); false: the big mode's tables in
+// HBM / L2, lane = column (reduced_solve_x<XU, false>, the same batches of XU rows).
+template <int XU, bool TT = true>
 __device__ __forceinline__ bool xhit_repeat(QP<1>& P, const signed char* lab, double* xs, double* ys, double* x_out,
                                             int& n_pdas) {
   const int l = lid(), H = P.H;
@@ -1340,23 +1342,67 @@ __device__ __forceinline__ bool xhit_repeat(QP<1>& P, const signed char* lab, do
   vb_q[l] = (l < H) ? P.wq : 0.0;
   wsync();
   const int lc = (l < H) ? l : 0, la = (l < m) ? l : 0;
-  const int gld = unif(gt_ld(H)), xsd = unif(P.xld);
-  const ldsd2* gr = (const ldsd2*)(lds_ptr(P.G) + lc * gld);
-  const ldsd2* xr2 = (const ldsd2*)(lds_ptr(P.XT) + la * xsd);
-  const ldsd2* q2 = (const ldsd2*)lds_ptr(vb_q);
-  const int hp = unif((H + 1) >> 1);
-  double ag = 0.0, ax = 0.0, ag1 = 0.0, ax1 = 0.0;
-  switch (hp) {
-    case 15: hit_pass<15>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
-    case 10: hit_pass<10>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
-    case 5: hit_pass<5>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
-    default: hit_pass<0>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+  double ag = 0.0, ax = 0.0, lam;
+  if constexpr (TT) {
+    const int gld = unif(gt_ld(H)), xsd = unif(P.xld);
+    const ldsd2* gr = (const ldsd2*)(lds_ptr(P.G) + lc * gld);
+    const ldsd2* xr2 = (const ldsd2*)(lds_ptr(P.XT) + la * xsd);
+    const ldsd2* q2 = (const ldsd2*)lds_ptr(vb_q);
+    const int hp = unif((H + 1) >> 1);
+    double ag1 = 0.0, ax1 = 0.0;
+    switch (hp) {
+      case 15: hit_pass<15>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+      case 10: hit_pass<10>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+      case 5: hit_pass<5>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+      default: hit_pass<0>(gr, xr2, q2, hp, ag, ag1, ax, ax1); break;
+    }
+    ag += ag1;
+    ax += ax1;
+    const ldsd* XT = lds_ptr(P.XT);
+    lam = (l < m) ? -ax - XT[l * xsd + H] : 0.0;                    // lane a: multiplier of W row a
+    ag = lds_ptr(P.G)[H * gld + lc] - ag;
+  } else {
+    // (reduced_solve_x<XU, false>'s pass, statement for statement)
+    const double* G = P.G;
+    const double* XT = P.XT;
+    const int Hf = H - H % XU;
+    const double* gp = G + lc;
+    const double* xp = XT + la;
+    const int xsd = P.xld;
+    for (int j0 = 0; j0 < Hf; j0 += XU) {
+      double qv[XU], gv[XU], xv[XU];
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        qv[u] = vb_q[j0 + u];
+        gv[u] = gp[u * H];
+        xv[u] = xp[u * xsd];
+      }
+      gp += XU * H;
+      xp += XU * xsd;
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        ag += gv[u] * qv[u];
+        ax += xv[u] * qv[u];
+      }
+    }
+    if (Hf < H) {
+      double qv[XU], gv[XU], xv[XU];
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        const int j = min(Hf + u, H - 1);
+        qv[u] = vb_q[Hf + u];
+        gv[u] = G[j * H + lc];
+        xv[u] = XT[j * xsd + la];
+      }
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        ag += gv[u] * qv[u];
+        ax += xv[u] * qv[u];
+      }
+    }
+    lam = (l < m) ? -ax - XT[H * P.xld + l] : 0.0;
+    ag = G[H * H + lc] - ag;
   }
-  ag += ag1;
-  ax += ax1;
-  const ldsd* XT = lds_ptr(P.XT);
-  const double lam = (l < m) ? -ax - XT[l * xsd + H] : 0.0;          // lane a: multiplier of W row a
-  ag = lds_ptr(P.G)[H * gld + lc] - ag;
   double x[1] = {(l < H) ? ag : 0.0}, y[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {

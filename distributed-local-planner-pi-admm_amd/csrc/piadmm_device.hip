@@ -332,7 +332,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     // ---- the steady state (r06, plain shape): the compact loop of iterations whose x-step is the
     // lean repeat (agent_part's speculative-shape counterpart below); the general body takes over
     // at the first iteration whose repeat does not certify, and after a z-step
-    if (!BIG && own && rep_ok) {
+    if (own && rep_ok && !qx.t32) {
       bool lean_fail = false;
       while (true) {
         L.iters = it + 1;
@@ -349,7 +349,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
         qx.wq = (l < H) ? wsh : 0.0;
         qx.qvalid = false;
         double ustar[1];
-        if (__builtin_expect(!xhit_repeat<XGEMV_U>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x), 0)) {
+        if (__builtin_expect(!xhit_repeat<BIG ? 8 : XGEMV_U, !BIG>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x), 0)) {
           lean_fail = true;                              // iteration it from the top, general body
           break;
         }
@@ -462,7 +462,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
     // values stay in registers (the same barriers, statements and counters as the general loop
     // below, which takes over at the first iteration that needs more: a z-step, the stop, the last
     // iteration, a repeat that does not certify)
-    if (!BIG && phase == 0 && have) {
+    if (phase == 0 && have && !qx.t32) {
       while (true) {
         L.iters = it + 1;
         if (own) {                                       // the kept speculation counts now
@@ -488,7 +488,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
           qx.wq = (l < H) ? wsh : 0.0;
           qx.qvalid = false;
           double ustar[1];
-          if (__builtin_expect(!xhit_repeat<XGEMV_U>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x), 0)) {
+          if (__builtin_expect(!xhit_repeat<BIG ? 8 : XGEMV_U, !BIG>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x), 0)) {
             phase = 1;                                   // the general loop's phase-1 x-step, then B(it)
             break;
           }
@@ -496,7 +496,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
           for (int r = 0; r < PIADMM_XREP; ++r) {        // (diagnostic build: the lean repeat again)
             double ud[1];
             int dp = 0;
-            (void)xhit_repeat<XGEMV_U>(qx, lab_x, xs_x, ys_x, ud, dp);
+            (void)xhit_repeat<BIG ? 8 : XGEMV_U, !BIG>(qx, lab_x, xs_x, ys_x, ud, dp);
           }
 #endif
           spec_st = 0;
@@ -555,7 +555,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       const int admm0 = n.admm_x;
       // phase 1 repeats the certified table hit of the x-step in U (spec_ok): the lean repeat on the
       // transposed tables (LDS mode), qp_solve when it does not certify (or in big mode)
-      const bool lean = !BIG && phase == 1 && xhit_repeat<XGEMV_U>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x);
+      const bool lean = phase == 1 && !qx.t32 && xhit_repeat<BIG ? 8 : XGEMV_U, !BIG>(qx, lab_x, xs_x, ys_x, ustar, n.pdas_x);
       const int stx = lean ? 0 : qp_solve<1, false, BIG ? 8 : XGEMV_U, BIG ? RM_BIG : RM_S | RM_T>(qx, xs_x, zs_x, ys_x, lab_x, warm_x, c.max_inner, c.polish_every, xfac,
                                qx.fld, ustar, n.admm_x, n.pdas_x, n.gi, (A.x_gi >= 2 && first && tgt == X.it0) ? min(A.x_gi - 1, 2) : (A.x_gi == 4 ? 3 : 0));
       STAMP_ADD(ST_XQP, t_q);
