@@ -397,6 +397,7 @@ def main_obca(args, world, rank, local_rank):
     value = n * K * world / wall
     bytes_launch = n * (obca.REC * 8 + obca.OUT * 8 + 12)
     achieved = bytes_launch / (ev_ms / 1e3) / 1e9
+    traffic = latest_profile("traffic", f"obca{n}")     # PMC bytes per launch (tools/profile_line.sh)
     line = {
         "metric": "OBCA local NLP solves/s (batched SQP, two-vehicle overtaking, N_horz 8)",
         "value": value, "unit": "local_nlp_solves/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
@@ -410,7 +411,9 @@ def main_obca(args, world, rank, local_rank):
                    "sqp_iters_mean": float(res.iters.mean()), "qp_steps_mean": float(res.qp_steps.mean()),
                    "parallelism": f"independent problems per GPU ({world} GPU(s)), no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": "obca::k_obca_sqp",
+                     "frac": achieved / PEAK_HBM_GBS,
+                     "traffic": traffic["hbm_bytes_per_step"] if traffic else None,
+                     "traffic_source": traffic["_file"] if traffic else None, "kernel": "obca::k_obca_sqp",
                      "avg_launch_ms": ev_ms, "algorithmic_bytes_per_launch": bytes_launch,
                      "note": "latency bound: 520 doubles of HBM traffic per problem, the SQP state stays in LDS; "
                              "see DESIGN.md section 9"},
