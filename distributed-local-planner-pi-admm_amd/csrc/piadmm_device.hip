@@ -453,6 +453,9 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
   // is never speculated on (tests/test_gpu_modes.py: the two loop shapes are equal).
   bool spec_ok = false;       // the x-step in U may be repeated speculatively
   bool spec_ran = false;      // this iteration's speculative x-step ran
+  // (TIES) a speculative x-step's unrounded controls: its round ties are logged once the verdict
+  // keeps it (a discarded speculation's rounding never happened in the reference's loop)
+  double tie_u = 0.0;
   int it = X.it0, phase = 0;  // phase 0: before barrier A(it); 1: before barrier B(it)
   bool done = false;
   while (it < X.it_end) {
@@ -502,7 +505,7 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
           spec_st = 0;
           warm_x = true;
           const double u = around(ustar[0], c.round_decimals);
-          if (TIES && c.round_decimals >= 0) round_ties(A, t, it + 1, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
+          if constexpr (TIES) tie_u = ustar[0];
           if (l < H) S.u[((it + 1) & 1) * 2 * H + w * H + l] = u;
           STAMP_ADD(ST_XSTEP, t_xs);
         }
@@ -525,6 +528,8 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
           have = false;
         } else {
           have = spec_ran;
+          if (TIES && c.round_decimals >= 0 && spec_ran)
+            round_ties(A, t, it + 1, PIADMM_TIE_ROUND_U, X.a0 + w, 0, tie_u, l < H);
         }
         ++it;
         if (!have || it >= X.it_end) break;
@@ -583,7 +588,12 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       warm_x = true;
       unsigned long long t_rd = STAMP_T();
       const double u = around(ustar[0], c.round_decimals);
-      if (TIES && c.round_decimals >= 0) round_ties(A, t, tgt, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
+      if (TIES && c.round_decimals >= 0) {
+        if (phase == 0)
+          round_ties(A, t, tgt, PIADMM_TIE_ROUND_U, X.a0 + w, 0, ustar[0], l < H);
+        else
+          tie_u = ustar[0];                              // logged if the verdict keeps it
+      }
       STAMP_ADD(ST_ROUND, t_rd);
       if (l < H) S.u[(tgt & 1) * 2 * H + w * H + l] = u;
       STAMP_ADD(ST_XSTEP, t_xs);
@@ -616,6 +626,8 @@ __device__ __forceinline__ void agent_part(const DevArgs& A, const StepCtx& X, L
       have = false;
     } else {
       have = spec_ran;
+      if (TIES && c.round_decimals >= 0 && spec_ran)
+        round_ties(A, t, it + 1, PIADMM_TIE_ROUND_U, X.a0 + w, 0, tie_u, l < H);
     }
     ++it;
     phase = 0;
@@ -1509,13 +1521,13 @@ static const void* mpc_fn(bool big, bool ties, bool spec) {
   return ties ? (const void*)k_mpc_step<false, true, 0> : (const void*)k_mpc_step<false, false, 0>;
 }
 
-// The speculative loop shape where it pays: no in-kernel grid barrier (F_COOP), the nonlinear
-// position model (MATLAB's dynamic_update_local, a sincos rollout per iteration, worth taking off
-// the agents' chain -- measured: matlab_pi 256 x H30 0.534 -> 0.518 ms per step; the linearised
-// model's cheap rollout does not pay for the second barrier, casadi_default 64 x H20 0.633 -> 0.677
-// ms), and not PIADMM_NO_SPEC=1 (DevArgs::no_spec, the plain loop everywhere).
+// The speculative loop shape wherever there is no in-kernel grid barrier (F_COOP) and not
+// PIADMM_NO_SPEC=1 (DevArgs::no_spec, the plain loop everywhere).  With the compact steady-state
+// loops it pays for both position models -- measured (iteration slope, tools/iter_slope.py):
+// matlab_pi 256 x H30 (nonlinear sincos rollout) and casadi_default 64 x H20 (linearised rollout)
+// 4.6k -> 3.3k cycles per outer iteration, configs[1] fixed 0.469 -> 0.377 ms per step.
 static bool spec_shape(const DevArgs& a, int flags) {
-  return !(flags & F_COOP) && a.cfg.pos_model != 0 && !(flags & F_NOSPEC) && a.no_spec == 0;
+  return !(flags & F_COOP) && !(flags & F_NOSPEC) && a.no_spec == 0;
 }
 
 int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s) {

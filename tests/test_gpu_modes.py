@@ -242,7 +242,7 @@ def test_fp32_tables_config5_tolerance_study(Solver):
     assert max(du_o, dx_o, du_g, dx_g) <= 1e-5
 
 
-@pytest.mark.parametrize("case", ["bench_fixed", "natural", "inexact", "big_fixed"])
+@pytest.mark.parametrize("case", ["bench_fixed", "natural", "inexact", "big_fixed", "linear_fixed", "linear_natural"])
 def test_speculative_loop_equals_plain_loop(Solver, monkeypatch, case):
     """The fused kernel's speculative loop shape (the agent waves solve iteration it+1's x-step
     while the pair wave rolls out, tests and decides iteration it; casadi/main.py:81-181) against
@@ -254,18 +254,23 @@ def test_speculative_loop_equals_plain_loop(Solver, monkeypatch, case):
     would not hold, so even uncertified (ADMM-capped) x-QPs see the plain loop's state.  Cases:
     the bench's tiles (matlab_pi 256 x H30 shape, fixed 100 outer iterations), natural
     per-component termination, and x-QPs forced uncertified (PIADMM_X_SOLVER=pdas with 3 ADMM
-    iterations: INEXACT answers depend on the warm state, which the speculation must not touch)."""
-    H = {"bench_fixed": 30, "big_fixed": 40}.get(case, 15)
+    iterations: INEXACT answers depend on the warm state, which the speculation must not touch), and
+    the casadi_default preset's linearised position model (configs[1]'s 64 x H20 shape, fixed and
+    natural)."""
+    H = {"bench_fixed": 30, "big_fixed": 40, "linear_fixed": 20}.get(case, 15)
     kw = dict(H=H)
-    if case in ("bench_fixed", "big_fixed"):
+    if case in ("bench_fixed", "big_fixed", "linear_fixed"):
         kw.update(fixed_iters=1, term_global=1)
+    if case == "linear_fixed":
+        kw.update(max_outer=60)
     if case == "big_fixed":
         kw.update(max_outer=40)       # big mode (H > 32): the tables in HBM / L2, the lean repeat's global pass
     if case == "inexact":
         kw.update(max_inner=3, fixed_iters=1, max_outer=12)
         monkeypatch.setenv("PIADMM_X_SOLVER", "pdas")
-    cfg = config.matlab_pi(**kw)
-    n_tiles, n_steps = {"bench_fixed": (32, 6), "big_fixed": (16, 4)}.get(case, (16, 14))
+    cfg = (config.casadi_default if case.startswith("linear") else config.matlab_pi)(**kw)
+    assert cfg.pos_model == (config.POS_LINEAR if case.startswith("linear") else config.POS_NONLINEAR)
+    n_tiles, n_steps = {"bench_fixed": (32, 6), "big_fixed": (16, 4), "linear_fixed": (32, 6)}.get(case, (16, 14))
     scn = scenario.tiled(n_tiles, H, n_steps=n_steps + 2, seed=5)
     runs = []
     for nospec in ("0", "1"):

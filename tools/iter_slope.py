@@ -2,7 +2,8 @@
 matlab_pi, fixed iterations, global scope) timed at several fixed iteration counts M; the slope of
 ms per MPC step against M is one outer iteration of the slowest component's chain (the per-step
 costs -- setup, the first iteration's solves, the z-step -- are the intercept).
-    python3 tools/iter_slope.py [lib ...]      (PIADMM_LIB paths; default: the built library)"""
+    python3 tools/iter_slope.py [lib ...]      (PIADMM_LIB paths; default: the built library)
+    PIADMM_SLOPE_JOB=preset,H,tiles selects another job (e.g. casadi_default,20,32: configs[1])."""
 import json
 import os
 import subprocess
@@ -12,12 +13,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r'''
 import sys, json
 sys.path[:0] = [sys.argv[1], sys.argv[1] + "/distributed-local-planner-pi-admm_amd"]
+import os
 from piadmm import config, scenario
 from piadmm.solver import PI_ADMM_MI355X
+preset, H, tiles = (os.environ.get("PIADMM_SLOPE_JOB") or "matlab_pi,30,128").split(",")
+H, tiles = int(H), int(tiles)
 out = {}
 for M in (20, 60, 100, 140):
-    cfg = config.matlab_pi(H=30, fixed_iters=1, max_outer=M, term_global=1)
-    scn = scenario.tiled(128, 30, n_steps=25, perturb=True, seed=0)
+    cfg = config.PRESETS[preset](H=H, fixed_iters=1, max_outer=M, term_global=1)
+    scn = scenario.tiled(tiles, H, n_steps=25, perturb=True, seed=0)
     with PI_ADMM_MI355X(cfg, scn) as s:
         s.time_steps(0, 5)
         s.set_xt(scn.xt0)
