@@ -123,6 +123,30 @@ __device__ __forceinline__ double shdn(double v, int o) {
 __device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
 __device__ __forceinline__ bool wall(bool p) { return __ballot(!p) == 0ull; }
 
+// The in-kernel grid barrier of the natural global stop test (one rank, cooperative launch: every
+// workgroup resident, every one calls it the same number of times).  Each workgroup release-stores
+// the barrier's epoch into its own word -- no read-modify-write on one shared counter to serialise
+// the arrivals -- and its first wave polls every word until all hold the epoch (or a later one).
+// Measured per barrier with the partials' reduction (tools/gbar_ubench.hip): 128 workgroups
+// 14.3 us with cooperative_groups' grid sync -> 6.0 us; 32 workgroups 6.8 -> 3.0 us.  Epochs grow
+// across launches (DevArgs::gbar_base), so the words are never reset.  The caller's thread 0
+// stores its partials before the call: its release store orders them.
+__device__ __forceinline__ void grid_flag_barrier(unsigned long long* words, int n, int me, unsigned long long epoch) {
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&words[me], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < WAVE) {
+    while (true) {
+      bool ok = true;
+      for (int k = threadIdx.x; k < n; k += WAVE)
+        ok = ok && __hip_atomic_load(&words[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+      if (wall(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
 // DPP move restricted to the 16-lane rows in ROWS (other rows read 0).
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dppd_rows(double v) {

@@ -595,6 +595,7 @@ static int32_t set_scenario_impl(piadmm_handle_t h, const double* spd, const dou
       rc |= dalloc(h, &A.gi_snap, snap_n);
   }
   rc |= dalloc(h, &A.gpart, (size_t)2 * C * 5);
+  rc |= dalloc(h, &A.gbar, (size_t)C);
   rc |= dalloc(h, &A.ghist, (size_t)h->step_cap * std::max(h->cfg.max_outer, 1) * 2);
   rc |= dalloc(h, &A.giters, (size_t)h->step_cap);
   rc |= dalloc(h, &A.gctl, 4);

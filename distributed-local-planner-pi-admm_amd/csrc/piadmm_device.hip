@@ -20,7 +20,7 @@
 //    primal-dual active-set (PDAS) polish on the reduced KKT system.
 // tools/qp_sim.py and tools/gi_sim.py are the NumPy prototypes of this math.
 // Shared device code: pd_common.h (wave primitives, rollouts), pd_qp.h (QP solver), pd_setup.h.
-#include <hip/hip_cooperative_groups.h>
+#include <atomic>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -126,11 +126,12 @@ __device__ __forceinline__ bool iter_tail(const DevArgs& A, const StepCtx& X, Lo
       for (int q = 0; q < 5; ++q)
         __hip_atomic_store(&part[ci * 5 + q], pv[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    cooperative_groups::this_grid().sync();
+    grid_flag_barrier(A.gbar, A.C, ci, A.gbar_base + (unsigned long long)nbar);
     {
       // the first NT threads load (components tid, tid + NT, ...), then five threads sum the
       // per-thread partials in thread order: a fixed order, identical in every workgroup and equal
-      // to k_term_partials' (the host-decided path)
+      // to k_term_partials' (the host-decided path).  The sum stops at min(C, NT) terms: the
+      // threads beyond hold +0.0, which leaves the sum (never -0.0: it starts at +0.0) unchanged
       constexpr int NT = NW * WAVE;
       double v[5] = {0, 0, 0, 0, 0};
       if ((int)threadIdx.x < NT)
@@ -145,7 +146,8 @@ __device__ __forceinline__ bool iter_tail(const DevArgs& A, const StepCtx& X, Lo
       __syncthreads();
       if (threadIdx.x < 5) {
         double tot = 0.0;
-        for (int k = 0; k < NT; ++k) tot += red[threadIdx.x * NT + k];
+        const int nk = min(A.C, NT);
+        for (int k = 0; k < nk; ++k) tot += red[threadIdx.x * NT + k];
         S.sc[16 + threadIdx.x] = tot;
       }
     }
@@ -1548,6 +1550,7 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     // every workgroup must be resident for the grid barrier: the cooperative launch fails
     // (and the caller falls back to host-decided termination) rather than deadlock
     DevArgs aa = a;
+    aa.gbar_base = launch_coop_epoch(nsteps, a.cfg.max_outer);
     void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
     (void)hipGetLastError();
     return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NWT * WAVE), args, (unsigned)sh, s));
@@ -1563,6 +1566,12 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
   DevArgs aa = a;
   void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
   return launch_rc(hipLaunchKernel(fn, dim3(a.C), dim3(nt), args, sh, s));
+}
+
+unsigned long long launch_coop_epoch(int nsteps, int max_outer) {
+  static std::atomic<unsigned long long> next{0};
+  const unsigned long long span = (unsigned long long)std::max(nsteps, 1) * (unsigned long long)(std::max(max_outer, 1) + 2) + 2;
+  return next.fetch_add(span);
 }
 
 // Can every workgroup of a k_mpc_step launch be resident at once (cooperative launch)?

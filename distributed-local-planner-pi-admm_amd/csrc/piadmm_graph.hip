@@ -27,7 +27,6 @@
 // grid barrier (cooperative launch, one rank) or one launch per outer iteration with the stop
 // decided on the host from all-reduced partials (RCCL).  F_XONLY / F_ZONLY split an iteration
 // launch at the position exchange of a sharded job (piadmm_capi.cpp).
-#include <hip/hip_cooperative_groups.h>
 
 #include "pd_setup.h"
 
@@ -784,7 +783,7 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
         for (int q = 0; q < 5; ++q)
           __hip_atomic_store(&part[ci * 5 + q], cp[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      cooperative_groups::this_grid().sync();
+      grid_flag_barrier(A.gbar, A.C, ci, A.gbar_base + (unsigned long long)nbar);
       double v[5] = {0, 0, 0, 0, 0};
       for (int k = threadIdx.x; k < A.C; k += blockDim.x)
 #pragma unroll
@@ -795,7 +794,8 @@ __device__ __forceinline__ void graph_step_body(const DevArgs& A, int t, int it0
       __syncthreads();
       if (threadIdx.x < 5) {
         double tot = 0.0;
-        for (int k = 0; k < GW * WAVE; ++k) tot += s_red[threadIdx.x][k];
+        const int nk = min(A.C, GW * WAVE);            // (the threads beyond hold +0.0)
+        for (int k = 0; k < nk; ++k) tot += s_red[threadIdx.x][k];
         s_tot[threadIdx.x] = tot;
       }
       __syncthreads();
@@ -974,6 +974,7 @@ int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int
   if (set_dyn_lds(fn, sh) != 0) return -1;
   if (flags & F_COOP) {
     DevArgs aa = a;
+    aa.gbar_base = launch_coop_epoch(nsteps, a.cfg.max_outer);
     void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
     (void)hipGetLastError();
     return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(GW * WAVE), args, (unsigned)sh, s));

@@ -108,6 +108,9 @@ struct DevArgs {
   size_t gi_wide_stride;    // giw_stride(H)
   double* gi_snap;          // graph mode: E * (64*64 + 64*2H + 64) the pair's last dual active set: S^-1 | Y | hinge regimes
   double* gpart;            // 2*C*5 coop: per-component termination partials (iteration parity)
+  unsigned long long* gbar;  // C coop: the grid barrier's arrival epochs, one word per workgroup (pd_common.h
+                            //   grid_flag_barrier); zeroed once, epochs only grow
+  unsigned long long gbar_base;  // coop: epoch base of this launch (set per cooperative launch, launch_coop_epoch)
   double* ghist;            // step_cap*max_outer*2 coop: global (rk, sk) history per step
   int* giters;              // step_cap coop: global outer iterations per step
   int* gctl;                // 4: device-decided global stop (F_DEVSTOP): stop, nanlast, iterations, flag
@@ -261,6 +264,9 @@ constexpr int F_INITONLY = 256;
 constexpr int F_NOSPEC = 512;
 
 int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
+// The epoch base of a cooperative launch of nsteps MPC steps: larger than every epoch an earlier
+// launch of the process used (a launch's barriers take base + 1 .. base + nsteps * max_outer)
+unsigned long long launch_coop_epoch(int nsteps, int max_outer);
 // candidate-pair detection (piadmm_detect.hip)
 int launch_detect_count(const double* xy, const double* r, int n, double inv_cs, unsigned T, unsigned* key, int* cnt,
                         int* start, int* fill, int* order, int* pcnt, int* off, long long* total, long long* bsum,
