@@ -146,7 +146,12 @@ __device__ __forceinline__ bool iter_tail(const DevArgs& A, const StepCtx& X, Lo
       __syncthreads();
       if (threadIdx.x < 5) {
         double tot = 0.0;
+#ifndef PIADMM_STAMPS
         const int nk = min(A.C, NT);
+#else
+        const int nk = NT;   // (the stamps build: ROCm 7.2's backend rejects the variable trip count there,
+                             // "Operand has incorrect register class"; the same sum)
+#endif
         for (int k = 0; k < nk; ++k) tot += red[threadIdx.x * NT + k];
         S.sc[16 + threadIdx.x] = tot;
       }

@@ -13,7 +13,8 @@ tiles = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 natural = len(sys.argv) > 4 and sys.argv[4] == "natural"   # argv[4]: natural | fixed
-cfg = config.matlab_pi(H=H, fixed_iters=0 if natural else 1, max_outer=100, term_global=int(natural))
+cfg = config.PRESETS[os.environ.get("PIADMM_STAMPS_PRESET", "matlab_pi")](H=H, fixed_iters=0 if natural else 1, max_outer=100,
+                                                                  term_global=int(natural))
 warm = int(sys.argv[5]) if len(sys.argv) > 5 else 0   # untimed steps first (step 0 builds the caches)
 scn = scenario.tiled(tiles, H, n_steps=warm + steps)
 s = PI_ADMM_MI355X(cfg, scn)
