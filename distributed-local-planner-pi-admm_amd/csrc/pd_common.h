@@ -42,7 +42,9 @@ enum StampSlot { ST_SETUP_X = 0, ST_SETUP_Z, ST_XSTEP, ST_XQP, ST_XRED, ST_XROLL
                  ST_N_GIZ = 40, ST_N_GIX, ST_N_ZQP, ST_N_ZFAIL, ST_N_XREBUILD,
                  // dual active set detail (pair QPs only): cycles of fwd / bwd / Y pass / drop, and counts
                  ST_GI_FWD = 45, ST_GI_BWD, ST_GI_YPASS, ST_GI_DROP, ST_N_DROP, ST_N_APPEND, ST_N_WARMROW,
-                 ST_SUM_M, ST_SUM_MEND, ST_N_GICALL, NSTAMP = 64 };
+                 ST_SUM_M, ST_SUM_MEND, ST_N_GICALL,
+                 // the pair's warm build per appended row: P^-1 n + A y (prep), S^-1 v + pivot, the bordering
+                 ST_WARM_PREP = 56, ST_WARM_SINV, ST_WARM_APPEND, NSTAMP = 64 };
 
 // ============================================================ address spaces
 // The kernels' scratch pointers travel through structs that also carry HBM pointers, so the

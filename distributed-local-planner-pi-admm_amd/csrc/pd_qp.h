@@ -1681,6 +1681,98 @@ __device__ __forceinline__ void pinv_row(const QP<NV>& P, int row, double sg, do
   }
 }
 
+// The pair's warm build split over two waves (r06): a helper wave computes each stored row's
+// P^-1 n (the Y column), A y and so the row's entries n_j' y against every earlier warm row, and
+// hands them over through a small LDS ring; the pair wave keeps only the S^-1 pass, the pivot and
+// the bordering.  The values are those the pair wave would compute itself (the same pinv_row and
+// A_mul, read through shuffles instead of the vb_ax buffer), so the build is bit-identical.
+// (LDS mode only, H <= WPIPE_HMAX: piadmm_internal.h; the ring follows S.sc)
+constexpr int WP_R = 3;                 // ring slots
+constexpr int WP_SLOT = 2 * 32 + 64 + 2;  // per slot: y (2 vehicles x H <= 32 lanes), n_j' y (64 rows), n_p' y_p, pad
+constexpr int WP_DBL = 4 + WP_R * WP_SLOT;  // g1, g2, the P^-1 pointer, pad, then the slots
+struct WarmPipe {
+  double* dat;     // LDS: WP_DBL doubles
+  int* hdr;        // LDS, after dat: [0] rows gm (0: no pipelined build this step), [1] rows
+                   // consumed, [2 .. 2 + WP_R) slot ready (row index + 1), [8 .. 72) the rows' codes
+};
+// The pair's stored active set as this step's warm rows: lane i gets the code of row i (-1: not
+// used) -- this step's set as stored, or the previous step's shifted one time slot.  Returns the
+// row count, 0 when there is no usable set.
+template <int NV>
+__device__ __forceinline__ int warm_codes(const QP<NV>& P, int& code) {
+  const int l = lid(), H = P.H;
+  code = -1;
+  const int gm = P.gws[0], gt = P.gws[1];
+  const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
+  if (!((same || prev) && gm > 0 && gm <= WAVE)) return 0;
+  code = (l < gm) ? P.gws[2 + l] : -1;
+  if (prev && code >= 0) {
+    const int row = code >> 1, s0 = row / H, k = row - s0 * H;
+    const bool keep = P.hinge(s0) ? (k >= 2) : (k >= 1);
+    code = keep ? 2 * (row - 1) + (code & 1) : -1;
+  }
+  // a kink held from its upper side (a linear row) restarts as the lower side (regimes
+  // start at zero; both sides are the same equality a'x = h)
+  if (code >= 0 && P.hinge((code >> 1) / H)) code &= ~1;
+  if (NV == 2 && P.g1 == 0.0 && P.g2 == 0.0 && code >= 0 && P.hinge((code >> 1) / H)) code = -1;
+  return gm;
+}
+
+// The helper wave's half of the pipelined warm build: rows 0 .. gm-1 of the codes the pair wave
+// published before the setup barrier, each into ring slot i % WP_R once the pair has taken row
+// i - WP_R out of it.  Every row is handed over (a row that is not appended just carries no data),
+// so both loops run exactly gm times.
+__device__ __forceinline__ void warm_help(const WarmPipe& wp, int H) {
+  const int gm = wp.hdr[0];
+  if (gm <= 0) return;
+  const int l = lid();
+  QP<2> Q;                          // the fields pinv_row and A_mul read
+  Q.H = H;
+  Q.n = 2 * H;
+  Q.g1 = wp.dat[0];
+  Q.g2 = wp.dat[1];
+  Q.Pinv = reinterpret_cast<const double*>(reinterpret_cast<const unsigned long long*>(wp.dat)[2]);
+  const int code = (l < gm) ? wp.hdr[8 + l] : -1;
+  const int rowj = code >= 0 ? code >> 1 : 0, sj = rowj / H, kj = rowj - sj * H;
+  const double sgj = (code & 1) ? -1.0 : 1.0;
+  for (int i = 0; i < gm; ++i) {
+    const int pc = rdli(code, i);
+    const int sl = i % WP_R;
+    if (i >= WP_R)
+      while (__hip_atomic_load(&wp.hdr[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < i + 1 - WP_R)
+        __builtin_amdgcn_s_sleep(1);
+    double* sd = wp.dat + 4 + sl * WP_SLOT;
+    if (pc >= 0) {
+      const int prow = pc >> 1;
+      const double sgp = (pc & 1) ? -1.0 : 1.0;
+      double yp[2], ay[QP<2>::NR];
+      pinv_row(Q, prow, sgp, yp);
+      A_mul(Q, yp, ay);
+      // (A y)[s H + k] is lane k's ay[s]: row j's entry n_j' y = sg_j (A y)[row_j], and the pivot's
+      // n_p' y_p = sg_p (A y)[row_p] -- the products prep and nvec form from the vb_ax buffer
+      double at[QP<2>::NR];
+#pragma unroll
+      for (int s = 0; s < QP<2>::NR; ++s) at[s] = __shfl(ay[s], kj);
+      double aj = at[0];
+#pragma unroll
+      for (int s = 1; s < QP<2>::NR; ++s)
+        if (sj == s) aj = at[s];
+      const int sp = prow / H, kp = prow - sp * H;
+      double ap = 0.0;
+#pragma unroll
+      for (int s = 0; s < QP<2>::NR; ++s)
+        if (sp == s) ap = __shfl(ay[s], kp);
+      if (l < 32)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) sd[v * 32 + l] = yp[v];   // (lanes >= H hold 0: H <= 32)
+      sd[64 + l] = sgj * aj;
+      if (l == 0) sd[128] = sgp * ap;
+    }
+    // (release: the slot's stores complete before the flag)
+    if (l == 0) __hip_atomic_store(&wp.hdr[2 + sl], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
 constexpr int GI_MAX_STEPS = 1024;   // a cold pair QP at H = 30 with most rows active takes ~300 adds + drops
 constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t, codes
 // Warm start (receding horizon): the previous MPC step's final active set, shifted one time
@@ -1698,7 +1790,7 @@ constexpr int GI_WS = 2 + WAVE;   // per-pair warm working set in HBM: m, step t
 template <int NV, int RM = 0>
 __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, signed char* lab, double* x, double* y,
                                          int& nsteps, signed char* flab = nullptr, bool use_wlab = true,
-                                         bool prebuild = false) {
+                                         bool prebuild = false, const WarmPipe* wp = nullptr) {
   // (prebuild: only append the pair's stored active set -- S^-1, the Y columns and the codes
   // depend on the step's geometry, not on q -- and return; the next solve of this QP starts from
   // it.  The pair wave does it while the agents' first x-steps run.)
@@ -1919,11 +2011,17 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
   auto warm_add = [&](int pc) {
     if (m >= cap) return;
     double yp[NV];
+    unsigned long long t_p = STAMP_T();
     const double spp = prep(pc, yp);
     const double va = nvec();
+    if (NV == 2) STAMP_ADD(ST_WARM_PREP, t_p);
+    unsigned long long t_s = STAMP_T();
     const double r = sinv_any<RS>(Si, ld, vbuf, va, m);
     const double delta = spp - wsum(va * r);
+    if (NV == 2) STAMP_ADD(ST_WARM_SINV, t_s);
+    unsigned long long t_a = STAMP_T();
     if (delta > DEP_TOL * spp) append(pc, yp, r, delta, 0.0);
+    if (NV == 2) STAMP_ADD(ST_WARM_APPEND, t_a);
     if (NV == 2) STAMP_CNT(ST_N_WARMROW, 1);
   };
   if (prebuild) {
@@ -1943,22 +2041,45 @@ __device__ __forceinline__ bool gi_solve(QP<NV>& P, const signed char* wlab, sig
     warm = true;
   } else if (P.gws && P.gws_warm) {
     // ---- pair: the stored active set (this step's, or the previous step's shifted)
-    const int gm = P.gws[0], gt = P.gws[1];
-    const bool same = gt == P.tstep, prev = gt == P.tstep - 1;
-    if ((same || prev) && gm > 0 && gm <= WAVE) {
-      int code = (l < gm) ? P.gws[2 + l] : -1;
-      if (prev && code >= 0) {
-        const int row = code >> 1, s0 = row / H, k = row - s0 * H;
-        const bool keep = P.hinge(s0) ? (k >= 2) : (k >= 1);
-        code = keep ? 2 * (row - 1) + (code & 1) : -1;
-      }
-      // a kink held from its upper side (a linear row) restarts as the lower side (regimes
-      // start at zero; both sides are the same equality a'x = h)
-      if (code >= 0 && P.hinge((code >> 1) / H)) code &= ~1;
-      if (NV == 2 && P.g1 == 0.0 && P.g2 == 0.0 && code >= 0 && P.hinge((code >> 1) / H)) code = -1;
-      for (int i = 0; i < gm; ++i) {
-        const int pc = rdli(code, i);
-        if (pc >= 0) warm_add(pc);
+    int code;
+    const int gm = warm_codes(P, code);
+    if (gm > 0) {
+      if (NV == 2 && wp && prebuild) {
+        // the helper wave's rows (WarmPipe): the same values warm_add's prep and nvec compute
+        int wj = 0;                                    // lane a < m: warm row index of active slot a
+        for (int i = 0; i < gm; ++i) {
+          const int pc = rdli(code, i);
+          const int sl = i % WP_R;
+          while (__hip_atomic_load(&wp->hdr[2 + sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != i + 1)
+            __builtin_amdgcn_s_sleep(1);
+          const double* sd = wp->dat + 4 + sl * WP_SLOT;
+          double yp[NV];
+#pragma unroll
+          for (int v = 0; v < NV; ++v) yp[v] = (l < 32) ? sd[v * 32 + l] : 0.0;
+          const double gl = sd[64 + l];
+          const double spp = sd[128];
+          const double gs = __shfl(gl, wj);
+          const double va = (l < m) ? gs : 0.0;          // n_a' y_p, a in the active set
+          // (release: the slot's loads are done before it is handed back)
+          if (l == 0) __hip_atomic_store(&wp->hdr[1], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (pc < 0 || m >= cap) continue;
+          unsigned long long t_s = STAMP_T();
+          const double r = sinv_any<RS>(Si, ld, vbuf, va, m);
+          const double delta = spp - wsum(va * r);
+          STAMP_ADD(ST_WARM_SINV, t_s);
+          unsigned long long t_a = STAMP_T();
+          if (delta > DEP_TOL * spp) {
+            if (l == m) wj = i;
+            append(pc, yp, r, delta, 0.0);
+          }
+          STAMP_ADD(ST_WARM_APPEND, t_a);
+          STAMP_CNT(ST_N_WARMROW, 1);
+        }
+      } else {
+        for (int i = 0; i < gm; ++i) {
+          const int pc = rdli(code, i);
+          if (pc >= 0) warm_add(pc);
+        }
       }
       warm = true;
     }

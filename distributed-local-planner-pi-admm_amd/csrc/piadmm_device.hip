@@ -21,12 +21,15 @@
 // tools/qp_sim.py and tools/gi_sim.py are the NumPy prototypes of this math.
 // Shared device code: pd_common.h (wave primitives, rollouts), pd_qp.h (QP solver), pd_setup.h.
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 #include <tuple>
 #include <vector>
 #include <algorithm>
 
 #include "pd_setup.h"
+
+static_assert(pd::WPIPE_WORDS == (size_t)pd::WP_DBL + 36, "the warm-row ring: lds_bytes and pd_qp.h WarmPipe agree");
 
 namespace pd {
 
@@ -57,6 +60,8 @@ struct StepCtx {
   WaveMem wm;
   bool spec;        // the speculative loop shape (agent_part)
   bool roll;        // speculative loop with the roller wave (roll_part): agent 1's rollout on wave RW
+  bool helper;      // wave RW also builds the pair's warm rows (pd_qp.h WarmPipe): LDS mode, H <= WPIPE_HMAX
+  WarmPipe wp;      // its LDS ring (after S.sc)
   int* vd;          // the pair wave's verdict on an iteration (speculative loop): act, stop, flag, aliased
   double* vdd;      // and dis_chk
   int* rflag;       // the roller's progress: it + 1 once agent 1's positions of iteration it are in LDS
@@ -796,6 +801,22 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
     // reduced solves before the ADMM fallback)
     STAMP_ADD(ST_SETUP_Z, t0);
   }
+  const bool prebuild = first && e >= 0 && qe.ycap > 0 && X.it0 < X.it_end;
+  if (X.helper) {
+    // the warm rows for the helper wave (every step: gm = 0 when there is no warm build)
+    int code = -1;
+    const int gm = (prebuild && qe.gws && qe.gws_warm) ? warm_codes(qe, code) : 0;
+    int* hd = X.wp.hdr;
+    if (l == 0) {
+      hd[0] = gm;
+      hd[1] = 0;
+      X.wp.dat[0] = qe.g1;
+      X.wp.dat[1] = qe.g2;
+      reinterpret_cast<unsigned long long*>(X.wp.dat)[2] = reinterpret_cast<unsigned long long>(qe.Pinv);
+    }
+    if (l < WP_R) hd[2 + l] = 0;
+    hd[8 + l] = code;
+  }
   __syncthreads();
 
   // speculative loop shape (agent_part): this wave also rolls the agents' controls out and
@@ -808,13 +829,13 @@ __device__ __forceinline__ void pair_part(const DevArgs& A, const StepCtx& X, Lo
   // the pair QP's first solve of the step goes straight to the dual active set from the stored
   // active set (no warm labels yet): append those rows now, while the agents solve their first
   // x-steps (they depend on the step's geometry only; setup_pair built it)
-  if (first && e >= 0 && qe.ycap > 0 && X.it0 < X.it_end) {
+  if (prebuild) {
     double xd[2];
     double yd[5];
     signed char ld[5];
     int nd = 0;
     unsigned long long t_pb = STAMP_T();
-    gi_solve<2, BIG ? RM_BIG : RM_S | RM_Y>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true);
+    gi_solve<2, BIG ? RM_BIG : RM_S | RM_Y>(qe, nullptr, ld, xd, yd, nd, nullptr, false, true, X.helper ? &X.wp : nullptr);
     STAMP_ADD(ST_ZR_SOLVE, t_pb);
   }
   bool resume = false;   // the compact loop ran barrier A, the rollouts and the test of iteration it
@@ -1166,6 +1187,7 @@ __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
   const double x0 = has ? S.xt[3] : 0.0, y0 = has ? S.xt[4] : 0.0, th0 = has ? S.xt[5] : 0.0;
   const bool nonlin_pos = c.pos_model != 0;
   __syncthreads();                                       // the parts' setup barrier
+  if (X.helper) warm_help(X.wp, H);                      // the pair's warm rows, before iteration it0's A
   for (int it = X.it0; it < X.it_end; ++it) {
     double* const pos = S.pos + (it & 1) * 4 * H1;
     unsigned long long t_sa = STAMP_T();
@@ -1188,6 +1210,31 @@ __device__ __forceinline__ void roll_part(const DevArgs& A, const StepCtx& X) {
     __syncthreads();                                     // B: the pair wave's verdict
     STAMP_ADD(ST_SYNC_B, t_sb);
     if (X.vd[1]) break;
+  }
+}
+
+// -------------------------------------------------------------------- the helper wave (plain shape)
+// The plain loop's fourth wave: the pair's warm rows at the step's start (pd_qp.h warm_help), then
+// the loop's barriers and decisions as the agent waves take them -- barrier A, the collision test,
+// barrier B after a z-step, the stop test (its grid barrier included) -- with no work of its own.
+template <bool TIES>
+__device__ __forceinline__ void help_part(const DevArgs& A, const StepCtx& X, LoopCtl& L, int& nbar) {
+  const piadmm_config_t& c = A.cfg;
+  const CompLds& S = X.S;
+  __syncthreads();                                       // the parts' setup barrier
+  warm_help(X.wp, X.H);
+  for (int it = X.it0; it < X.it_end; ++it) {
+    L.iters = it + 1;
+    double* const pos = S.pos + (it & 1) * 4 * X.H1;
+    __syncthreads();                                     // A
+    L.act = collide<TIES>(A, X, pos, it);
+    if (!L.act && L.flag == 0 && !c.fixed_iters && !X.global) {   // no edge ever: stop
+      L.stopped = true;
+      break;
+    }
+    L.flag = 1;
+    if (L.act) __syncthreads();                          // B
+    if (iter_tail<TIES>(A, X, L, it, nbar)) break;
   }
 }
 
@@ -1262,6 +1309,10 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   X.spec = SH == 1;
   // (launch_mpc_step: SH = 1 iff no in-kernel grid barrier, the nonlinear position model and no F_NOSPEC)
   X.roll = X.spec && blockDim.x == NWA * WAVE;   // launch_mpc_step adds the roller wave to this shape
+  // the fourth wave also builds the pair's warm rows where its LDS ring fits (lds_bytes)
+  X.helper = !BIG && H <= WPIPE_HMAX && blockDim.x == NWA * WAVE && !(flags & F_NOHELPER);
+  X.wp.dat = S.sc + 32;
+  X.wp.hdr = reinterpret_cast<int*>(X.wp.dat + WP_DBL);
   X.it0 = it0;
   const bool first = X.first;
   // a component whose step already ended in an earlier launch of this step (per-component stop,
@@ -1337,6 +1388,7 @@ __device__ __forceinline__ void mpc_step_body(const DevArgs& A, int t, int it0, 
   if (X.w < NW) agent_part<BIG, TIES, SH>(A, X, L, nbar, n);
   else if (X.w == PW) pair_part<BIG, TIES, SH>(A, X, L, nbar, n);
   else if constexpr (SH == 1) roll_part(A, X);
+  else help_part<TIES>(A, X, L, nbar);
   __syncthreads();
   STAMP_ADD(ST_KERNEL, t_k);
   unsigned long long t_epi = STAMP_T();
@@ -1551,6 +1603,12 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
 #endif
   const void* fn = mpc_fn(big, a.tie_on != 0, spec);
   if (set_dyn_lds(fn, sh) != 0) return -1;
+  // the fourth wave: the speculative shape's roller, and in LDS mode up to WPIPE_HMAX the helper
+  // that builds the pair's warm rows beside it (both shapes; PIADMM_NO_HELPER=1 leaves it out)
+  const char* nh = std::getenv("PIADMM_NO_HELPER");     // (read per launch: the tests' A/B toggles it)
+  const bool no_helper = nh && nh[0] == '1';
+  if (no_helper) flags |= F_NOHELPER;
+  const bool helper = !big && a.cfg.H <= WPIPE_HMAX && !no_helper;
   if (flags & F_COOP) {
     // every workgroup must be resident for the grid barrier: the cooperative launch fails
     // (and the caller falls back to host-decided termination) rather than deadlock
@@ -1558,7 +1616,7 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     aa.gbar_base = launch_coop_epoch(nsteps, a.cfg.max_outer);
     void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
     (void)hipGetLastError();
-    return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3(NWT * WAVE), args, (unsigned)sh, s));
+    return launch_rc(hipLaunchCooperativeKernel(fn, dim3(a.C), dim3((helper ? NWA : NWT) * WAVE), args, (unsigned)sh, s));
   }
   (void)hipGetLastError();   // a stale error of an earlier runtime call is not this launch's
   // the speculative loop runs with the roller wave; PIADMM_NO_ROLLER=1 keeps three waves (the pair
@@ -1567,7 +1625,7 @@ int launch_mpc_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int f
     const char* e = std::getenv("PIADMM_NO_ROLLER");
     return e && e[0] == '1';
   }();
-  const int nt = (spec && !no_roller ? NWA : NWT) * WAVE;
+  const int nt = ((spec ? !no_roller : helper) ? NWA : NWT) * WAVE;
   DevArgs aa = a;
   void* args[] = {&aa, &t, &nsteps, &it0, &it1, &flags};
   return launch_rc(hipLaunchKernel(fn, dim3(a.C), dim3(nt), args, sh, s));
@@ -1589,7 +1647,7 @@ bool coop_fits(const DevArgs& a, int device) {
   const bool big = a.cfg.H > HMAX;
   const void* fn = mpc_fn(big, a.tie_on != 0, false);   // (the cooperative launch runs the plain shape)
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NWT * WAVE, sh) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, NWA * WAVE, sh) != hipSuccess) return false;
   return (long long)per * ncu >= (long long)a.C;
 }
 

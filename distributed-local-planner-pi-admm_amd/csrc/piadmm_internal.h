@@ -182,6 +182,11 @@ constexpr size_t MAX_LDS = 160 * 1024;
 constexpr size_t kxf_stride(int H) { return ((size_t)H * H + 1) & ~(size_t)1; }
 constexpr size_t kxf_words(int H) { return kxf_stride(H); }
 
+// The pair's warm build on two waves (pd_qp.h WarmPipe): its LDS ring (4 + 3 x 130 doubles, then
+// 72 ints) after the scalars, in LDS mode up to H = 30 (at H = 31, 32 the workgroup would exceed
+// 160 KB; there the pair wave builds alone).
+constexpr int WPIPE_HMAX = 30;
+constexpr size_t WPIPE_WORDS = 4 + 3 * 130 + 36;
 // LDS bytes needed by one workgroup for horizon H (must match the carve in k_mpc_step).
 // LDS mode (H <= HMAX): every matrix of the component in LDS.  Big mode: agent K_s^-1, G and
 // X' and the pair K_s^-1 in HBM / L2; LDS keeps the factor scratches and the vectors.
@@ -207,6 +212,7 @@ inline size_t lds_bytes(int H, int precision = 0) {
   d += 2 * 3 + 2 * 2 + 4 * H;      // xt, seeds, u (two buffers: outer-iteration parity)
   d += 5 * 2 * 2 * H1;             // hat, lam, S, D, last_hat
   d += 32;                         // scalars
+  if (H <= WPIPE_HMAX) d += WPIPE_WORDS;   // the helper wave's warm-row ring (pd_qp.h WarmPipe)
   if (H > HMAX && f32) d += 2 * (size_t)H * H + 2;   // big mode: fp32 image of the pair K_s^-1
   return d * sizeof(double);
 }
@@ -262,6 +268,8 @@ constexpr int F_INITONLY = 256;
 // k_mpc_step: the plain loop shape even where the speculative one would run (PIADMM_NO_SPEC=1; the
 // equality test of the two shapes, tests/test_gpu_modes.py)
 constexpr int F_NOSPEC = 512;
+// k_mpc_step: the pair wave builds its warm rows alone (PIADMM_NO_HELPER=1: the helper wave's A/B)
+constexpr int F_NOHELPER = 1024;
 
 int launch_graph_step(const DevArgs& a, int t, int nsteps, int it0, int it1, int flags, hipStream_t s);
 // The epoch base of a cooperative launch of nsteps MPC steps: larger than every epoch an earlier

@@ -292,3 +292,41 @@ def test_speculative_loop_equals_plain_loop(Solver, monkeypatch, case):
         assert ca["inexact"] > 0                 # the uncertified path is exercised
     else:
         assert ca["inexact"] == 0
+
+
+@pytest.mark.parametrize("case", ["bench_fixed", "natural", "smoke_natural", "linear_natural", "smoke_job"])
+def test_warm_helper_equals_pair_alone(Solver, monkeypatch, case):
+    """The pair's warm build on two waves (the helper wave computes each stored row's P^-1 n, A y
+    and its products with the earlier rows, pd_qp.h WarmPipe) against the pair wave alone
+    (PIADMM_NO_HELPER=1): the helper hands over the values the pair wave would compute itself, so
+    every output, residual history, iteration count and work counter is bit-identical.  Cases: the
+    bench's tiles (fixed 100 iterations, the speculative shape's roller as the helper), natural
+    global termination (the plain shape's fourth wave, cooperative launch), a small job under it,
+    the linearised position model, and smoke()'s own job (per-component stop)."""
+    H = {"bench_fixed": 30, "smoke_natural": 10, "linear_natural": 20, "smoke_job": 10}.get(case, 15)
+    kw = dict(H=H)
+    if case == "bench_fixed":
+        kw.update(fixed_iters=1, term_global=1)
+    elif case != "smoke_job":
+        kw.update(term_global=1)
+    cfg = (config.casadi_default if case == "linear_natural" else config.matlab_pi)(**kw)
+    n_tiles, n_steps = {"bench_fixed": (32, 6), "smoke_natural": (2, 20), "smoke_job": (2, 30)}.get(case, (16, 12))
+    if case == "smoke_job":   # __graft_entry__.smoke()'s job: per-component stop (the speculative shape)
+        scn = scenario.tiled(2, 10, n_steps=30, seed=1)
+    else:
+        scn = scenario.tiled(n_tiles, H, n_steps=n_steps + 2, seed=7)
+    runs = []
+    for nh in ("0", "1"):
+        monkeypatch.setenv("PIADMM_NO_HELPER", nh)
+        with Solver(cfg, scn) as s:
+            recs = [s.mpc_step() for _ in range(n_steps)]
+            runs.append((recs, s.counters(), s.state()))
+    (ra, ca, sa), (rb, cb, sb) = runs
+    for k, (a, b) in enumerate(zip(ra, rb)):
+        for f in ("iters", "status", "xt", "u"):
+            np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f"{f} at step {k}")
+        np.testing.assert_array_equal(np.nan_to_num(a.resid, nan=-1.0), np.nan_to_num(b.resid, nan=-1.0))
+    for f in ("pos_old", "hat", "lam", "S", "D"):
+        np.testing.assert_array_equal(sa[f], sb[f], err_msg=f)
+    assert ca == cb
+    assert ca["z_qps"] > 0

@@ -49,3 +49,9 @@ print("  %-12s" % "phase" + "".join("%14s" % w for w in ("agent0", "agent1", "pa
 for i, n in enumerate(NAMES):
     if np.any(sw[:, i] > 0):
         print("  %-12s" % n + "".join("%14.0f" % sw[w, i] for w in range(4)))
+# the pair's warm build per appended row (slots 56-58) and the rows appended (slot 51)
+rows = st[:, 51].mean() / steps
+print("warm build detail (pair wave, mean per component and step): rows %.1f" % rows)
+for i, n in ((56, "prep (P^-1 n, A y, N'y)"), (57, "S^-1 v + pivot"), (58, "bordering")):
+    v = st[:, i].mean() / steps
+    print("  %-24s %10.0f cycles  (%6.0f per row)" % (n, v, v / max(rows, 1e-9)))
